@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident validate+index of a synthetic 4 KiB-entry
+store (BASELINE.json metric "GiB/s hashed (device-resident), full-file
+validate+index scan"), N=1 workload = configs[1] (1M x 4 KiB, 4.06 GiB).
+
+One step = one full srd_validate_index_device() pass over the store already
+resident in HBM: chain recovery (recover_valid_chain), CRC-32 of every chain
+payload + compare (is_valid_checksum), and the latest-wins index rebuild
+(KeyIndexer::build).  value = algorithmic bytes sum(payload_len + 20) over all
+ranks / max-over-ranks wall time of K steps.
+
+N>1 (torchrun): each rank validates its own store of --entries-per-gpu entries
+on its GPU (weak scaling, no data-path collective); only the step timing is
+reduced (MAX) over ranks.
+
+Also prints: roofline of the dominant kernel (scan_kernel, HIP events on the
+library's stream) and a CPU baseline (oracle/, the C restatement of the
+reference path, timed on this host on rank 0 at N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rust-simd-r-drive_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import srd_amd as S  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(n_entries: int, payload: int) -> int:
+    return n_entries * (payload + 20)  # sum(L_i + 20)
+
+
+def cpu_baseline(store_dev: torch.Tensor, size: int, bytes_alg: int, budget_s: float):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # the checker / CPU restatement (test infrastructure)
+
+    host = store_dev[:size].cpu().numpy()
+    O.validate_index(host[: min(size, 1 << 26)], 1)  # warm the page cache / tables
+    res = {}
+    for threads in (1, os.cpu_count() or 1):
+        threads = min(threads, 16)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            st = O.validate_index(host, threads)
+            reps += 1
+            if time.perf_counter() - t0 > budget_s / 2 or reps >= 5:
+                break
+        dt = (time.perf_counter() - t0) / reps
+        res[threads] = (bytes_alg / dt / 2**30, st, dt)
+    one = res[1]
+    allc = max(k for k in res)
+    return {
+        "value": round(one[0], 3),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"full C2 store ({size} B), oracle/srd_oracle.c faithful single-thread open()+"
+        f"is_valid_checksum per chain entry (PCLMUL CRC), {one[2]*1e3:.1f} ms/pass",
+        "all_cores": {"value": round(res[allc][0], 3), "cores": allc, "ms_per_pass": round(res[allc][2] * 1e3, 2)},
+        "check": {"final_len": one[1].final_len, "n_chain": one[1].n_chain, "n_index": one[1].n_index},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--entries-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--payload", type=int, default=4096)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--e2e", action="store_true", help="also time host->HBM->result end to end (stderr)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    ctx = S.Context(local)
+
+    n, L = args.entries_per_gpu, args.payload
+    size = S.synth_store_len(n, L)
+    store = torch.empty(size + 4096, dtype=torch.uint8, device=f"cuda:{local}")
+    S.synth_store_device(store.data_ptr(), n, L, ctx=ctx)
+    torch.cuda.synchronize()
+    bytes_alg = algorithmic_bytes(n, L)
+
+    def step():
+        return S.validate_index_device(store.data_ptr(), size, 0, ctx)
+
+    for _ in range(args.warmup):
+        r = step()
+    assert r.final_len == size and r.n_chain == n and r.n_crc_bad == 0 and r.n_index == n, (
+        r.final_len, r.n_chain, r.n_crc_bad, r.n_index)
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    scan_ms_sum, scan_n = 0.0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        sm, sn, _ = ctx.timings()
+        scan_ms_sum += sm
+        scan_n += sn
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    ms_per_step = dt / args.steps * 1e3
+    value = bytes_alg * world / dt * args.steps / 2**30
+    scan_ms = scan_ms_sum / max(scan_n, 1)
+    achieved = bytes_alg / (scan_ms * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get("scan_kernel_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "GiB/s hashed (device-resident), full-file validate+index scan",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (counter-mode splitmix64 payloads, keys bench-key-{i}), generated in HBM",
+        "config": {
+            "workload": f"C2: {n} x {L} B entries, {size} B store per GPU, validate+index "
+                        f"(recover_valid_chain + CRC-32 every payload + KeyIndexer::build)",
+            "entries_per_gpu": n,
+            "payload_bytes": L,
+            "store_bytes_per_gpu": size,
+            "algorithmic_bytes_per_gpu": bytes_alg,
+            "parallelism": f"{world} independent GPU stores (entry-range shards), no collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "scan_kernel<false>",
+            "kernel_ms": round(scan_ms, 4),
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(store, size, bytes_alg, args.cpu_budget)
+    if args.e2e and rank == 0:
+        host = torch.empty(size, dtype=torch.uint8).pin_memory()
+        host.copy_(store[:size])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            res = S.validate_index(host.numpy(), 0, ctx)
+        e2e = (time.perf_counter() - t0) / 3
+        print(json.dumps({"e2e_host_to_index_ms": round(e2e * 1e3, 2),
+                          "e2e_GiBps": round(bytes_alg / e2e / 2**30, 3),
+                          "final_len": res.final_len}), file=sys.stderr)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/*
+ * srd_amd.h -- C ABI of the MI355X-native open-time hot path of SIMD R Drive
+ * (jzombie/rust-simd-r-drive v0.16.3-alpha): validation-chain recovery,
+ * per-payload IEEE CRC-32 check, and the latest-wins key-index rebuild,
+ * plus the batch digest entry points.
+ *
+ * Plain pointers and sizes only (no torch / HIP types).  `stream` arguments
+ * are `hipStream_t` passed as `void*` (NULL = the context's own stream).
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to the reference repo root):
+ *
+ *   srd_recover_valid_chain   <- DataStore::recover_valid_chain
+ *                                src/storage_engine/data_store.rs:383-482
+ *   srd_key_indexer_build     <- KeyIndexer::build
+ *                                src/storage_engine/key_indexer.rs:98-124
+ *   srd_validate_index(_device) <- the two calls inside DataStore::open
+ *                                (data_store.rs:89 and :108) fused with
+ *                                EntryHandle::is_valid_checksum
+ *                                (simd-r-drive-entry-handle/src/entry_handle.rs:260-275)
+ *                                over every chain entry
+ *   srd_crc32_batch(_device)  <- compute_checksum
+ *                                src/storage_engine/digest/compute_checksum.rs:15-20
+ *   srd_xxh3_64_batch(_device) <- compute_hash_batch
+ *                                src/storage_engine/digest/compute_hash.rs:64-77
+ *   srd_xxh3_64               <- compute_hash  (compute_hash.rs:25-27)
+ *
+ * Semantics (bit-exact with the reference):
+ *   - final_len = largest tail t <= file_len whose backward chain is
+ *     structurally valid down to offset 0 (0 if none), exactly as the
+ *     reference's byte-wise outer loop finds it.
+ *   - chain = entries of the chain ending at final_len, in file order.
+ *   - crc_computed = IEEE CRC-32 (crc32fast) of each chain payload;
+ *     crc_ok = (crc_computed == stored little-endian checksum).
+ *   - index = key_hash -> pack(tag16 = key_hash >> 48, meta_off48), latest
+ *     entry per key_hash wins, tombstones INCLUDED (as KeyIndexer::build).
+ * Errors: 0 = ok; negative = HIP / allocation / argument error
+ * (srd_last_error() has the message).  Invalid chains and bad CRCs are
+ * data, never errors.  Arithmetic on offsets wraps like release-mode Rust.
+ */
+#ifndef SRD_AMD_H
+#define SRD_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRD_OK 0
+#define SRD_ERR_HIP (-1)
+#define SRD_ERR_ALLOC (-2)
+#define SRD_ERR_ARG (-3)
+#define SRD_ERR_INTERNAL (-4)
+
+/* option flags */
+#define SRD_FLAG_FORCE_FULL 1u   /* skip the optimistic (strong-candidate) pass */
+#define SRD_FLAG_NO_CRC 2u       /* structural recovery + index only */
+
+typedef struct srd_ctx srd_ctx; /* one device + stream + reusable workspace */
+
+int srd_ctx_create(int device, srd_ctx **out);
+void srd_ctx_destroy(srd_ctx *ctx);
+/* The HIP stream the context launches on (hipStream_t as void*). */
+void *srd_ctx_stream(srd_ctx *ctx);
+const char *srd_last_error(void);
+/* HIP-event timings of the last srd_validate_index(_device) call on ctx,
+ * measured on the context stream: summed duration of the streaming scan
+ * kernel launches (ms), their count, and the device span of the whole call. */
+int srd_ctx_timings(srd_ctx *ctx, double *scan_ms, int *scan_launches,
+                    double *total_ms);
+
+/* Result of one validate+index pass whose arrays live in DEVICE memory owned
+ * by the context (valid until the next call on the same ctx). */
+typedef struct {
+  uint64_t file_len;
+  uint64_t final_len;      /* recover_valid_chain */
+  uint64_t n_chain;        /* entries on the chain ending at final_len */
+  uint64_t n_index;        /* KeyIndexer entries */
+  uint64_t n_crc_bad;      /* chain entries whose CRC does not match */
+  uint64_t n_candidates;   /* chain-node candidates recorded by the scan */
+  uint64_t n_weak;         /* candidates skipped by the optimistic pass */
+  uint32_t mode;           /* 0 = optimistic pass sufficed, 1 = full pass */
+  uint32_t reserved;
+  /* chain, file order; device pointers */
+  uint64_t *meta_off, *key_hash, *prev_offset, *payload_start, *payload_len;
+  uint32_t *crc_stored, *crc_computed;
+  uint8_t *crc_ok;
+  /* index (chain order of the latest entry per key); device pointers */
+  uint64_t *index_key_hash, *index_packed;
+} srd_device_result;
+
+/* Device-resident validate+index over `file_len` bytes at `d_file`
+ * (device pointer; the bytes are the mmap'd store). */
+int srd_validate_index_device(srd_ctx *ctx, const uint8_t *d_file,
+                              uint64_t file_len, uint32_t flags,
+                              srd_device_result *out);
+
+/* Same result with host-memory arrays (malloc'd; free with srd_result_free).
+ * `file` is host memory (e.g. the mmap); it is staged to HBM inside. */
+typedef srd_device_result srd_result;
+int srd_validate_index(srd_ctx *ctx, const uint8_t *file, uint64_t file_len,
+                       uint32_t flags, srd_result *out);
+void srd_result_free(srd_result *res);
+
+/* recover_valid_chain: final_len only (host input). */
+int srd_recover_valid_chain(srd_ctx *ctx, const uint8_t *file,
+                            uint64_t file_len, uint64_t *final_len);
+
+/* KeyIndexer::build over the chain ending at `tail` (host input).  Writes up
+ * to `cap` pairs; *n_out = number of index entries. */
+int srd_key_indexer_build(srd_ctx *ctx, const uint8_t *file, uint64_t tail,
+                          uint64_t *key_hash_out, uint64_t *packed_out,
+                          uint64_t cap, uint64_t *n_out);
+
+/* CRC-32 (crc32fast) of n byte ranges [offs[i], offs[i]+lens[i]) of buf. */
+int srd_crc32_batch(srd_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
+                    const uint64_t *offs, const uint64_t *lens, uint64_t n,
+                    uint32_t *out);
+int srd_crc32_batch_device(srd_ctx *ctx, const uint8_t *d_buf,
+                           const uint64_t *d_offs, const uint64_t *d_lens,
+                           uint64_t n, uint32_t *d_out, void *stream);
+
+/* XXH3-64 (seed 0, default secret) of n keys [offs[i], offs[i]+lens[i]). */
+int srd_xxh3_64_batch(srd_ctx *ctx, const uint8_t *keys, uint64_t keys_len,
+                      const uint64_t *offs, const uint64_t *lens, uint64_t n,
+                      uint64_t *out);
+int srd_xxh3_64_batch_device(srd_ctx *ctx, const uint8_t *d_keys,
+                             const uint64_t *d_offs, const uint64_t *d_lens,
+                             uint64_t n, uint64_t *d_out, void *stream);
+
+/* Synthetic store of the BASELINE configs written on the device (the
+ * checksum-on-append writer of data_store.rs:847-939 for keys
+ * "bench-key-{i}" and counter-mode splitmix64 payloads).  lens==NULL ->
+ * every payload is fixed_len bytes.  Returns the file length in *len_out;
+ * d_out==NULL only computes the length. */
+int srd_synth_store_device(srd_ctx *ctx, uint8_t *d_out, uint64_t n_entries,
+                           uint64_t fixed_len, const uint64_t *lens,
+                           uint64_t seed, uint64_t *len_out);
+
+/* Library self-test of the CRC algebra tables (host only, no GPU). */
+int srd_selftest_host(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

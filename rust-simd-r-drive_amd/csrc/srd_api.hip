@@ -1,0 +1,838 @@
+// srd_api.hip -- host orchestration + C ABI (include/srd_amd.h).
+//
+// One translation unit with the kernels (device globals live here).
+// Glue scans/compactions use hipCUB (library primitives, like calling
+// rocBLAS for a plain GEMM); every byte-touching hot kernel is hand-written
+// in srd_kernels.hip.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "srd_amd.h"
+#include "srd_kernels.hip"
+
+using namespace srd;
+
+static thread_local std::string g_err;
+static void set_err(const std::string& s) { g_err = s; }
+extern "C" const char* srd_last_error(void) { return g_err.c_str(); }
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      set_err(std::string(#x) + ": " + hipGetErrorString(e_));                            \
+      return SRD_ERR_HIP;                                                                 \
+    }                                                                                     \
+  } while (0)
+
+namespace {
+
+struct Buf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::vector<Buf> bufs;  // indexed by the enum below
+  uint32_t cap = 256;     // candidate slots per span
+  srd_device_result res{};
+  // host-input staging
+  Buf file;
+  // timing (HIP events on `stream`)
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double scan_ms = 0, total_ms = 0;
+  int scan_launches = 0;
+};
+
+enum BufId {
+  B_TILE_T, B_TILE_SX1, B_SPAN_COUNT, B_SPAN_BASE,
+  B_CM, B_CP, B_CKH, B_CCRC, B_CSXM, B_CSUF, B_CTAIL, B_CFLAGS,
+  B_COUNTERS,  // [0]=max_root [1]=n_weak [2]=overflow [3]=best_g1 [4]=changed [5]=n_slow [6]=n_bad [7]=special
+  B_DM, B_DPAR, B_DSLOT, B_DHEAD, B_RUNHEAD, B_INTS, B_WALK,
+  B_ST, B_JMP, B_VFLAG, B_VLIST, B_NV, B_VPOS, B_VPAR, B_VHEAD, B_VSLOT,
+  B_ONPATH, B_CPOS, B_CHAIN_G, B_CORE,
+  B_O_MO, B_O_KH, B_O_PREV, B_O_START, B_O_LEN, B_O_CRCST, B_O_CRC, B_O_OK,
+  B_O_PIECES, B_O_SUF, B_O_SXM, B_O_TAIL, B_SLOW,
+  B_HKEYS, B_HVALS, B_LATEST, B_IPOS, B_IKEY, B_IPACKED,
+  B_CUB_TMP,
+  B_COUNT_
+};
+
+int ensure(Ctx* c, BufId id, size_t bytes) {
+  Buf& b = c->bufs[id];
+  if (b.n >= bytes && b.p) return 0;
+  if (b.p) HIPCHK(hipFree(b.p));
+  b.p = nullptr;
+  b.n = 0;
+  size_t want = std::max<size_t>(bytes, 256);
+  if (hipMalloc(&b.p, want) != hipSuccess) {
+    set_err("hipMalloc failed for " + std::to_string(want) + " bytes");
+    b.p = nullptr;
+    return SRD_ERR_ALLOC;
+  }
+  b.n = want;
+  return 0;
+}
+template <class T>
+T* P(Ctx* c, BufId id) { return (T*)c->bufs[id].p; }
+
+std::once_flag g_tab_once;
+CrcTables g_host_tabs;
+
+int upload_tables() {
+  static int rc = 1;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  std::call_once(g_tab_once, [] { build_crc_tables(g_host_tabs); });
+  // per device upload
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  static uint64_t uploaded = 0;
+  if (uploaded & (1ull << dev)) return 0;
+  DevTables t;
+  memcpy(t.tab, g_host_tabs.tab, sizeof t.tab);
+  memcpy(t.lw, g_host_tabs.lw, sizeof t.lw);
+  memcpy(t.winit, g_host_tabs.winit, sizeof t.winit);
+  memcpy(t.zero_crc, g_host_tabs.zero_crc, sizeof t.zero_crc);
+  t.x32768 = g_host_tabs.x32768;
+  memcpy(t.pow8, g_host_tabs.pow8, sizeof t.pow8);
+  memcpy(t.invpow, g_host_tabs.invpow, sizeof t.invpow);
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_tabs), &t, sizeof t));
+  uploaded |= 1ull << dev;
+  (void)rc;
+  return 0;
+}
+
+inline unsigned blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+#define TRY(x)                 \
+  do {                         \
+    int r_ = (x);              \
+    if (r_) return r_;         \
+  } while (0)
+
+// hipCUB temp size for all glue ops up to n elements
+int ensure_cub(Ctx* c, uint64_t n) {
+  size_t t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
+  int nn = (int)std::min<uint64_t>(n + 1, 0x7fffffff);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (uint32_t*)nullptr, (uint64_t*)nullptr, nn);
+  hipcub::DeviceScan::InclusiveScan(nullptr, t2, (uint64_t*)nullptr, (uint64_t*)nullptr, hipcub::Max(), nn);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, t3, (uint32_t*)nullptr, (uint32_t*)nullptr, nn);
+  hipcub::DeviceSelect::Flagged(nullptr, t4, hipcub::CountingInputIterator<uint64_t>(0), (uint32_t*)nullptr,
+                                (uint64_t*)nullptr, (uint64_t*)nullptr, nn);
+  t5 = std::max(std::max(t1, t2), std::max(t3, t4));
+  return ensure(c, B_CUB_TMP, t5 + 256);
+}
+
+int read_counters(Ctx* c, uint64_t* h) {
+  HIPCHK(hipMemcpyAsync(h, P<uint64_t>(c, B_COUNTERS), 8 * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// walk state (start) must already be on the device
+int walk_and_mark(Ctx* c, const int64_t* par, const uint64_t* slot, uint64_t n, const uint64_t* map,
+                  WalkState* hws) {
+  WalkState* ws = P<WalkState>(c, B_WALK);
+  uint8_t* core = P<uint8_t>(c, B_CORE);
+  uint64_t* key = P<uint64_t>(c, B_DHEAD);
+  HIPCHK(hipMemsetAsync(core, 0, n, c->stream));
+  child_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(par, n, core);
+  core_key_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(core, ws, n, key);
+  size_t tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint64_t>(c, B_RUNHEAD),
+                                           hipcub::Max(), (int)n, c->stream));
+  head_key_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(core, par, P<uint64_t>(c, B_RUNHEAD), n, key);
+  tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint64_t>(c, B_RUNHEAD),
+                                           hipcub::Max(), (int)n, c->stream));
+  walk_kernel<<<1, 64, 0, c->stream>>>(par, P<uint64_t>(c, B_RUNHEAD), slot, P<uint64_t>(c, B_CP),
+                                       P<uint64_t>(c, B_INTS), ws, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(hws, ws, sizeof(WalkState), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (hws->status != 1) return 0;
+  mark_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_INTS), ws, n, core,
+                                                     P<uint32_t>(c, B_ONPATH));
+  HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_ONPATH) + n, 0, 4, c->stream));
+  tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_ONPATH),
+                                          P<uint32_t>(c, B_CPOS), (int)(n + 1), c->stream));
+  scatter_chain_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint32_t>(c, B_ONPATH), P<uint32_t>(c, B_CPOS), n,
+                                                              map, P<uint64_t>(c, B_CHAIN_G));
+  HIPCHK(hipGetLastError());
+  uint32_t on = 0;
+  HIPCHK(hipMemcpyAsync(&on, P<uint32_t>(c, B_CPOS) + n, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  hws->chain_len = 1 + (uint64_t)on;
+  return 0;
+}
+
+}  // namespace
+
+struct srd_ctx : Ctx {};
+
+extern "C" int srd_ctx_create(int device, srd_ctx** out) {
+  if (!out) { set_err("null out"); return SRD_ERR_ARG; }
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) { set_err("bad device index"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(device));
+  auto* c = new srd_ctx();
+  c->device = device;
+  c->bufs.resize(B_COUNT_);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    set_err("hipStreamCreate failed");
+    return SRD_ERR_HIP;
+  }
+  int r = upload_tables();
+  if (r) { delete c; return r; }
+  for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+  *out = c;
+  return 0;
+}
+
+extern "C" void srd_ctx_destroy(srd_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  for (auto& b : c->bufs)
+    if (b.p) hipFree(b.p);
+  if (c->file.p) hipFree(c->file.p);
+  for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" void* srd_ctx_stream(srd_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+static int alloc_scan(Ctx* c, uint64_t n_tiles, uint64_t n_spans) {
+  const uint64_t slots = n_spans * c->cap;
+  TRY(ensure(c, B_TILE_T, n_tiles * 4));
+  TRY(ensure(c, B_TILE_SX1, n_tiles * 4));
+  TRY(ensure(c, B_SPAN_COUNT, (n_spans + 1) * 4));
+  TRY(ensure(c, B_SPAN_BASE, (n_spans + 1) * 8));
+  TRY(ensure(c, B_CM, slots * 8));
+  TRY(ensure(c, B_CP, slots * 8));
+  TRY(ensure(c, B_CKH, slots * 8));
+  TRY(ensure(c, B_CCRC, slots * 4));
+  TRY(ensure(c, B_CSXM, slots * 4));
+  TRY(ensure(c, B_CSUF, slots * 4));
+  TRY(ensure(c, B_CTAIL, slots * 4));
+  TRY(ensure(c, B_CFLAGS, slots * 4));
+  TRY(ensure(c, B_COUNTERS, 8 * 8));
+  TRY(ensure(c, B_WALK, sizeof(WalkState)));
+  return 0;
+}
+
+static int alloc_dense(Ctx* c, uint64_t K) {
+  TRY(ensure(c, B_DM, K * 8));
+  TRY(ensure(c, B_DPAR, K * 8));
+  TRY(ensure(c, B_DSLOT, K * 8));
+  TRY(ensure(c, B_DHEAD, K * 8));
+  TRY(ensure(c, B_RUNHEAD, K * 8));
+  TRY(ensure(c, B_INTS, K * 16 + 16));
+  TRY(ensure(c, B_ONPATH, (K + 1) * 4));
+  TRY(ensure(c, B_CPOS, (K + 1) * 4));
+  TRY(ensure(c, B_CHAIN_G, (K + 1) * 8));
+  TRY(ensure(c, B_CORE, K + 1));
+  TRY(ensure_cub(c, K + 1));
+  return 0;
+}
+
+static int alloc_out(Ctx* c, uint64_t n) {
+  TRY(ensure(c, B_O_MO, n * 8));
+  TRY(ensure(c, B_O_KH, n * 8));
+  TRY(ensure(c, B_O_PREV, n * 8));
+  TRY(ensure(c, B_O_START, n * 8));
+  TRY(ensure(c, B_O_LEN, n * 8));
+  TRY(ensure(c, B_O_CRCST, n * 4));
+  TRY(ensure(c, B_O_CRC, n * 4));
+  TRY(ensure(c, B_O_OK, n));
+  TRY(ensure(c, B_O_PIECES, n * 4));
+  TRY(ensure(c, B_O_SUF, n * 4));
+  TRY(ensure(c, B_O_SXM, n * 4));
+  TRY(ensure(c, B_O_TAIL, n * 4));
+  TRY(ensure(c, B_SLOW, n * 8));
+  uint64_t hc = 64;
+  while (hc < 2 * n) hc <<= 1;
+  TRY(ensure(c, B_HKEYS, hc * 8));
+  TRY(ensure(c, B_HVALS, hc * 8));
+  TRY(ensure(c, B_LATEST, (n + 1) * 4));
+  TRY(ensure(c, B_IPOS, (n + 1) * 4));
+  TRY(ensure(c, B_IKEY, n * 8));
+  TRY(ensure(c, B_IPACKED, n * 8));
+  TRY(ensure_cub(c, n + 1));
+  return 0;
+}
+
+// finalize + index for a chain of n entries whose chain_g / walk state are set
+static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint32_t flags,
+                  srd_device_result* out) {
+  TRY(alloc_out(c, n));
+  uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
+  HIPCHK(hipMemsetAsync(cnt + 5, 0, 16, c->stream));  // n_slow, n_bad
+  FinArgs f{};
+  f.file = d_file;
+  f.flen = flen;
+  f.n_chain = n;
+  f.chain_g = P<uint64_t>(c, B_CHAIN_G);
+  f.slot = P<uint64_t>(c, B_DSLOT);
+  f.par = P<int64_t>(c, B_DPAR);
+  f.ws = P<WalkState>(c, B_WALK);
+  f.c_m = P<uint64_t>(c, B_CM);
+  f.c_p = P<uint64_t>(c, B_CP);
+  f.c_kh = P<uint64_t>(c, B_CKH);
+  f.c_crc = P<uint32_t>(c, B_CCRC);
+  f.c_sxm = P<uint32_t>(c, B_CSXM);
+  f.c_suf = P<uint32_t>(c, B_CSUF);
+  f.c_tail = P<uint32_t>(c, B_CTAIL);
+  f.c_flags = P<uint32_t>(c, B_CFLAGS);
+  f.tileT = P<uint32_t>(c, B_TILE_T);
+  f.tileSX1 = P<uint32_t>(c, B_TILE_SX1);
+  f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
+  f.o_mo = P<uint64_t>(c, B_O_MO);
+  f.o_kh = P<uint64_t>(c, B_O_KH);
+  f.o_prev = P<uint64_t>(c, B_O_PREV);
+  f.o_start = P<uint64_t>(c, B_O_START);
+  f.o_len = P<uint64_t>(c, B_O_LEN);
+  f.o_crc_st = P<uint32_t>(c, B_O_CRCST);
+  f.o_crc = P<uint32_t>(c, B_O_CRC);
+  f.o_pieces = P<uint32_t>(c, B_O_PIECES);
+  f.o_suf = P<uint32_t>(c, B_O_SUF);
+  f.o_sxm = P<uint32_t>(c, B_O_SXM);
+  f.o_tail = P<uint32_t>(c, B_O_TAIL);
+  f.o_ok = P<uint8_t>(c, B_O_OK);
+  f.slow_list = P<uint64_t>(c, B_SLOW);
+  f.n_slow = (unsigned long long*)(cnt + 5);
+  f.n_bad = (unsigned long long*)(cnt + 6);
+  if (n) {
+    finalize_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(f);
+    HIPCHK(hipGetLastError());
+    if (!f.no_crc) {
+      slow_kernel<<<256, 64, 0, c->stream>>>(f);
+      HIPCHK(hipGetLastError());
+    }
+  }
+  // ---- KeyIndexer::build ----
+  uint64_t hc = 64;
+  while (hc < 2 * n) hc <<= 1;
+  HIPCHK(hipMemsetAsync(P<void>(c, B_HKEYS), 0xff, hc * 8, c->stream));
+  HIPCHK(hipMemsetAsync(P<void>(c, B_HVALS), 0, hc * 8, c->stream));
+  HIPCHK(hipMemsetAsync(cnt + 7, 0, 8, c->stream));
+  HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_LATEST) + n, 0, 4, c->stream));
+  if (n) {
+    index_insert_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
+        P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_HKEYS),
+        P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7));
+    index_latest_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
+        P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_HKEYS),
+        P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7), P<uint32_t>(c, B_LATEST));
+    HIPCHK(hipGetLastError());
+  }
+  size_t tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_LATEST),
+                                          P<uint32_t>(c, B_IPOS), (int)(n + 1), c->stream));
+  if (n) {
+    index_emit_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO),
+                                                             P<uint32_t>(c, B_LATEST), P<uint32_t>(c, B_IPOS), n,
+                                                             P<uint64_t>(c, B_IKEY), P<uint64_t>(c, B_IPACKED));
+    HIPCHK(hipGetLastError());
+  }
+  uint32_t nidx = 0;
+  HIPCHK(hipMemcpyAsync(&nidx, P<uint32_t>(c, B_IPOS) + n, 4, hipMemcpyDeviceToHost, c->stream));
+  uint64_t h[8];
+  TRY(read_counters(c, h));
+  out->n_index = nidx;
+  out->n_crc_bad = h[6];
+  out->n_chain = n;
+  out->meta_off = P<uint64_t>(c, B_O_MO);
+  out->key_hash = P<uint64_t>(c, B_O_KH);
+  out->prev_offset = P<uint64_t>(c, B_O_PREV);
+  out->payload_start = P<uint64_t>(c, B_O_START);
+  out->payload_len = P<uint64_t>(c, B_O_LEN);
+  out->crc_stored = P<uint32_t>(c, B_O_CRCST);
+  out->crc_computed = P<uint32_t>(c, B_O_CRC);
+  out->crc_ok = P<uint8_t>(c, B_O_OK);
+  out->index_key_hash = P<uint64_t>(c, B_IKEY);
+  out->index_packed = P<uint64_t>(c, B_IPACKED);
+  return 0;
+}
+
+// is the 8-byte p-field of tail t zero (t is a root)?  host reads 8 bytes
+static int tail_is_root(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t t, bool* is_root) {
+  *is_root = false;
+  if (t < 21 || t > flen) return 0;
+  uint8_t b[8];
+  HIPCHK(hipMemcpyAsync(b, d_file + t - 12, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  uint64_t v;
+  memcpy(&v, b, 8);
+  *is_root = v == 0;
+  return 0;
+}
+
+static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uint64_t* K, uint64_t* h) {
+  const uint64_t n_tiles = (flen + TILE - 1) / TILE;
+  const uint64_t n_spans = (n_tiles + SPAN_TILES - 1) / SPAN_TILES;
+  while (true) {
+    TRY(alloc_scan(c, n_tiles, n_spans));
+    TRY(ensure_cub(c, n_spans + 1));
+    uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
+    HIPCHK(hipMemsetAsync(cnt, 0, 64, c->stream));
+    HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT), 0, (n_spans + 1) * 4, c->stream));
+    ScanArgs a{};
+    a.file = d_file;
+    a.flen = flen;
+    a.n_tiles = n_tiles;
+    a.n_spans = n_spans;
+    a.cap = c->cap;
+    a.tileT = P<uint32_t>(c, B_TILE_T);
+    a.tileSX1 = P<uint32_t>(c, B_TILE_SX1);
+    a.span_count = P<uint32_t>(c, B_SPAN_COUNT);
+    a.c_m = P<uint64_t>(c, B_CM);
+    a.c_p = P<uint64_t>(c, B_CP);
+    a.c_kh = P<uint64_t>(c, B_CKH);
+    a.c_crc = P<uint32_t>(c, B_CCRC);
+    a.c_sxm = P<uint32_t>(c, B_CSXM);
+    a.c_suf = P<uint32_t>(c, B_CSUF);
+    a.c_tail = P<uint32_t>(c, B_CTAIL);
+    a.c_flags = P<uint32_t>(c, B_CFLAGS);
+    a.max_root = (unsigned long long*)(cnt + 0);
+    a.n_weak = (unsigned long long*)(cnt + 1);
+    a.overflow = (unsigned int*)(cnt + 2);
+    if (n_spans) {
+      unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES - 1) / SCAN_WAVES, 512);
+      HIPCHK(hipEventRecord(c->ev[0], c->stream));
+      if (full)
+        scan_kernel<true><<<g, SCAN_WAVES * 64, 0, c->stream>>>(a);
+      else
+        scan_kernel<false><<<g, SCAN_WAVES * 64, 0, c->stream>>>(a);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    }
+    size_t tb = c->bufs[B_CUB_TMP].n;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_SPAN_COUNT),
+                                            P<uint64_t>(c, B_SPAN_BASE), (int)(n_spans + 1), c->stream));
+    HIPCHK(hipMemcpyAsync(K, P<uint64_t>(c, B_SPAN_BASE) + n_spans, 8, hipMemcpyDeviceToHost, c->stream));
+    TRY(read_counters(c, h));
+    if (n_spans) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+      c->scan_ms += ms;
+      c->scan_launches++;
+    }
+    if ((uint32_t)h[2] == 0) break;
+    if (c->cap >= SPAN_BYTES) { set_err("candidate overflow"); return SRD_ERR_INTERNAL; }
+    c->cap = (uint32_t)std::min<uint64_t>((uint64_t)c->cap * 4, SPAN_BYTES);
+  }
+  if (*K) {
+    TRY(alloc_dense(c, *K));
+    LinkArgs l{};
+    l.file = d_file;
+    l.flen = flen;
+    l.n_spans = n_spans;
+    l.cap = c->cap;
+    l.span_count = P<uint32_t>(c, B_SPAN_COUNT);
+    l.span_base = P<uint64_t>(c, B_SPAN_BASE);
+    l.c_m = P<uint64_t>(c, B_CM);
+    l.c_p = P<uint64_t>(c, B_CP);
+    l.d_m = P<uint64_t>(c, B_DM);
+    l.d_par = P<int64_t>(c, B_DPAR);
+    l.d_slot = P<uint64_t>(c, B_DSLOT);
+    link_kernel<<<(unsigned)n_spans, 64, 0, c->stream>>>(l);
+    HIPCHK(hipGetLastError());
+  } else {
+    TRY(alloc_dense(c, 1));
+  }
+  return 0;
+}
+
+__global__ void vpos_kernel(const uint64_t* vl, uint64_t n, uint64_t* vp) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) vp[vl[i]] = i;
+}
+
+static int set_single_root(Ctx* c, uint64_t t) {
+  WalkState w{};
+  w.status = 1;
+  w.chain_len = 1;
+  w.root_t = t;
+  w.final_len = t;
+  HIPCHK(hipMemcpyAsync(P<WalkState>(c, B_WALK), &w, sizeof w, hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen, uint32_t flags,
+                                srd_device_result* out);
+
+extern "C" int srd_validate_index_device(srd_ctx* c, const uint8_t* d_file, uint64_t flen, uint32_t flags,
+                                         srd_device_result* out) {
+  if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
+  c->scan_ms = 0;
+  c->scan_launches = 0;
+  HIPCHK(hipEventRecord(c->ev[2], c->stream));
+  int r = validate_device_impl(c, d_file, flen, flags, out);
+  HIPCHK(hipEventRecord(c->ev[3], c->stream));
+  HIPCHK(hipEventSynchronize(c->ev[3]));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+  c->total_ms = ms;
+  return r;
+}
+
+extern "C" int srd_ctx_timings(srd_ctx* c, double* scan_ms, int* scan_launches, double* total_ms) {
+  if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (scan_ms) *scan_ms = c->scan_ms;
+  if (scan_launches) *scan_launches = c->scan_launches;
+  if (total_ms) *total_ms = c->total_ms;
+  return 0;
+}
+
+static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen, uint32_t flags,
+                                srd_device_result* out) {
+  if (!c || !out || (!d_file && flen)) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (flen >= (1ull << 40)) { set_err("stores >= 1 TiB are not supported"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
+  memset(out, 0, sizeof *out);
+  out->file_len = flen;
+  if (flen < 21) {  // no tail can be valid (recover_valid_chain :384-386, t>=21)
+    TRY(alloc_dense(c, 1));
+    TRY(alloc_scan(c, 1, 1));
+    return finish(c, d_file, flen, 0, flags, out);
+  }
+  bool full = flags & SRD_FLAG_FORCE_FULL;
+  uint64_t K = 0, h[8];
+  // ---- optimistic pass: strong candidates only; valid iff the walk from
+  //      file_len reaches a root through recorded nodes ----
+  if (!full) {
+    TRY(run_scan(c, d_file, flen, false, &K, h));
+    out->n_candidates = K;
+    out->n_weak = h[1];
+    bool root = false;
+    TRY(tail_is_root(c, d_file, flen, flen, &root));
+    if (root) {
+      TRY(set_single_root(c, flen));
+      out->final_len = flen;
+      return finish(c, d_file, flen, 1, flags, out);
+    }
+    uint64_t lastm = ~0ull;
+    if (K) {
+      HIPCHK(hipMemcpyAsync(&lastm, P<uint64_t>(c, B_DM) + K - 1, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    if (K && lastm == flen - 20) {
+      WalkState w{};
+      w.start = K - 1;
+      HIPCHK(hipMemcpyAsync(P<WalkState>(c, B_WALK), &w, sizeof w, hipMemcpyHostToDevice, c->stream));
+      WalkState hw{};
+      TRY(walk_and_mark(c, P<int64_t>(c, B_DPAR), P<uint64_t>(c, B_DSLOT), K, nullptr, &hw));
+      if (hw.status == 1) {
+        out->final_len = flen;
+        return finish(c, d_file, flen, hw.chain_len, flags, out);
+      }
+    }
+    full = true;  // could not conclude: every candidate is needed
+  }
+  // ---- full pass ----
+  out->mode = 1;
+  TRY(run_scan(c, d_file, flen, true, &K, h));
+  out->n_candidates = K;
+  out->n_weak = 0;
+  const uint64_t max_root = h[0];
+  uint64_t best_g1 = 0, tlin = 0;
+  if (K) {
+    TRY(ensure(c, B_ST, K));
+    TRY(ensure(c, B_JMP, K * 8));
+    TRY(ensure(c, B_VFLAG, K * 4));
+    status_init_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<int64_t>(c, B_DPAR), K, P<uint8_t>(c, B_ST),
+                                                              P<int64_t>(c, B_JMP));
+    uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
+    for (int round = 0; round < 80; round++) {
+      HIPCHK(hipMemsetAsync(cnt + 4, 0, 8, c->stream));
+      status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, P<uint8_t>(c, B_ST), P<int64_t>(c, B_JMP),
+                                                                 (unsigned int*)(cnt + 4));
+      HIPCHK(hipGetLastError());
+      TRY(read_counters(c, h));
+      if (!h[4]) break;
+    }
+    HIPCHK(hipMemsetAsync(cnt + 3, 0, 8, c->stream));
+    valid_max_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<uint8_t>(c, B_ST), P<uint64_t>(c, B_DM), K,
+                                                            (unsigned long long*)(cnt + 3), P<uint32_t>(c, B_VFLAG));
+    HIPCHK(hipGetLastError());
+    TRY(read_counters(c, h));
+    best_g1 = h[3];
+    if (best_g1) {
+      uint64_t bm;
+      HIPCHK(hipMemcpyAsync(&bm, P<uint64_t>(c, B_DM) + best_g1 - 1, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      tlin = bm + 20;
+    }
+  }
+  const uint64_t final_len = std::max(tlin, max_root);
+  out->final_len = final_len;
+  if (final_len == 0) return finish(c, d_file, flen, 0, flags, out);
+  if (final_len == max_root && max_root > tlin) {
+    TRY(set_single_root(c, final_len));
+    return finish(c, d_file, flen, 1, flags, out);
+  }
+  // compact the valid nodes, walk from the best one
+  TRY(ensure(c, B_VLIST, K * 8));
+  TRY(ensure(c, B_NV, 8));
+  TRY(ensure(c, B_VPOS, K * 8));
+  TRY(ensure(c, B_VPAR, K * 8));
+  TRY(ensure(c, B_VSLOT, K * 8));
+  size_t tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceSelect::Flagged(P<void>(c, B_CUB_TMP), tb, hipcub::CountingInputIterator<uint64_t>(0),
+                                       P<uint32_t>(c, B_VFLAG), P<uint64_t>(c, B_VLIST), P<uint64_t>(c, B_NV),
+                                       (int)K, c->stream));
+  uint64_t nv = 0;
+  HIPCHK(hipMemcpyAsync(&nv, P<uint64_t>(c, B_NV), 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  // vpos[vlist[i]] = i  (scatter via a tiny lambda kernel)
+  vpos_kernel<<<blocks(nv, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_VLIST), nv, P<uint64_t>(c, B_VPOS));
+  remap_kernel<<<blocks(nv, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_VLIST), P<uint64_t>(c, B_NV),
+                                                       P<int64_t>(c, B_DPAR), P<uint64_t>(c, B_VPOS),
+                                                       P<int64_t>(c, B_VPAR), P<uint64_t>(c, B_VSLOT),
+                                                       P<uint64_t>(c, B_DSLOT));
+  HIPCHK(hipGetLastError());
+  uint64_t vstart = 0;
+  HIPCHK(hipMemcpyAsync(&vstart, P<uint64_t>(c, B_VPOS) + best_g1 - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  WalkState w{};
+  w.start = vstart;
+  HIPCHK(hipMemcpyAsync(P<WalkState>(c, B_WALK), &w, sizeof w, hipMemcpyHostToDevice, c->stream));
+  WalkState hw{};
+  TRY(walk_and_mark(c, P<int64_t>(c, B_VPAR), P<uint64_t>(c, B_VSLOT), nv, P<uint64_t>(c, B_VLIST), &hw));
+  if (hw.status != 1) { set_err("internal: valid walk did not reach a root"); return SRD_ERR_INTERNAL; }
+  return finish(c, d_file, flen, hw.chain_len, flags, out);
+}
+
+// ---------------------------------------------------------------- host input
+static int stage_file(Ctx* c, const uint8_t* file, uint64_t flen, const uint8_t** d) {
+  if (c->file.n < flen + 64) {
+    if (c->file.p) HIPCHK(hipFree(c->file.p));
+    c->file.p = nullptr;
+    c->file.n = 0;
+    if (hipMalloc(&c->file.p, flen + 64) != hipSuccess) { set_err("hipMalloc(file)"); return SRD_ERR_ALLOC; }
+    c->file.n = flen + 64;
+  }
+  if (flen) HIPCHK(hipMemcpyAsync(c->file.p, file, flen, hipMemcpyHostToDevice, c->stream));
+  *d = (const uint8_t*)c->file.p;
+  return 0;
+}
+
+template <class T>
+static T* d2h(Ctx* c, const T* d, uint64_t n, int* rc) {
+  T* h = (T*)malloc(std::max<uint64_t>(n, 1) * sizeof(T));
+  if (!h) { *rc = SRD_ERR_ALLOC; return nullptr; }
+  if (n && hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, c->stream) != hipSuccess) *rc = SRD_ERR_HIP;
+  return h;
+}
+
+extern "C" int srd_validate_index(srd_ctx* c, const uint8_t* file, uint64_t flen, uint32_t flags, srd_result* out) {
+  if (!c || !out || (!file && flen)) { set_err("bad argument"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
+  const uint8_t* d = nullptr;
+  TRY(stage_file(c, file, flen, &d));
+  srd_device_result r;
+  TRY(srd_validate_index_device(c, d, flen, flags, &r));
+  *out = r;
+  int rc = 0;
+  uint64_t n = r.n_chain, ni = r.n_index;
+  out->meta_off = d2h(c, r.meta_off, n, &rc);
+  out->key_hash = d2h(c, r.key_hash, n, &rc);
+  out->prev_offset = d2h(c, r.prev_offset, n, &rc);
+  out->payload_start = d2h(c, r.payload_start, n, &rc);
+  out->payload_len = d2h(c, r.payload_len, n, &rc);
+  out->crc_stored = d2h(c, r.crc_stored, n, &rc);
+  out->crc_computed = d2h(c, r.crc_computed, n, &rc);
+  out->crc_ok = d2h(c, r.crc_ok, n, &rc);
+  out->index_key_hash = d2h(c, r.index_key_hash, ni, &rc);
+  out->index_packed = d2h(c, r.index_packed, ni, &rc);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (rc) { set_err("result copy failed"); srd_result_free(out); }
+  return rc;
+}
+
+extern "C" void srd_result_free(srd_result* r) {
+  if (!r) return;
+  free(r->meta_off); free(r->key_hash); free(r->prev_offset); free(r->payload_start); free(r->payload_len);
+  free(r->crc_stored); free(r->crc_computed); free(r->crc_ok); free(r->index_key_hash); free(r->index_packed);
+  memset(r, 0, sizeof *r);
+}
+
+extern "C" int srd_recover_valid_chain(srd_ctx* c, const uint8_t* file, uint64_t flen, uint64_t* final_len) {
+  if (!final_len) { set_err("bad argument"); return SRD_ERR_ARG; }
+  const uint8_t* d = nullptr;
+  TRY(stage_file(c, file, flen, &d));
+  srd_device_result r;
+  TRY(srd_validate_index_device(c, d, flen, SRD_FLAG_NO_CRC, &r));
+  *final_len = r.final_len;
+  return 0;
+}
+
+extern "C" int srd_key_indexer_build(srd_ctx* c, const uint8_t* file, uint64_t tail, uint64_t* keys,
+                                     uint64_t* packed, uint64_t cap, uint64_t* n_out) {
+  if (!n_out) { set_err("bad argument"); return SRD_ERR_ARG; }
+  const uint8_t* d = nullptr;
+  TRY(stage_file(c, file, tail, &d));
+  srd_device_result r;
+  TRY(srd_validate_index_device(c, d, tail, SRD_FLAG_NO_CRC, &r));
+  if (r.final_len != tail) {
+    set_err("tail is not a valid chain tail (KeyIndexer::build expects the recovered tail)");
+    return SRD_ERR_ARG;
+  }
+  *n_out = r.n_index;
+  uint64_t k = std::min(cap, r.n_index);
+  if (k) {
+    HIPCHK(hipMemcpyAsync(keys, r.index_key_hash, k * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(packed, r.index_packed, k * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+extern "C" int srd_crc32_batch_device(srd_ctx* c, const uint8_t* d_buf, const uint64_t* d_offs,
+                                      const uint64_t* d_lens, uint64_t n, uint32_t* d_out, void* stream) {
+  if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (!n) return 0;
+  crc_batch_kernel<<<(unsigned)std::min<uint64_t>(n, 8192), 64, 0, s>>>(d_buf, d_offs, d_lens, n, d_out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int srd_xxh3_64_batch_device(srd_ctx* c, const uint8_t* d_keys, const uint64_t* d_offs,
+                                        const uint64_t* d_lens, uint64_t n, uint64_t* d_out, void* stream) {
+  if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (!n) return 0;
+  xxh3_batch_kernel<<<blocks(n, 256), 256, 0, s>>>(d_keys, d_offs, d_lens, n, d_out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+template <class OUT, class F>
+static int batch_host(srd_ctx* c, const uint8_t* buf, uint64_t blen, const uint64_t* offs, const uint64_t* lens,
+                      uint64_t n, OUT* out, F launch) {
+  HIPCHK(hipSetDevice(c->device));
+  for (uint64_t i = 0; i < n; i++)
+    if (offs[i] > blen || lens[i] > blen - offs[i]) { set_err("range out of bounds"); return SRD_ERR_ARG; }
+  void *db = nullptr, *dof = nullptr, *dl = nullptr, *dout = nullptr;
+  HIPCHK(hipMalloc(&db, blen + 1));
+  HIPCHK(hipMalloc(&dof, n * 8 + 8));
+  HIPCHK(hipMalloc(&dl, n * 8 + 8));
+  HIPCHK(hipMalloc(&dout, n * sizeof(OUT) + 8));
+  if (blen) HIPCHK(hipMemcpyAsync(db, buf, blen, hipMemcpyHostToDevice, c->stream));
+  if (n) {
+    HIPCHK(hipMemcpyAsync(dof, offs, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(dl, lens, n * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  int r = launch((const uint8_t*)db, (const uint64_t*)dof, (const uint64_t*)dl, (OUT*)dout);
+  if (!r && n) HIPCHK(hipMemcpyAsync(out, dout, n * sizeof(OUT), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  hipFree(db); hipFree(dof); hipFree(dl); hipFree(dout);
+  return r;
+}
+
+extern "C" int srd_crc32_batch(srd_ctx* c, const uint8_t* buf, uint64_t blen, const uint64_t* offs,
+                               const uint64_t* lens, uint64_t n, uint32_t* out) {
+  if (!c || (n && (!offs || !lens || !out))) { set_err("bad argument"); return SRD_ERR_ARG; }
+  return batch_host<uint32_t>(c, buf, blen, offs, lens, n, out, [&](auto db, auto dof, auto dl, auto dout) {
+    return srd_crc32_batch_device(c, db, dof, dl, n, dout, nullptr);
+  });
+}
+
+extern "C" int srd_xxh3_64_batch(srd_ctx* c, const uint8_t* keys, uint64_t klen, const uint64_t* offs,
+                                 const uint64_t* lens, uint64_t n, uint64_t* out) {
+  if (!c || (n && (!offs || !lens || !out))) { set_err("bad argument"); return SRD_ERR_ARG; }
+  return batch_host<uint64_t>(c, keys, klen, offs, lens, n, out, [&](auto db, auto dof, auto dl, auto dout) {
+    return srd_xxh3_64_batch_device(c, db, dof, dl, n, dout, nullptr);
+  });
+}
+
+extern "C" int srd_synth_store_device(srd_ctx* c, uint8_t* d_out, uint64_t n, uint64_t fixed_len,
+                                      const uint64_t* lens, uint64_t seed, uint64_t* len_out) {
+  if (!len_out) { set_err("bad argument"); return SRD_ERR_ARG; }
+  std::vector<uint64_t> off(n);
+  uint64_t tail = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t L = lens ? lens[i] : fixed_len;
+    if (L == 0) { set_err("empty payload"); return SRD_ERR_ARG; }
+    off[i] = tail;
+    tail += ((64 - tail % 64) & 63) + L + 20;
+  }
+  *len_out = tail;
+  if (!d_out || !n) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  void *doff = nullptr, *dl = nullptr;
+  HIPCHK(hipMalloc(&doff, n * 8));
+  HIPCHK(hipMemcpyAsync(doff, off.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+  if (lens) {
+    HIPCHK(hipMalloc(&dl, n * 8));
+    HIPCHK(hipMemcpyAsync(dl, lens, n * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  synth_kernel<<<(unsigned)std::min<uint64_t>(n, 65536), 64, 0, c->stream>>>(
+      d_out, (const uint64_t*)doff, (const uint64_t*)dl, fixed_len, n, seed);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  hipFree(doff);
+  if (dl) hipFree(dl);
+  return 0;
+}
+
+// host self-test of the CRC algebra (no GPU): checks the tables against a
+// byte-wise CRC on pseudo-random data with the same combine the kernels use.
+extern "C" int srd_selftest_host(void) {
+  std::call_once(g_tab_once, [] { build_crc_tables(g_host_tabs); });
+  const CrcTables& t = g_host_tabs;
+  static uint8_t buf[5 * 4096];
+  memset(buf, 0, sizeof buf);
+  uint64_t z = 12345;
+  for (int i = 0; i < 3 * 4096 + 200; i++) { auto& b = buf[i]; z = z * 6364136223846793005ull + 1442695040888963407ull; b = (uint8_t)(z >> 56); }
+  // x^-8 * x^8 == 1
+  if (mulp(t.invpow[1], t.pow8[0]) != kX0) return 1;
+  // check crc_from_pieces-style assembly for several (s, m)
+  auto raw = [&](uint64_t a, uint64_t b) { return host_crc_raw_bytes(t, 0, buf + a, b - a); };
+  auto crc32 = [&](uint64_t a, uint64_t b) { return ~host_crc_raw_bytes(t, ~0u, buf + a, b - a); };
+  auto sx = [&](uint64_t k, uint32_t j) {  // crc_raw(lines j..63 of tile k)
+    return raw(k * 4096 + 64 * j, k * 4096 + 4096);
+  };
+  const uint64_t cases[][2] = {{0, 100}, {64, 4096}, {128, 5000}, {4096, 8192 + 77}, {192, 12288 + 3}, {0, 63}};
+  for (auto& cs : cases) {
+    uint64_t s = cs[0], m = cs[1];
+    uint64_t len = m - s;
+    uint32_t want = crc32(s, m);
+    uint32_t tail = raw(m & ~63ull, m);
+    uint32_t got;
+    if (len < 64) {
+      got = tail ^ t.zero_crc[len];
+    } else {
+      uint64_t k0 = s / 4096, k1 = m / 4096;
+      uint32_t acc = sx(k0, (uint32_t)((s % 4096) / 64)) ^ t.winit[(s % 4096) / 64];
+      uint32_t sxm = sx(k1, (uint32_t)((m % 4096) / 64));
+      uint32_t y;
+      if (k0 == k1) y = acc ^ sxm;
+      else {
+        for (uint64_t k = k0 + 1; k < k1; k++) acc = mulp(t.x32768, acc) ^ sx(k, 0);
+        y = mulp(t.x32768, acc) ^ sx(k1, 0) ^ sxm;
+      }
+      got = ~(mulp(t.invpow[(k1 + 1) * 4096 - m], y) ^ tail);
+    }
+    if (got != want) return 2;
+  }
+  return 0;
+}

@@ -1,0 +1,803 @@
+// srd_kernels.hip -- MI355X (gfx950) kernels of the validate+index hot path.
+//
+// Reference path being replaced (jzombie/rust-simd-r-drive v0.16.3-alpha):
+//   DataStore::open           src/storage_engine/data_store.rs:84-117
+//   recover_valid_chain       src/storage_engine/data_store.rs:383-482
+//   KeyIndexer::build         src/storage_engine/key_indexer.rs:98-124
+//   is_valid_checksum         simd-r-drive-entry-handle/src/entry_handle.rs:260-275
+//
+// Pipeline:
+//   1. scan_kernel   one streaming pass over the file.  Each wave owns spans of
+//                    16 tiles (4 KiB tile = 64 lines x 64 B, one line per
+//                    lane).  Per tile it (a) finds chain-node candidates with
+//                    a zero-triple filter + wave-cooperative exact check,
+//                    (b) computes every line's raw CRC with LDS slice-by-4
+//                    tables, (c) weights lines by x^(512(63-l)) and runs a
+//                    64-lane suffix-XOR scan, so any 64-aligned range's CRC
+//                    can later be assembled from O(1) per-tile values.
+//   2. link_kernel   parent lookup per candidate (binary search in the span
+//                    of the target) -> node / root / miss.
+//   3. walk + mark   the chain from final_len, run-compressed (consecutive
+//                    candidates that link to their predecessor form a run).
+//   4. finalize      per chain entry: CRC from per-tile values (a few GF(2)
+//                    multiplies), slow path recomputes a tile when a piece is
+//                    missing.
+//   5. index         XXH3-hashed open-addressing table, latest wins.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "srd_crc.h"
+#include "srd_xxh3.h"
+
+namespace srd {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TILE = 4096;
+constexpr int SPAN_TILES = 16;
+constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
+constexpr int REPL = 16;             // LDS table replication (bank spreading)
+constexpr int SCAN_WAVES = 8;        // waves per scan block
+constexpr int TCAP = 128;            // per-tile candidate list in LDS
+constexpr int64_t PAR_ROOT = -1;
+constexpr int64_t PAR_MISS = -2;
+
+// flags of a candidate record
+constexpr uint32_t F_TOMB = 1u, F_TAIL = 2u, F_SXM = 4u;
+constexpr int F_SUF_SHIFT = 3;        // 2 bits: 0 value, 1 next-tile T, 2 next-tile SX1, 3 missing
+
+struct DevTables {
+  uint32_t tab[4][256];
+  uint32_t lw[64];
+  uint32_t winit[64];
+  uint32_t zero_crc[64];
+  uint32_t x32768;
+  uint32_t pow8[64];
+  uint32_t invpow[4097];
+};
+__device__ DevTables g_tabs;
+
+struct ScanArgs {
+  const uint8_t* file;
+  uint64_t flen;
+  uint64_t n_tiles, n_spans;
+  uint32_t cap;
+  uint32_t* tileT;
+  uint32_t* tileSX1;
+  uint32_t* span_count;
+  uint64_t* c_m;
+  uint64_t* c_p;
+  uint64_t* c_kh;
+  uint32_t* c_crc;
+  uint32_t* c_sxm;
+  uint32_t* c_suf;
+  uint32_t* c_tail;
+  uint32_t* c_flags;
+  unsigned long long* max_root;
+  unsigned long long* n_weak;
+  unsigned int* overflow;
+};
+
+__device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
+  if (o + 4 <= n) return *(const uint32_t*)(f + o);
+  uint32_t v = 0;
+  for (int k = 0; k < 4; k++)
+    if (o + k < n) v |= (uint32_t)f[o + k] << (8 * k);
+  return v;
+}
+__device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t* f, uint64_t o) {
+  uint64_t v = 0;
+  for (int k = 0; k < 8; k++) v |= (uint64_t)f[o + k] << (8 * k);
+  return v;
+}
+__device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* f, uint64_t o) {
+  uint32_t v = 0;
+  for (int k = 0; k < 4; k++) v |= (uint32_t)f[o + k] << (8 * k);
+  return v;
+}
+__device__ __forceinline__ uint64_t prepad64(uint64_t o) { return (64 - (o & 63)) & 63; }
+
+__device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbit(hi, lo, sh);
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t w = __shfl_xor(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+// --------------------------------------------------------------------------
+// 1. the fused streaming scan
+// --------------------------------------------------------------------------
+template <bool FULL>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_kernel(ScanArgs a) {
+  __shared__ uint32_t s_tab[4 * 256 * REPL];
+  __shared__ uint32_t s_win[SCAN_WAVES][24];
+  __shared__ uint32_t s_tslot[SCAN_WAVES][TCAP];
+  __shared__ uint32_t s_tinfo[SCAN_WAVES][TCAP];
+
+  for (int i = threadIdx.x; i < 4 * 256 * REPL; i += blockDim.x)
+    s_tab[i] = (&g_tabs.tab[0][0])[i / REPL];
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint32_t cpy = lane & (REPL - 1);
+  const uint32_t lwl = g_tabs.lw[lane];
+  const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES;
+  const uint8_t* file = a.file;
+  const uint64_t flen = a.flen;
+
+  uint64_t rootmax = 0, weak = 0;
+
+  for (uint64_t sp = (uint64_t)blockIdx.x * SCAN_WAVES + wv; sp < a.n_spans; sp += total_waves) {
+    uint32_t count = 0;
+    for (int tt = 0; tt < SPAN_TILES; tt++) {
+      const uint64_t k = sp * SPAN_TILES + tt;
+      if (k >= a.n_tiles) break;
+      const uint64_t B = k * (uint64_t)TILE;
+      const uint64_t L = B + 64ull * lane;
+
+      // ---- load my line (+ neighbours' bytes) ----
+      uint32_t d[16];
+      if (L + 64 <= flen) {
+        const u32x4* q = (const u32x4*)(file + L);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          u32x4 v = __builtin_nontemporal_load(q + j);
+          d[4 * j] = v[0]; d[4 * j + 1] = v[1]; d[4 * j + 2] = v[2]; d[4 * j + 3] = v[3];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++) d[j] = ld_dw_guarded(file, flen, L + 4 * j);
+      }
+      uint32_t look[5];
+#pragma unroll
+      for (int j = 0; j < 5; j++) look[j] = __shfl_down(d[j], 1);
+      if (lane == 63) {
+#pragma unroll
+        for (int j = 0; j < 5; j++) look[j] = ld_dw_guarded(file, flen, B + TILE + 4 * j);
+      }
+      uint32_t prevdw = __shfl_up(d[15], 1);
+      if (lane == 0) prevdw = B >= 4 ? ld_dw_guarded(file, flen, B - 4) : 0u;
+
+      // ---- quick filter: any zero triple where a p-field's top bytes sit ----
+      uint32_t acc = 0;
+#pragma unroll
+      for (int i = 3; i < 20; i++) {
+        uint32_t wi = i < 16 ? d[i] : look[i - 16];
+        uint32_t wn = (i + 1) < 16 ? d[i + 1] : look[i + 1 - 16];
+        uint32_t x = wi | alignb(wn, wi, 8) | alignb(wn, wi, 16);
+        acc |= (x - 0x01010101u) & ~x;
+      }
+      uint64_t slow = __ballot((acc & 0x80808080u) != 0);
+
+      uint32_t ntc = 0;
+      int snapoff = 64;
+      while (slow) {
+        const int f = __builtin_ctzll(slow);
+        slow &= slow - 1;
+        if (lane == f) {
+          s_win[wv][0] = prevdw;
+#pragma unroll
+          for (int j = 0; j < 16; j++) s_win[wv][1 + j] = d[j];
+#pragma unroll
+          for (int j = 0; j < 5; j++) s_win[wv][17 + j] = look[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t b = lane;
+        const uint64_t m = B + 64ull * f + b;
+        const int base = 1 + (b >> 2);
+        const uint32_t sh = (b & 3) * 8;
+        uint32_t W[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) W[i] = s_win[wv][base + i];
+        const uint32_t tdw = s_win[wv][(3 + b) >> 2];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t tbyte = (tdw >> (((3 + b) & 3) * 8)) & 0xffu;
+        const uint32_t f0 = alignb(W[1], W[0], sh), f1 = alignb(W[2], W[1], sh);
+        const uint32_t f2 = alignb(W[3], W[2], sh), f3 = alignb(W[4], W[3], sh);
+        const uint32_t f4 = alignb(W[5], W[4], sh);
+        const uint64_t p = (uint64_t)f2 | ((uint64_t)f3 << 32);
+        const bool inrange = (m >= 1) && (m + 20 <= flen);
+        if (inrange && p == 0) rootmax = rootmax > m + 20 ? rootmax : m + 20;
+        const bool tomb = (m > p) && (m - p == 1) && tbyte == 0;
+        const uint64_t start = tomb ? p : p + prepad64(p);
+        const bool isnode = inrange && p != 0 && start < m && p < m && p >= 20;
+        const bool strong = isnode && (FULL || f4 != 0);
+        weak += (isnode && !strong) ? 1 : 0;
+        const uint64_t cm = __ballot(strong);
+        if (cm) {
+          const uint32_t nc = __popcll(cm);
+          const uint32_t rank = __popcll(cm & ((1ull << lane) - 1));
+          if (strong) {
+            const uint32_t idx = count + rank;
+            const uint32_t tl = ntc + rank;
+            const uint64_t t = m + 20;
+            const uint64_t s2 = t + prepad64(t);
+            const uint32_t js = (uint32_t)((s2 - B) >> 6);
+            if (idx < a.cap) {
+              const uint64_t gi = sp * a.cap + idx;
+              a.c_m[gi] = m;
+              a.c_p[gi] = p;
+              a.c_kh[gi] = (uint64_t)f0 | ((uint64_t)f1 << 32);
+              a.c_crc[gi] = f4;
+              if (tl >= TCAP) a.c_flags[gi] = (tomb ? F_TOMB : 0u) | (3u << F_SUF_SHIFT);
+            } else {
+              atomicOr(a.overflow, 1u);
+            }
+            if (tl < TCAP) {
+              s_tslot[wv][tl] = idx;
+              s_tinfo[wv][tl] = (uint32_t)f | (b << 8) | (js << 16) | (tomb ? 0x80000000u : 0u);
+            }
+          }
+          if (lane == f) snapoff = __builtin_ctzll(cm);
+          count += nc;
+          ntc += nc;
+        }
+      }
+
+      // ---- per-line raw CRC (slice-by-4, replicated LDS tables) ----
+      uint32_t s = 0, snap = 0, snapdw = 0;
+      const int snapw = snapoff >> 2;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        if (j == snapw) { snap = s; snapdw = d[j]; }
+        s ^= d[j];
+        s = s_tab[((3 << 8) + (s & 0xff)) * REPL + cpy] ^ s_tab[((2 << 8) + ((s >> 8) & 0xff)) * REPL + cpy] ^
+            s_tab[((1 << 8) + ((s >> 16) & 0xff)) * REPL + cpy] ^ s_tab[((s >> 24)) * REPL + cpy];
+      }
+      uint32_t tailv = 0;
+      if (snapoff < 64) {
+        tailv = snap;
+        for (int q = 0; q < (snapoff & 3); q++)
+          tailv = s_tab[((tailv ^ (snapdw >> (8 * q))) & 0xff) * REPL + cpy] ^ (tailv >> 8);
+      }
+      // ---- lane weight + suffix XOR over the tile ----
+      uint32_t sx = mulp(lwl, s);
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t v = __shfl_down(sx, o);
+        if (lane + o < 64) sx ^= v;
+      }
+      if (lane == 0) a.tileT[k] = sx;
+      if (lane == 1) a.tileSX1[k] = sx;
+
+      // ---- complete this tile's candidate records ----
+      const uint32_t nlist = ntc < TCAP ? ntc : TCAP;
+      for (uint32_t b0 = 0; b0 < nlist; b0 += 64) {
+        const uint32_t i = b0 + lane;
+        const bool act = i < nlist;
+        const uint32_t info = act ? s_tinfo[wv][i] : 0u;
+        const int f = info & 63, r = (info >> 8) & 63, js = (info >> 16) & 127;
+        const uint32_t sxm = __shfl(sx, f);
+        const uint32_t tl = __shfl(tailv, f);
+        const int so = __shfl(snapoff, f);
+        const uint32_t sufv = __shfl(sx, js & 63);
+        if (act) {
+          const uint32_t idx = s_tslot[wv][i];
+          if (idx < a.cap) {
+            const uint64_t gi = sp * a.cap + idx;
+            const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
+            a.c_sxm[gi] = sxm;
+            a.c_suf[gi] = sufv;
+            a.c_tail[gi] = tl;
+            a.c_flags[gi] = ((info >> 31) ? F_TOMB : 0u) | (so == r ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT);
+          }
+        }
+      }
+    }
+    if (lane == 0) a.span_count[sp] = count;
+  }
+  rootmax = wave_max_u64(rootmax);
+  for (int o = 32; o > 0; o >>= 1) weak += __shfl_xor(weak, o);
+  if (lane == 0) {
+    if (rootmax) atomicMax(a.max_root, (unsigned long long)rootmax);
+    if (weak) atomicAdd(a.n_weak, (unsigned long long)weak);
+  }
+}
+
+// --------------------------------------------------------------------------
+// 2. parent lookup
+// --------------------------------------------------------------------------
+struct LinkArgs {
+  const uint8_t* file;
+  uint64_t flen, n_spans;
+  uint32_t cap;
+  const uint32_t* span_count;
+  const uint64_t* span_base;  // exclusive prefix of min(count, cap)
+  const uint64_t* c_m;
+  const uint64_t* c_p;
+  uint64_t* d_m;
+  int64_t* d_par;
+  uint64_t* d_slot;
+};
+
+__global__ __launch_bounds__(64) void link_kernel(LinkArgs a) {
+  const uint64_t sp = blockIdx.x;
+  const uint32_t n = min(a.span_count[sp], a.cap);
+  const uint64_t gb = a.span_base[sp];
+  for (uint32_t i = threadIdx.x; i < n; i += 64) {
+    const uint64_t gi = sp * a.cap + i;
+    const uint64_t m = a.c_m[gi], p = a.c_p[gi];
+    const uint64_t mp = p - 20;  // p >= 20 by construction
+    const uint64_t sp2 = mp / SPAN_BYTES;
+    int64_t par = PAR_MISS;
+    if (sp2 < a.n_spans) {
+      uint32_t lo = 0, hi = min(a.span_count[sp2], a.cap);
+      const uint64_t* cm = a.c_m + sp2 * a.cap;
+      while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (cm[mid] < mp) lo = mid + 1; else hi = mid;
+      }
+      if (lo < min(a.span_count[sp2], a.cap) && cm[lo] == mp) par = (int64_t)(a.span_base[sp2] + lo);
+    }
+    if (par == PAR_MISS && p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) par = PAR_ROOT;
+    const uint64_t g = gb + i;
+    a.d_m[g] = m;
+    a.d_par[g] = par;
+    a.d_slot[g] = gi;
+  }
+}
+
+// --------------------------------------------------------------------------
+// 3. chain walk over runs (single thread) + marking
+// --------------------------------------------------------------------------
+struct WalkState {
+  int64_t status;      // 1 ok, -1 miss (cannot conclude), -2 no start
+  uint64_t n_int;      // intervals [h, x] in an index space
+  uint64_t chain_len;  // entries incl. root
+  uint64_t root_t;     // tail of the chain's root entry
+  uint64_t final_len;
+  uint64_t start;      // start index in the walk space
+  int64_t pad[2];
+};
+
+// idx space: 0..n-1 ; par_of(i) gives par in the same space ; runhead[i]
+__global__ void walk_kernel(const int64_t* par, const uint64_t* runhead, const uint64_t* slot,
+                            const uint64_t* c_p, uint64_t* ints, WalkState* ws, uint64_t max_ints) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t x = ws->start, n = 0, len = 1;
+  int64_t status = 1;
+  while (true) {
+    uint64_t h = runhead[x] - 1;  // runhead holds (run head index + 1)
+    if (n < max_ints) { ints[2 * n] = h; ints[2 * n + 1] = x; }
+    n++;
+    len += x - h + 1;
+    int64_t q = par[h];
+    if (q == PAR_ROOT) { ws->root_t = c_p[slot[h]]; break; }
+    if (q < 0) { status = -1; break; }
+    x = (uint64_t)q;
+  }
+  ws->status = status;
+  ws->n_int = n;
+  ws->chain_len = len;
+}
+
+// Leaf pruning: a chain node other than the start always has a child (the
+// next chain entry links to it), so nodes nobody links to (false candidates)
+// are dropped before run compression.  core[g] = has a child || g == start.
+__global__ void child_kernel(const int64_t* par, uint64_t n, uint8_t* core) {
+  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  int64_t p = par[g];
+  if (p >= 0) core[p] = 1;
+}
+__global__ void core_key_kernel(uint8_t* core, const WalkState* ws, uint64_t n, uint64_t* key) {
+  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  if (g == ws->start) core[g] = 1;
+  key[g] = core[g] ? g + 1 : 0;
+}
+// runs over core nodes: head if its parent is not the previous core node
+__global__ void head_key_kernel(const uint8_t* core, const int64_t* par, const uint64_t* cmax, uint64_t n,
+                                uint64_t* key) {
+  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  uint64_t k = 0;
+  if (core[g]) {
+    const uint64_t prev1 = g ? cmax[g - 1] : 0;  // previous core index + 1
+    const bool cont = prev1 && par[g] == (int64_t)(prev1 - 1);
+    k = cont ? 0 : g + 1;
+  }
+  key[g] = k;
+}
+
+// onpath[i] = 1 if i is a core node inside one of the (descending) intervals
+__global__ void mark_kernel(const uint64_t* ints, const WalkState* ws, uint64_t n, const uint8_t* core,
+                            uint32_t* onpath) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (!core[i]) { onpath[i] = 0; return; }
+  uint64_t ni = ws->n_int;
+  // intervals sorted by descending h (and x); find first with h <= i
+  uint64_t lo = 0, hi = ni;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (ints[2 * mid] > i) lo = mid + 1; else hi = mid;
+  }
+  onpath[i] = (lo < ni && ints[2 * lo + 1] >= i) ? 1u : 0u;
+}
+
+// chain index c (1..) -> walk-space index
+__global__ void scatter_chain_kernel(const uint32_t* onpath, const uint32_t* cpos, uint64_t n,
+                                     const uint64_t* map, uint64_t* chain_g) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !onpath[i]) return;
+  chain_g[1 + cpos[i]] = map ? map[i] : i;
+}
+
+// --------------------------------------------------------------------------
+// full mode: statuses by pointer jumping
+// --------------------------------------------------------------------------
+__global__ void status_init_kernel(const int64_t* par, uint64_t n, uint8_t* st, int64_t* jmp) {
+  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  int64_t p = par[g];
+  st[g] = p == PAR_ROOT ? 1 : (p == PAR_MISS ? 2 : 0);
+  jmp[g] = p;
+}
+__global__ void status_round_kernel(uint64_t n, uint8_t* st, int64_t* jmp, unsigned int* changed) {
+  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n || st[g]) return;
+  int64_t j = jmp[g];
+  uint8_t s = st[j];
+  if (s) st[g] = s;
+  else { jmp[g] = jmp[j]; *changed = 1; }
+}
+__global__ void valid_max_kernel(const uint8_t* st, const uint64_t* d_m, uint64_t n,
+                                 unsigned long long* best_g1, uint32_t* vflag) {
+  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  bool v = st[g] == 1;
+  vflag[g] = v;
+  if (v) atomicMax(best_g1, (unsigned long long)(g + 1));
+}
+// remap parents into the compacted valid space
+__global__ void remap_kernel(const uint64_t* vlist, const uint64_t* nv, const int64_t* par,
+                             const uint64_t* vpos, int64_t* vpar, uint64_t* vslot,
+                             const uint64_t* slot) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *nv) return;
+  uint64_t g = vlist[i];
+  int64_t p = par[g];
+  int64_t vp = p >= 0 ? (int64_t)vpos[p] : p;
+  vpar[i] = vp;
+  vslot[i] = slot[g];
+}
+
+// --------------------------------------------------------------------------
+// 4. finalize: per chain entry outputs + CRC from the per-tile values
+// --------------------------------------------------------------------------
+struct FinArgs {
+  const uint8_t* file;
+  uint64_t flen;
+  uint64_t n_chain;
+  const uint64_t* chain_g;   // [n_chain], entry 0 = root (unused)
+  const uint64_t* slot;      // dense g -> record slot
+  const int64_t* par;        // dense g -> dense parent
+  const WalkState* ws;
+  const uint64_t* c_m;
+  const uint64_t* c_p;
+  const uint64_t* c_kh;
+  const uint32_t* c_crc;
+  const uint32_t* c_sxm;
+  const uint32_t* c_suf;
+  const uint32_t* c_tail;
+  const uint32_t* c_flags;
+  const uint32_t* tileT;
+  const uint32_t* tileSX1;
+  int no_crc;
+  // outputs
+  uint64_t *o_mo, *o_kh, *o_prev, *o_start, *o_len;
+  uint32_t *o_crc_st, *o_crc, *o_pieces;  // o_pieces: bit0 suf ok, bit1 sxm ok, bit2 tail ok (slow path input)
+  uint32_t *o_suf, *o_sxm, *o_tail;
+  uint8_t* o_ok;
+  uint64_t* slow_list;
+  unsigned long long* n_slow;
+  unsigned long long* n_bad;
+};
+
+__device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint32_t suf, uint32_t sxm,
+                                                    uint32_t tail, const uint32_t* tileT) {
+  const uint64_t len = m - s;
+  if (len < 64) return tail ^ g_tabs.zero_crc[len];
+  const uint64_t k0 = s / TILE, k1 = m / TILE;
+  const uint32_t j0 = (uint32_t)((s % TILE) / 64);
+  uint32_t acc = suf ^ g_tabs.winit[j0];
+  uint32_t y;
+  if (k0 == k1) {
+    y = acc ^ sxm;
+  } else {
+    for (uint64_t k = k0 + 1; k < k1; k++) acc = mulp(g_tabs.x32768, acc) ^ tileT[k];
+    y = mulp(g_tabs.x32768, acc) ^ tileT[k1] ^ sxm;
+  }
+  const uint64_t dd = (k1 + 1) * TILE - m;
+  return ~(mulp(g_tabs.invpow[dd], y) ^ tail);
+}
+
+__global__ void finalize_kernel(FinArgs a) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n_chain) return;
+  uint64_t mo, kh, p, start, len;
+  uint32_t crc_st, suf = 0, sxm = 0, tail = 0, pieces = 0;
+  bool tomb;
+  if (c == 0) {
+    const uint64_t t = a.ws->root_t;
+    mo = t - 20;
+    kh = ld_u64_unaligned(a.file, mo);
+    crc_st = ld_u32_unaligned(a.file, mo + 16);
+    p = 0;
+    tomb = false;  // start is 0 either way
+    start = 0;
+    suf = a.tileT[0];
+    pieces = 1;
+  } else {
+    const uint64_t g = a.chain_g[c];
+    const uint64_t gi = a.slot[g];
+    mo = a.c_m[gi];
+    p = a.c_p[gi];
+    kh = a.c_kh[gi];
+    crc_st = a.c_crc[gi];
+    const uint32_t fl = a.c_flags[gi];
+    tomb = fl & F_TOMB;
+    start = tomb ? p : p + prepad64(p);
+    if (fl & F_SXM) { sxm = a.c_sxm[gi]; pieces |= 2; }
+    if (fl & F_TAIL) { tail = a.c_tail[gi]; pieces |= 4; }
+    const int64_t pg = a.par[g];
+    if (pg >= 0) {
+      const uint64_t pgi = a.slot[pg];
+      const uint32_t pf = a.c_flags[pgi];
+      const uint32_t kind = (pf >> F_SUF_SHIFT) & 3;
+      const uint64_t k0 = start / TILE;
+      if (kind == 0) { suf = a.c_suf[pgi]; pieces |= 1; }
+      else if (kind == 1) { suf = a.tileT[k0]; pieces |= 1; }
+      else if (kind == 2) { suf = a.tileSX1[k0]; pieces |= 1; }
+    } else if (start == 0) {
+      suf = a.tileT[0];
+      pieces |= 1;
+    }
+  }
+  len = mo - start;
+  a.o_mo[c] = mo;
+  a.o_kh[c] = kh;
+  a.o_prev[c] = p;
+  a.o_start[c] = start;
+  a.o_len[c] = len;
+  a.o_crc_st[c] = crc_st;
+  if (a.no_crc) { a.o_crc[c] = 0; a.o_ok[c] = 0; return; }
+  if (tomb) {
+    const uint32_t crc = 0xD202EF8Du;  // CRC32(b"\0"): the tombstone byte is 0 by the rule
+    a.o_crc[c] = crc;
+    a.o_ok[c] = crc == crc_st;
+    if (crc != crc_st) atomicAdd(a.n_bad, 1ull);
+    return;
+  }
+  // pieces needed: suf (if len>=64), sxm (if len>=64), tail (always)
+  const bool need_long = len >= 64;
+  const bool have = (pieces & 4) && (!need_long || ((pieces & 1) && (pieces & 2)));
+  if (have) {
+    const uint32_t crc = crc_from_pieces(start, mo, suf, sxm, tail, a.tileT);
+    a.o_crc[c] = crc;
+    a.o_ok[c] = crc == crc_st;
+    if (crc != crc_st) atomicAdd(a.n_bad, 1ull);
+  } else {
+    a.o_pieces[c] = pieces;
+    a.o_suf[c] = suf;
+    a.o_sxm[c] = sxm;
+    a.o_tail[c] = tail;
+    const unsigned long long w = atomicAdd(a.n_slow, 1ull);
+    a.slow_list[w] = c;
+  }
+}
+
+// Recompute, with one wave, the per-tile values of tile k: SX at line j and
+// crc_raw of the first r bytes of line j (r in 0..63).
+__device__ void tile_probe(const uint8_t* file, uint64_t flen, uint64_t k, uint32_t j, uint32_t r,
+                           uint32_t* sx_out, uint32_t* tail_out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t L = k * TILE + 64ull * lane;
+  uint32_t s = 0, tl = 0;
+  for (int q = 0; q < 64; q++) {
+    const uint64_t o = L + q;
+    const uint32_t byte = o < flen ? file[o] : 0u;
+    if (q == (int)r) tl = s;
+    s = g_tabs.tab[0][(s ^ byte) & 0xff] ^ (s >> 8);
+  }
+  uint32_t sx = mulp(g_tabs.lw[lane], s);
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t v = __shfl_down(sx, o);
+    if (lane + o < 64) sx ^= v;
+  }
+  *sx_out = __shfl(sx, (int)j);
+  *tail_out = __shfl(tl, (int)j);
+}
+
+// one wave per slow entry
+__global__ __launch_bounds__(64) void slow_kernel(FinArgs a) {
+  const unsigned long long ns = *a.n_slow;
+  for (uint64_t w = blockIdx.x; w < ns; w += gridDim.x) {
+    const uint64_t c = a.slow_list[w];
+    const uint64_t s = a.o_start[c], m = a.o_mo[c];
+    uint32_t pieces = a.o_pieces[c], suf = a.o_suf[c], sxm = a.o_sxm[c], tail = a.o_tail[c];
+    uint32_t sxv, tv;
+    if (!(pieces & 1)) {
+      tile_probe(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64), 0, &sxv, &tv);
+      suf = sxv;
+    }
+    if (!(pieces & 6) || !(pieces & 2) || !(pieces & 4)) {
+      tile_probe(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64), (uint32_t)(m % 64), &sxv, &tv);
+      if (!(pieces & 2)) sxm = sxv;
+      if (!(pieces & 4)) tail = tv;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      const uint32_t crc = crc_from_pieces(s, m, suf, sxm, tail, a.tileT);
+      a.o_crc[c] = crc;
+      a.o_ok[c] = crc == a.o_crc_st[c];
+      if (crc != a.o_crc_st[c]) atomicAdd(a.n_bad, 1ull);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// 5. KeyIndexer::build -- latest wins, tombstones included
+// --------------------------------------------------------------------------
+constexpr uint64_t EMPTY_KEY = ~0ull;
+
+__global__ void index_insert_kernel(const uint64_t* kh, const uint64_t* mo, uint64_t n, uint64_t* keys,
+                                    unsigned long long* vals, uint64_t mask, unsigned long long* special) {
+  uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const uint64_t k = kh[c];
+  const unsigned long long v = mo[c] + 1;
+  if (k == EMPTY_KEY) { atomicMax(special, v); return; }
+  uint64_t i = xxh3_64_u64(k) & mask;
+  while (true) {
+    unsigned long long old = atomicCAS((unsigned long long*)&keys[i], (unsigned long long)EMPTY_KEY,
+                                       (unsigned long long)k);
+    if (old == EMPTY_KEY || old == k) { atomicMax(&vals[i], v); return; }
+    i = (i + 1) & mask;
+  }
+}
+__global__ void index_latest_kernel(const uint64_t* kh, const uint64_t* mo, uint64_t n, const uint64_t* keys,
+                                    const unsigned long long* vals, uint64_t mask,
+                                    const unsigned long long* special, uint32_t* latest) {
+  uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const uint64_t k = kh[c];
+  const unsigned long long v = mo[c] + 1;
+  unsigned long long best;
+  if (k == EMPTY_KEY) best = *special;
+  else {
+    uint64_t i = xxh3_64_u64(k) & mask;
+    while (keys[i] != k) i = (i + 1) & mask;
+    best = vals[i];
+  }
+  latest[c] = best == v;
+}
+__global__ void index_emit_kernel(const uint64_t* kh, const uint64_t* mo, const uint32_t* latest,
+                                  const uint32_t* pos, uint64_t n, uint64_t* okey, uint64_t* opacked) {
+  uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n || !latest[c]) return;
+  const uint64_t k = kh[c];
+  okey[pos[c]] = k;
+  opacked[pos[c]] = ((k >> 48) << 48) | (mo[c] & 0xFFFFFFFFFFFFull);  // key_indexer.rs:79-85
+}
+
+// --------------------------------------------------------------------------
+// batch digests (compute_checksum / compute_hash_batch)
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t xpow8_dev(uint64_t n) {
+  uint32_t r = kX0;
+  for (int k = 0; n; k++, n >>= 1)
+    if (n & 1) r = mulp(g_tabs.pow8[k], r);
+  return r;
+}
+
+// one wave per range; range bytes may have any alignment
+__global__ __launch_bounds__(64) void crc_batch_kernel(const uint8_t* buf, const uint64_t* offs,
+                                                       const uint64_t* lens, uint64_t n, uint32_t* out) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint8_t* p = buf + offs[i];
+    const uint64_t len = lens[i];
+    uint32_t acc = 0;
+    uint64_t o = 0;
+    for (; o + TILE <= len; o += TILE) {  // full 4 KiB blocks
+      uint32_t s = 0;
+      const uint8_t* q = p + o + 64 * lane;
+      for (int b = 0; b < 64; b++) s = g_tabs.tab[0][(s ^ q[b]) & 0xff] ^ (s >> 8);
+      uint32_t u = mulp(g_tabs.lw[lane], s);
+      for (int w = 32; w > 0; w >>= 1) u ^= __shfl_xor(u, w);
+      acc = mulp(g_tabs.x32768, acc) ^ u;
+    }
+    const uint64_t rem = len - o;
+    // remainder: line i covers [64i, min(64i+64, rem))
+    uint32_t u = 0;
+    const uint64_t ls = 64ull * lane;
+    if (ls < rem) {
+      const uint64_t le = ls + 64 < rem ? ls + 64 : rem;
+      uint32_t s = 0;
+      for (uint64_t b = ls; b < le; b++) s = g_tabs.tab[0][(s ^ p[o + b]) & 0xff] ^ (s >> 8);
+      u = mulp(xpow8_dev(rem - le), s);
+    }
+    for (int w = 32; w > 0; w >>= 1) u ^= __shfl_xor(u, w);
+    if (lane == 0) {
+      const uint32_t raw = mulp(xpow8_dev(rem), acc) ^ u;
+      out[i] = raw ^ ~mulp(xpow8_dev(len), 0xFFFFFFFFu);
+    }
+  }
+}
+
+__global__ void xxh3_batch_kernel(const uint8_t* keys, const uint64_t* offs, const uint64_t* lens, uint64_t n,
+                                  uint64_t* out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = xxh3_64(keys + offs[i], lens[i]);
+}
+
+// --------------------------------------------------------------------------
+// synthetic store writer (checksum-on-append, data_store.rs:847-939)
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t synth_word(uint64_t seed, uint64_t entry, uint64_t word) {
+  uint64_t z = seed + ((entry << 32) + word + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// one wave per entry; entry_off[i] = prev tail (where the prepad starts)
+__global__ __launch_bounds__(64) void synth_kernel(uint8_t* out, const uint64_t* entry_off,
+                                                   const uint64_t* lens, uint64_t fixed_len, uint64_t n,
+                                                   uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint64_t tail = entry_off[i];
+    const uint64_t len = lens ? lens[i] : fixed_len;
+    const uint64_t pad = prepad64(tail);
+    const uint64_t st = tail + pad;  // 64-aligned
+    if (lane < (int)pad) out[tail + lane] = 0;
+    // payload: 8-byte words
+    uint32_t acc = 0;
+    for (uint64_t blk = 0; blk < len; blk += TILE) {
+      const uint64_t ls = blk + 64ull * lane;
+      uint32_t s = 0;
+      uint64_t le = ls + 64 < len ? ls + 64 : len;
+      if (ls < len) {
+        for (uint64_t w = ls / 8; w * 8 < le; w++) {
+          const uint64_t v = synth_word(seed, i, w);
+          const uint64_t nb = le - w * 8 < 8 ? le - w * 8 : 8;
+          if (nb == 8) *(uint64_t*)(out + st + w * 8) = v;  // st is 64-aligned
+          else for (uint64_t b = 0; b < nb; b++) out[st + w * 8 + b] = (uint8_t)(v >> (8 * b));
+          for (uint64_t b = 0; b < nb; b++) s = g_tabs.tab[0][(s ^ (uint32_t)(v >> (8 * b))) & 0xff] ^ (s >> 8);
+        }
+      }
+      const uint64_t bl = len - blk < TILE ? len - blk : TILE;
+      uint32_t u = ls < len ? mulp(xpow8_dev(bl - (le - blk)), s) : 0u;
+      for (int w = 32; w > 0; w >>= 1) u ^= __shfl_xor(u, w);
+      acc = mulp(xpow8_dev(bl), acc) ^ u;
+    }
+    if (lane == 0) {
+      const uint32_t crc = acc ^ ~mulp(xpow8_dev(len), 0xFFFFFFFFu);
+      // key "bench-key-{i}"
+      uint8_t key[32] = {'b', 'e', 'n', 'c', 'h', '-', 'k', 'e', 'y', '-'};
+      uint8_t dig[24];
+      int nd = 0;
+      uint64_t v = i;
+      do { dig[nd++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+      for (int q = 0; q < nd; q++) key[10 + q] = dig[nd - 1 - q];
+      const uint64_t kh = xxh3_64(key, 10 + nd);
+      uint8_t* mb = out + st + len;
+      for (int b = 0; b < 8; b++) mb[b] = (uint8_t)(kh >> (8 * b));
+      for (int b = 0; b < 8; b++) mb[8 + b] = (uint8_t)(tail >> (8 * b));
+      for (int b = 0; b < 4; b++) mb[16 + b] = (uint8_t)(crc >> (8 * b));
+    }
+  }
+}
+
+}  // namespace srd

@@ -1,0 +1,398 @@
+"""Python binding of the MI355X-native validate+index path (include/srd_amd.h).
+
+Mirrors the reference's interface for this path (jzombie/rust-simd-r-drive):
+
+  recover_valid_chain(file)      data_store.rs:383-482  -> final_len
+  KeyIndexer.build(file, tail)   key_indexer.rs:98-124   -> {key_hash: packed}
+  KeyIndexer.tag_from_hash/pack/unpack                   key_indexer.rs:64-93
+  compute_checksum(data)         compute_checksum.rs:15-20 -> 4 LE bytes
+  compute_hash(key)              compute_hash.rs:25-27
+  compute_hash_batch(keys)       compute_hash.rs:64-77
+  DataStore.open(path)           data_store.rs:84-117 (mmap -> recover ->
+                                 truncate + re-open -> index), with every chain
+                                 payload's CRC verified on the GPU
+  EntryHandle.is_valid_checksum  entry_handle.rs:260-275
+
+All compute runs in libsrd_amd.so (HIP, gfx950).  There is no CPU fallback:
+if the library or a GPU is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import mmap as _mmap
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libsrd_amd.so")
+
+SRD_FLAG_FORCE_FULL = 1
+SRD_FLAG_NO_CRC = 2
+METADATA_SIZE = 20
+NULL_BYTE = b"\x00"
+TAG_BITS = 16
+OFFSET_MASK = (1 << 48) - 1
+
+# symbols include/srd_amd.h declares
+EXPORTS = [
+    "srd_ctx_create", "srd_ctx_destroy", "srd_ctx_stream", "srd_last_error", "srd_ctx_timings",
+    "srd_validate_index_device", "srd_validate_index", "srd_result_free",
+    "srd_recover_valid_chain", "srd_key_indexer_build", "srd_crc32_batch",
+    "srd_crc32_batch_device", "srd_xxh3_64_batch", "srd_xxh3_64_batch_device",
+    "srd_synth_store_device", "srd_selftest_host",
+]
+
+
+class DeviceResult(C.Structure):
+    _fields_ = [
+        ("file_len", C.c_uint64), ("final_len", C.c_uint64), ("n_chain", C.c_uint64),
+        ("n_index", C.c_uint64), ("n_crc_bad", C.c_uint64), ("n_candidates", C.c_uint64),
+        ("n_weak", C.c_uint64), ("mode", C.c_uint32), ("reserved", C.c_uint32),
+        ("meta_off", C.c_void_p), ("key_hash", C.c_void_p), ("prev_offset", C.c_void_p),
+        ("payload_start", C.c_void_p), ("payload_len", C.c_void_p),
+        ("crc_stored", C.c_void_p), ("crc_computed", C.c_void_p), ("crc_ok", C.c_void_p),
+        ("index_key_hash", C.c_void_p), ("index_packed", C.c_void_p),
+    ]
+
+
+def build() -> str:
+    """Compile the HIP library in-tree (hipcc --offload-arch=gfx950)."""
+    subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `make -C {HERE}` (no CPU fallback exists)")
+        # One HIP runtime per process: if PyTorch is present, load it first so
+        # that libsrd_amd.so binds to the libamdhip64.so.7 torch already mapped
+        # (torch NEEDs "libamdhip64.so", we NEED the soname "libamdhip64.so.7";
+        # loading us first would map a second runtime from /opt/rocm).
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        L = C.CDLL(LIB_PATH)
+        vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+        L.srd_ctx_create.argtypes = [i32, C.POINTER(vp)]
+        L.srd_ctx_destroy.argtypes = [vp]
+        L.srd_ctx_stream.argtypes = [vp]
+        L.srd_ctx_stream.restype = vp
+        L.srd_last_error.restype = C.c_char_p
+        L.srd_ctx_timings.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double)]
+        L.srd_validate_index_device.argtypes = [vp, vp, u64, u32, C.POINTER(DeviceResult)]
+        L.srd_validate_index.argtypes = [vp, vp, u64, u32, C.POINTER(DeviceResult)]
+        L.srd_result_free.argtypes = [C.POINTER(DeviceResult)]
+        L.srd_recover_valid_chain.argtypes = [vp, vp, u64, C.POINTER(u64)]
+        L.srd_key_indexer_build.argtypes = [vp, vp, u64, vp, vp, u64, C.POINTER(u64)]
+        L.srd_crc32_batch.argtypes = [vp, vp, u64, vp, vp, u64, vp]
+        L.srd_crc32_batch_device.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+        L.srd_xxh3_64_batch.argtypes = [vp, vp, u64, vp, vp, u64, vp]
+        L.srd_xxh3_64_batch_device.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+        L.srd_synth_store_device.argtypes = [vp, vp, u64, u64, vp, u64, C.POINTER(u64)]
+        for f in EXPORTS:
+            if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error"):
+                getattr(L, f).restype = i32
+        _lib = L
+    return _lib
+
+
+class SrdError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != 0:
+        raise SrdError(f"srd error {rc}: {lib().srd_last_error().decode()}")
+
+
+class Context:
+    """One GPU + stream + reusable HBM workspace (srd_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.h = C.c_void_p()
+        _check(lib().srd_ctx_create(device, C.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            lib().srd_ctx_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def timings(self):
+        """(scan_ms, scan_launches, total_ms) of the last validate call (HIP events)."""
+        a, n, b = C.c_double(), C.c_int(), C.c_double()
+        _check(lib().srd_ctx_timings(self.h, C.byref(a), C.byref(n), C.byref(b)))
+        return a.value, n.value, b.value
+
+    @property
+    def stream(self) -> int:
+        return lib().srd_ctx_stream(self.h)
+
+
+_default_ctx = None
+
+
+def default_ctx() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(int(os.environ.get("SRD_DEVICE", "0")))
+    return _default_ctx
+
+
+def _u8(file) -> np.ndarray:
+    if isinstance(file, np.ndarray):
+        return np.ascontiguousarray(file, dtype=np.uint8).reshape(-1)
+    return np.frombuffer(memoryview(file), dtype=np.uint8)
+
+
+def _ptr(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data) if a.size else C.c_void_p(0)
+
+
+class Result:
+    """Host copy of srd_result: the recovered tail, the chain and the index."""
+
+    def __init__(self, r: DeviceResult):
+        self.file_len = r.file_len
+        self.final_len = r.final_len
+        self.n_chain = r.n_chain
+        self.n_index = r.n_index
+        self.n_crc_bad = r.n_crc_bad
+        self.n_candidates = r.n_candidates
+        self.n_weak = r.n_weak
+        self.mode = r.mode
+
+        def arr(p, n, dt):
+            if n == 0 or not p:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), (n,)).copy()
+
+        n, ni = r.n_chain, r.n_index
+        self.meta_off = arr(r.meta_off, n, np.uint64)
+        self.key_hash = arr(r.key_hash, n, np.uint64)
+        self.prev_offset = arr(r.prev_offset, n, np.uint64)
+        self.payload_start = arr(r.payload_start, n, np.uint64)
+        self.payload_len = arr(r.payload_len, n, np.uint64)
+        self.crc_stored = arr(r.crc_stored, n, np.uint32)
+        self.crc_computed = arr(r.crc_computed, n, np.uint32)
+        self.crc_ok = arr(r.crc_ok, n, np.uint8)
+        self.index_key_hash = arr(r.index_key_hash, ni, np.uint64)
+        self.index_packed = arr(r.index_packed, ni, np.uint64)
+
+    def index(self) -> dict[int, int]:
+        return {int(k): int(v) for k, v in zip(self.index_key_hash, self.index_packed)}
+
+    def chain(self) -> list[dict]:
+        keys = ["meta_off", "key_hash", "prev_offset", "payload_start", "payload_len",
+                "crc_stored", "crc_computed", "crc_ok"]
+        return [{k: int(getattr(self, k)[i]) for k in keys} for i in range(self.n_chain)]
+
+
+def validate_index(file, flags: int = 0, ctx: Context | None = None) -> Result:
+    """The fused open-time pass: recover_valid_chain + KeyIndexer::build +
+    is_valid_checksum over every chain entry, on the GPU."""
+    ctx = ctx or default_ctx()
+    a = _u8(file)
+    r = DeviceResult()
+    _check(lib().srd_validate_index(ctx.h, _ptr(a), a.size, flags, C.byref(r)))
+    try:
+        return Result(r)
+    finally:
+        lib().srd_result_free(C.byref(r))
+
+
+def validate_index_device(d_ptr: int, file_len: int, flags: int = 0, ctx: Context | None = None) -> DeviceResult:
+    """Device-resident variant: d_ptr is a device pointer (e.g. a torch
+    uint8 CUDA tensor's data_ptr()).  Result arrays stay in HBM."""
+    ctx = ctx or default_ctx()
+    r = DeviceResult()
+    _check(lib().srd_validate_index_device(ctx.h, C.c_void_p(d_ptr), file_len, flags, C.byref(r)))
+    return r
+
+
+def recover_valid_chain(file, ctx: Context | None = None) -> int:
+    """data_store.rs:383-482: the largest valid tail <= file_len (0 if none)."""
+    ctx = ctx or default_ctx()
+    a = _u8(file)
+    out = C.c_uint64()
+    _check(lib().srd_recover_valid_chain(ctx.h, _ptr(a), a.size, C.byref(out)))
+    return out.value
+
+
+def compute_hash_batch(keys, ctx: Context | None = None) -> list[int]:
+    """compute_hash.rs:64-77"""
+    ctx = ctx or default_ctx()
+    keys = [bytes(k) for k in keys]
+    buf = np.frombuffer(b"".join(keys) or b"\x00", np.uint8)
+    lens = np.array([len(k) for k in keys], np.uint64)
+    offs = np.zeros(len(keys), np.uint64)
+    if len(keys) > 1:
+        offs[1:] = np.cumsum(lens)[:-1]
+    out = np.zeros(max(len(keys), 1), np.uint64)
+    _check(lib().srd_xxh3_64_batch(ctx.h, _ptr(buf), buf.size, _ptr(offs), _ptr(lens), len(keys), _ptr(out)))
+    return [int(x) for x in out[: len(keys)]]
+
+
+def compute_hash(key: bytes) -> int:
+    """compute_hash.rs:25-27"""
+    return compute_hash_batch([key])[0]
+
+
+def crc32_batch(buf, offs, lens, ctx: Context | None = None) -> np.ndarray:
+    ctx = ctx or default_ctx()
+    a = _u8(buf)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint64)
+    out = np.zeros(max(len(offs), 1), np.uint32)
+    _check(lib().srd_crc32_batch(ctx.h, _ptr(a), a.size, _ptr(offs), _ptr(lens), len(offs), _ptr(out)))
+    return out[: len(offs)]
+
+
+def compute_checksum(data: bytes) -> bytes:
+    """compute_checksum.rs:15-20: CRC-32 as 4 little-endian bytes."""
+    d = bytes(data)
+    v = int(crc32_batch(np.frombuffer(d or b"\x00", np.uint8), [0], [len(d)])[0])
+    return v.to_bytes(4, "little")
+
+
+class KeyIndexer:
+    """key_indexer.rs: key_hash -> (tag16 << 48 | offset48)."""
+
+    def __init__(self, index: dict[int, int]):
+        self.index = index
+
+    @staticmethod
+    def tag_from_hash(key_hash: int) -> int:
+        return key_hash >> (64 - TAG_BITS)
+
+    @staticmethod
+    def pack(tag: int, offset: int) -> int:
+        return (tag << (64 - TAG_BITS)) | offset
+
+    @staticmethod
+    def unpack(packed: int) -> tuple[int, int]:
+        return packed >> (64 - TAG_BITS), packed & OFFSET_MASK
+
+    @classmethod
+    def build(cls, file, tail: int, ctx: Context | None = None) -> "KeyIndexer":
+        ctx = ctx or default_ctx()
+        a = _u8(file)
+        cap = max(1, tail // METADATA_SIZE + 1)
+        k = np.zeros(cap, np.uint64)
+        v = np.zeros(cap, np.uint64)
+        n = C.c_uint64()
+        _check(lib().srd_key_indexer_build(ctx.h, _ptr(a), tail, _ptr(k), _ptr(v), cap, C.byref(n)))
+        return cls({int(k[i]): int(v[i]) for i in range(n.value)})
+
+    def get_packed(self, key_hash: int):
+        return self.index.get(key_hash)
+
+    def get_offset(self, key_hash: int):
+        p = self.index.get(key_hash)
+        return None if p is None else p & OFFSET_MASK
+
+    def __len__(self):
+        return len(self.index)
+
+
+class EntryHandle:
+    def __init__(self, store: "DataStore", i: int):
+        self.store, self.i = store, i
+        r = store.result
+        self.metadata_offset = int(r.meta_off[i])
+        self.start_offset = int(r.payload_start[i])
+        self.end_offset = self.metadata_offset
+        self.key_hash = int(r.key_hash[i])
+
+    def as_slice(self) -> bytes:
+        return bytes(self.store.mm[self.start_offset:self.end_offset])
+
+    def checksum(self) -> int:
+        return int(self.store.result.crc_stored[self.i])
+
+    def is_valid_checksum(self) -> bool:
+        """entry_handle.rs:260-275, computed on the GPU during open."""
+        return bool(self.store.result.crc_ok[self.i])
+
+
+class DataStore:
+    """The part of DataStore::open (data_store.rs:84-117) this path replaces."""
+
+    def __init__(self, path, mm, result: Result):
+        self.path, self.mm, self.result = path, mm, result
+        self.tail_offset = result.final_len
+        self.key_indexer = KeyIndexer(result.index())
+        self._pos = {int(m): i for i, m in enumerate(result.meta_off)}
+
+    @classmethod
+    def open(cls, path, ctx: Context | None = None) -> "DataStore":
+        with open(path, "a+b"):
+            pass
+        size = os.path.getsize(path)
+        with open(path, "r+b") as f:
+            mm = _mmap.mmap(f.fileno(), 0, access=_mmap.ACCESS_READ) if size else b""
+            res = validate_index(np.frombuffer(mm, np.uint8) if size else b"", ctx=ctx)
+        if res.final_len < size:
+            # data_store.rs:91-104: warn, truncate to the valid tail, re-open
+            import warnings
+            warnings.warn(f"Truncating corrupted data in {path} from offset {res.final_len} to {size}.")
+            if size and hasattr(mm, "close"):
+                mm.close()
+            with open(path, "r+b") as f:
+                f.truncate(res.final_len)
+                os.fsync(f.fileno())
+            return cls.open(path, ctx)
+        return cls(path, mm, res)
+
+    def read_entry(self, key_hash: int):
+        packed = self.key_indexer.get_packed(key_hash)
+        if packed is None:
+            return None
+        tag, off = KeyIndexer.unpack(packed)
+        if tag != KeyIndexer.tag_from_hash(key_hash):
+            return None
+        i = self._pos[off]
+        if int(self.result.payload_len[i]) == 1 and self.mm[int(self.result.payload_start[i])] == 0:
+            return None  # tombstone
+        return EntryHandle(self, i)
+
+    def read(self, key: bytes):
+        return self.read_entry(compute_hash(key))
+
+    def len(self) -> int:
+        return len(self.key_indexer)
+
+
+def synth_store_len(n_entries: int, payload_len: int = 4096, lens=None) -> int:
+    out = C.c_uint64()
+    lp = None
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, np.uint64)
+        lp = _ptr(lens)
+    _check(lib().srd_synth_store_device(C.c_void_p(0), None, n_entries, payload_len, lp, 0, C.byref(out)))
+    return out.value
+
+
+def synth_store_device(d_ptr: int, n_entries: int, payload_len: int = 4096, lens=None,
+                       seed: int = 0x5EED0001, ctx: Context | None = None) -> int:
+    ctx = ctx or default_ctx()
+    out = C.c_uint64()
+    lp = None
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, np.uint64)
+        lp = _ptr(lens)
+    _check(lib().srd_synth_store_device(ctx.h, C.c_void_p(d_ptr), n_entries, payload_len, lp, seed, C.byref(out)))
+    return out.value

@@ -1,0 +1,211 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+golden fixtures.  Bit-exact for every integer output: final_len, the chain
+(meta_off, key_hash, prev_offset, payload_start, payload_len, stored and
+computed CRC, crc_ok) and the KeyIndexer map."""
+import os
+import random
+import struct
+import zlib
+
+import numpy as np
+import pytest
+import xxhash
+
+import oracle as O
+import srd_amd as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = S.Context(0)
+    yield c
+    c.close()
+
+
+def check_against_oracle(data, ctx, flags=0, name=""):
+    a = O.as_u8(data)
+    want_len = O.recover_valid_chain(a)
+    r = S.validate_index(a, flags, ctx)
+    assert r.final_len == want_len, (name, r.final_len, want_len)
+    ch = O.chain(a, want_len)
+    assert r.n_chain == len(ch), (name, r.n_chain, len(ch))
+    if ch:
+        for k in ("meta_off", "key_hash", "prev_offset", "payload_start", "payload_len", "crc_stored",
+                  "crc_computed", "crc_ok"):
+            got = getattr(r, k).astype(np.uint64)
+            exp = np.array([e[k] for e in ch], np.uint64)
+            bad = np.nonzero(got != exp)[0]
+            assert bad.size == 0, (name, k, bad[:5], got[bad[:5]], exp[bad[:5]])
+    assert r.index() == O.key_indexer_build(a, want_len), name
+    assert r.n_crc_bad == sum(1 - e["crc_ok"] for e in ch)
+    return r
+
+
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_golden_fixtures(golden_cases, ctx, flags):
+    for name, (data, m) in golden_cases.items():
+        r = S.validate_index(data, flags, ctx)
+        assert r.final_len == m["final_len"], name
+        assert r.n_chain == len(m["chain"]), name
+        for i, e in enumerate(m["chain"]):
+            assert int(r.meta_off[i]) == e["meta_off"], name
+            assert int(r.key_hash[i]) == int(e["key_hash"], 16), name
+            assert int(r.payload_start[i]) == e["payload_start"], name
+            assert int(r.payload_len[i]) == e["payload_len"], name
+            assert int(r.crc_stored[i]) == e["crc_stored"], name
+            assert int(r.crc_computed[i]) == e["crc_computed"], (name, i)
+            assert int(r.crc_ok[i]) == e["crc_ok"], name
+        assert r.index() == {int(k, 16): int(v, 16) for k, v in m["index"].items()}, name
+
+
+def test_recover_and_key_indexer_api(golden_cases, ctx):
+    for name, (data, m) in golden_cases.items():
+        assert S.recover_valid_chain(data, ctx) == m["final_len"], name
+        ki = S.KeyIndexer.build(data[: m["final_len"]], m["final_len"], ctx)
+        assert ki.index == {int(k, 16): int(v, 16) for k, v in m["index"].items()}, name
+
+
+def test_xxh3_reference_goldens(ref_goldens, ctx):
+    # tests/hash_stability_tests.rs:16-72 through compute_hash_batch
+    keys = [bytes.fromhex(k) for k in ref_goldens["xxh3_64"]]
+    got = S.compute_hash_batch(keys, ctx)
+    assert got == [int(v, 16) for v in ref_goldens["xxh3_64"].values()]
+    for g in ref_goldens["namespace"]:  # hash_stability_tests.rs:76-100
+        a, b = S.compute_hash_batch([g["prefix"].encode(), g["key"].encode()], ctx)
+        assert struct.pack("<QQ", a, b).hex() == g["out"]
+
+
+def test_xxh3_random_lengths(ctx):
+    rnd = random.Random(7)
+    keys = [rnd.randbytes(n) for n in list(range(0, 260)) + [300, 1000, 1024, 1025, 2048, 5000]]
+    assert S.compute_hash_batch(keys, ctx) == [xxhash.xxh3_64_intdigest(k) for k in keys]
+
+
+def test_crc32_batch(ref_goldens, ctx):
+    rnd = random.Random(3)
+    buf = rnd.randbytes(300_000)
+    offs, lens = [], []
+    for n in list(range(0, 130)) + [4095, 4096, 4097, 8192 + 5, 100_000]:
+        o = rnd.randrange(0, len(buf) - n)
+        offs.append(o)
+        lens.append(n)
+    got = S.crc32_batch(buf, offs, lens, ctx)
+    assert [int(x) for x in got] == [zlib.crc32(buf[o:o + n]) for o, n in zip(offs, lens)]
+    for hexd, want in ref_goldens["crc32"].items():
+        assert S.compute_checksum(bytes.fromhex(hexd)) == int(want, 16).to_bytes(4, "little")
+
+
+def _device_synth(n, payload_len=4096, lens=None):
+    import torch
+    size = S.synth_store_len(n, payload_len, lens)
+    t = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    S.synth_store_device(t.data_ptr(), n, payload_len, lens)
+    torch.cuda.synchronize()
+    return t[:size].cpu().numpy()
+
+
+def test_device_writer_matches_oracle():
+    # checksum-on-append writer (data_store.rs:847-939) vs the oracle writer
+    assert np.array_equal(_device_synth(300), O.synth_store(300))
+    lens = np.array([1, 2, 3, 63, 64, 65, 100, 4095, 4096, 4097, 9000, 70000, 5, 1 << 17], np.uint64)
+    assert np.array_equal(_device_synth(len(lens), lens=lens), O.synth_store(len(lens), lens=lens))
+
+
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_c1_store(ctx, flags):
+    check_against_oracle(O.synth_store(1000), ctx, flags, "c1")
+
+
+def _zipf_lens(n, seed=0x5EED0003, s=2.0):
+    # C3 shape: 2^k, k=6..20, Zipf over r=k-5; L = 2^k - j for k>=7
+    rng = np.random.default_rng(seed)
+    r = np.arange(1, 16)
+    p = 1.0 / r ** s
+    p /= p.sum()
+    k = rng.choice(np.arange(6, 21), size=n, p=p)
+    j = rng.integers(0, 64, size=n)
+    L = (1 << k) - np.where(k >= 7, j, 0)
+    return L.astype(np.uint64)
+
+
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_mixed_sizes(ctx, flags):
+    lens = _zipf_lens(3000)
+    check_against_oracle(O.synth_store(len(lens), lens=lens), ctx, flags, "zipf")
+
+
+def test_tombstones_and_overwrites_random(ctx):
+    rnd = random.Random(11)
+    buf = bytearray()
+    t = 0
+    for step in range(400):
+        k = rnd.randrange(60)
+        kh = xxhash.xxh3_64_intdigest(b"key%d" % k)
+        if rnd.random() < 0.2:
+            t = O.write_entries(buf, t, [(kh, b"\x00")], allow_null=True)
+        else:
+            n = rnd.choice([1, 3, 8, 20, 64, 100, 700, 4096, 5000])
+            pl = bytes(rnd.choice([0, 0, 0, 1, 2, 255]) for _ in range(n)) if rnd.random() < 0.5 else rnd.randbytes(n)
+            if pl == b"\x00":
+                pl = b"\x01"
+            t = O.write_entries(buf, t, [(kh, pl)])
+    for flags in (0, S.SRD_FLAG_FORCE_FULL):
+        check_against_oracle(bytes(buf), ctx, flags, "tomb")
+
+
+def test_torn_and_corrupted(ctx):
+    rnd = random.Random(5)
+    base = O.synth_store(40)
+    lens = _zipf_lens(60, seed=9)
+    mixed = O.synth_store(len(lens), lens=lens)
+    for store in (base, mixed):
+        for _ in range(12):
+            cut = rnd.randrange(1, store.size)
+            check_against_oracle(store[:cut], ctx, 0, "cut%d" % cut)
+        for _ in range(6):
+            b = store.copy()
+            pos = rnd.randrange(b.size)
+            b[pos] ^= 1 << rnd.randrange(8)
+            check_against_oracle(b, ctx, 0, "flip%d" % pos)
+        check_against_oracle(np.concatenate([store, np.frombuffer(b"CORRUPT", np.uint8)]), ctx, 0, "corrupt")
+
+
+def test_datastore_open_truncates_torn_tail(tmp_path, ctx):
+    # persistence_tests.rs:126-173
+    p = tmp_path / "store.bin"
+    s = O.synth_store(20, 100)
+    p.write_bytes(s.tobytes() + b"CORRUPT")
+    with pytest.warns(UserWarning):
+        ds = S.DataStore.open(str(p), ctx)
+    assert os.path.getsize(p) == s.size and ds.tail_offset == s.size
+    e = ds.read(b"bench-key-7")
+    assert e is not None and e.is_valid_checksum()
+    assert ds.len() == 20
+
+
+def test_full_size_c2_properties(ctx):
+    """C2 (1M x 4 KiB, 4.06 GiB) device-resident, checked by size-independent
+    properties + a sampled oracle comparison."""
+    import torch
+    n = 1 << 20
+    size = S.synth_store_len(n)
+    t = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    S.synth_store_device(t.data_ptr(), n, 4096, ctx=ctx)
+    torch.cuda.synchronize()
+    r = S.validate_index_device(t.data_ptr(), size, 0, ctx)
+    assert (r.final_len, r.n_chain, r.n_index, r.n_crc_bad, r.mode) == (size, n, n, 0, 0)
+    host = t[:size].cpu().numpy()
+    st = O.validate_index(host, 8)
+    assert (st.final_len, st.n_chain, st.n_index, st.n_crc_bad) == (size, n, n, 0)
+    # flip one payload byte deep in the store -> exactly one bad CRC
+    pos = 4160 * 777_777 + 1234
+    t[pos] ^= 0x40
+    r = S.validate_index_device(t.data_ptr(), size, 0, ctx)
+    assert (r.final_len, r.n_chain, r.n_crc_bad) == (size, n, 1)
+    # torn tail: drop the last 100 bytes -> oracle decides final_len
+    cut = size - 100
+    r = S.validate_index_device(t.data_ptr(), cut, 0, ctx)
+    host[pos] ^= 0x40
+    assert r.final_len == O.recover_valid_chain(host[:cut])
