@@ -45,6 +45,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   std::vector<Buf> bufs;  // indexed by the enum below
   uint32_t cap = 256;     // candidate slots per span
+  unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -55,8 +56,8 @@ struct Ctx {
 };
 
 enum BufId {
-  B_TILE_T, B_TILE_SX1, B_SPAN_COUNT, B_SPAN_BASE,
-  B_CM, B_CP, B_CKH, B_CCRC, B_CSXM, B_CSUF, B_CTAIL, B_CFLAGS,
+  B_TILE, B_SPAN_COUNT, B_SPAN_BASE,
+  B_CM, B_CREC,
   B_COUNTERS,  // [0]=max_root [1]=n_weak [2]=overflow [3]=best_g1 [4]=changed [5]=n_slow [6]=n_bad [7]=special
   B_DM, B_DPAR, B_DSLOT, B_DHEAD, B_RUNHEAD, B_INTS, B_WALK,
   B_ST, B_JMP, B_VFLAG, B_VLIST, B_NV, B_VPOS, B_VPAR, B_VHEAD, B_VSLOT,
@@ -107,6 +108,10 @@ int upload_tables() {
   t.x32768 = g_host_tabs.x32768;
   memcpy(t.pow8, g_host_tabs.pow8, sizeof t.pow8);
   memcpy(t.invpow, g_host_tabs.invpow, sizeof t.invpow);
+  for (int pos = 0; pos < 8; pos++)
+    for (int nb = 0; nb < 16; nb++)
+      for (int l = 0; l < 64; l++)
+        t.nib[((pos * 16 + nb) << 6) + l] = mulp(g_host_tabs.lw[l], (uint32_t)nb << (4 * pos));
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_tabs), &t, sizeof t));
   uploaded |= 1ull << dev;
   (void)rc;
@@ -156,7 +161,7 @@ int walk_and_mark(Ctx* c, const int64_t* par, const uint64_t* slot, uint64_t n, 
   tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint64_t>(c, B_RUNHEAD),
                                            hipcub::Max(), (int)n, c->stream));
-  walk_kernel<<<1, 64, 0, c->stream>>>(par, P<uint64_t>(c, B_RUNHEAD), slot, P<uint64_t>(c, B_CP),
+  walk_kernel<<<1, 64, 0, c->stream>>>(par, P<uint64_t>(c, B_RUNHEAD), slot, P<u32x4>(c, B_CREC),
                                        P<uint64_t>(c, B_INTS), ws, n);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(hws, ws, sizeof(WalkState), hipMemcpyDeviceToHost, c->stream));
@@ -199,6 +204,9 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   int r = upload_tables();
   if (r) { delete c; return r; }
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    c->scan_blocks = (unsigned)ncu;
   *out = c;
   return 0;
 }
@@ -219,18 +227,11 @@ extern "C" void* srd_ctx_stream(srd_ctx* c) { return c ? (void*)c->stream : null
 
 static int alloc_scan(Ctx* c, uint64_t n_tiles, uint64_t n_spans) {
   const uint64_t slots = n_spans * c->cap;
-  TRY(ensure(c, B_TILE_T, n_tiles * 4));
-  TRY(ensure(c, B_TILE_SX1, n_tiles * 4));
+  TRY(ensure(c, B_TILE, n_tiles * 8));
   TRY(ensure(c, B_SPAN_COUNT, (n_spans + 1) * 4));
   TRY(ensure(c, B_SPAN_BASE, (n_spans + 1) * 8));
   TRY(ensure(c, B_CM, slots * 8));
-  TRY(ensure(c, B_CP, slots * 8));
-  TRY(ensure(c, B_CKH, slots * 8));
-  TRY(ensure(c, B_CCRC, slots * 4));
-  TRY(ensure(c, B_CSXM, slots * 4));
-  TRY(ensure(c, B_CSUF, slots * 4));
-  TRY(ensure(c, B_CTAIL, slots * 4));
-  TRY(ensure(c, B_CFLAGS, slots * 4));
+  TRY(ensure(c, B_CREC, slots * 32));
   TRY(ensure(c, B_COUNTERS, 8 * 8));
   TRY(ensure(c, B_WALK, sizeof(WalkState)));
   return 0;
@@ -292,15 +293,8 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
   f.par = P<int64_t>(c, B_DPAR);
   f.ws = P<WalkState>(c, B_WALK);
   f.c_m = P<uint64_t>(c, B_CM);
-  f.c_p = P<uint64_t>(c, B_CP);
-  f.c_kh = P<uint64_t>(c, B_CKH);
-  f.c_crc = P<uint32_t>(c, B_CCRC);
-  f.c_sxm = P<uint32_t>(c, B_CSXM);
-  f.c_suf = P<uint32_t>(c, B_CSUF);
-  f.c_tail = P<uint32_t>(c, B_CTAIL);
-  f.c_flags = P<uint32_t>(c, B_CFLAGS);
-  f.tileT = P<uint32_t>(c, B_TILE_T);
-  f.tileSX1 = P<uint32_t>(c, B_TILE_SX1);
+  f.c_rec = P<u32x4>(c, B_CREC);
+  f.tile = P<uint32_t>(c, B_TILE);
   f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
   f.o_mo = P<uint64_t>(c, B_O_MO);
   f.o_kh = P<uint64_t>(c, B_O_KH);
@@ -398,27 +392,18 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.n_tiles = n_tiles;
     a.n_spans = n_spans;
     a.cap = c->cap;
-    a.tileT = P<uint32_t>(c, B_TILE_T);
-    a.tileSX1 = P<uint32_t>(c, B_TILE_SX1);
+    a.tile = P<uint32_t>(c, B_TILE);
     a.span_count = P<uint32_t>(c, B_SPAN_COUNT);
     a.c_m = P<uint64_t>(c, B_CM);
-    a.c_p = P<uint64_t>(c, B_CP);
-    a.c_kh = P<uint64_t>(c, B_CKH);
-    a.c_crc = P<uint32_t>(c, B_CCRC);
-    a.c_sxm = P<uint32_t>(c, B_CSXM);
-    a.c_suf = P<uint32_t>(c, B_CSUF);
-    a.c_tail = P<uint32_t>(c, B_CTAIL);
-    a.c_flags = P<uint32_t>(c, B_CFLAGS);
-    a.max_root = (unsigned long long*)(cnt + 0);
-    a.n_weak = (unsigned long long*)(cnt + 1);
-    a.overflow = (unsigned int*)(cnt + 2);
+    a.c_rec = P<u32x4>(c, B_CREC);
+    a.counters = (unsigned long long*)cnt;
     if (n_spans) {
-      unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES - 1) / SCAN_WAVES, 512);
+      unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
       if (full)
-        scan_kernel<true><<<g, SCAN_WAVES * 64, 0, c->stream>>>(a);
+        scan_kernel<true><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
       else
-        scan_kernel<false><<<g, SCAN_WAVES * 64, 0, c->stream>>>(a);
+        scan_kernel<false><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev[1], c->stream));
     }
@@ -447,7 +432,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     l.span_count = P<uint32_t>(c, B_SPAN_COUNT);
     l.span_base = P<uint64_t>(c, B_SPAN_BASE);
     l.c_m = P<uint64_t>(c, B_CM);
-    l.c_p = P<uint64_t>(c, B_CP);
+    l.c_rec = P<u32x4>(c, B_CREC);
     l.d_m = P<uint64_t>(c, B_DM);
     l.d_par = P<int64_t>(c, B_DPAR);
     l.d_slot = P<uint64_t>(c, B_DSLOT);

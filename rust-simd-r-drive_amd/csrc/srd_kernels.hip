@@ -54,6 +54,7 @@ struct DevTables {
   uint32_t x32768;
   uint32_t pow8[64];
   uint32_t invpow[4097];
+  uint32_t nib[8 * 16 * 64];       // lane-weight nibble tables
 };
 __device__ DevTables g_tabs;
 
@@ -62,20 +63,11 @@ struct ScanArgs {
   uint64_t flen;
   uint64_t n_tiles, n_spans;
   uint32_t cap;
-  uint32_t* tileT;
-  uint32_t* tileSX1;
+  uint32_t* tile;                  // [2*n_tiles]: SX_0 (= tile CRC), SX_1
   uint32_t* span_count;
-  uint64_t* c_m;
-  uint64_t* c_p;
-  uint64_t* c_kh;
-  uint32_t* c_crc;
-  uint32_t* c_sxm;
-  uint32_t* c_suf;
-  uint32_t* c_tail;
-  uint32_t* c_flags;
-  unsigned long long* max_root;
-  unsigned long long* n_weak;
-  unsigned int* overflow;
+  uint64_t* c_m;                   // [n_spans*cap] candidate metadata offsets
+  u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
+  unsigned long long* counters;    // [0] max root tail, [1] weak, [2] overflow
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -112,193 +104,207 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // --------------------------------------------------------------------------
 // 1. the fused streaming scan
 // --------------------------------------------------------------------------
-template <bool FULL>
-__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_kernel(ScanArgs a) {
-  __shared__ uint32_t s_tab[4 * 256 * REPL];
-  __shared__ uint32_t s_win[SCAN_WAVES][24];
-  __shared__ uint32_t s_tslot[SCAN_WAVES][TCAP];
-  __shared__ uint32_t s_tinfo[SCAN_WAVES][TCAP];
+// LDS: slice-by-4 CRC tables replicated REPL times (lane l reads copy l%REPL,
+// so the 32 lanes of a ds_read_b32 group hit at most 2 distinct addresses per
+// bank), the lane-weight nibble tables (entry (pos,nib) of lane l at word
+// ((pos*16+nib)*64 + l): every lane its own bank, conflict-free) and one
+// 25-dword window per wave for the cooperative candidate check.
+constexpr int SCAN_WAVES_V2 = 16;
+struct ScanLds {
+  uint32_t tab[4 * 256 * REPL];
+  uint32_t nib[8 * 16 * 64];
+  uint32_t win[SCAN_WAVES_V2][28];
+};
 
-  for (int i = threadIdx.x; i < 4 * 256 * REPL; i += blockDim.x)
-    s_tab[i] = (&g_tabs.tab[0][0])[i / REPL];
+__device__ __forceinline__ uint32_t crc_line(const uint32_t (&d)[16], const uint32_t* __restrict__ tab,
+                                             uint32_t cpy) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    s ^= d[j];
+    s = tab[((3 << 8) + (s & 0xff)) * REPL + cpy] ^ tab[((2 << 8) + ((s >> 8) & 0xff)) * REPL + cpy] ^
+        tab[((1 << 8) + ((s >> 16) & 0xff)) * REPL + cpy] ^ tab[(s >> 24) * REPL + cpy];
+  }
+  return s;
+}
+
+// c * x^(512*(63-lane)) via 8 nibble lookups
+__device__ __forceinline__ uint32_t lane_weight(uint32_t c, const uint32_t* __restrict__ nib, int lane) {
+  uint32_t u = 0;
+#pragma unroll
+  for (int pos = 0; pos < 8; pos++) u ^= nib[((pos * 16 + ((c >> (4 * pos)) & 15)) << 6) + lane];
+  return u;
+}
+
+template <bool FULL>
+__global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
+  __shared__ ScanLds lds;
+  for (int i = threadIdx.x; i < 4 * 256 * REPL; i += blockDim.x) lds.tab[i] = (&g_tabs.tab[0][0])[i / REPL];
+  for (int i = threadIdx.x; i < 8 * 16 * 64; i += blockDim.x) lds.nib[i] = g_tabs.nib[i];
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const uint32_t cpy = lane & (REPL - 1);
-  const uint32_t lwl = g_tabs.lw[lane];
-  const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES;
-  const uint8_t* file = a.file;
+  const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES_V2;
+  const uint8_t* __restrict__ file = a.file;
   const uint64_t flen = a.flen;
+  uint32_t* win = lds.win[wv];
 
   uint64_t rootmax = 0, weak = 0;
 
-  for (uint64_t sp = (uint64_t)blockIdx.x * SCAN_WAVES + wv; sp < a.n_spans; sp += total_waves) {
-    uint32_t count = 0;
-    for (int tt = 0; tt < SPAN_TILES; tt++) {
-      const uint64_t k = sp * SPAN_TILES + tt;
-      if (k >= a.n_tiles) break;
-      const uint64_t B = k * (uint64_t)TILE;
-      const uint64_t L = B + 64ull * lane;
-
-      // ---- load my line (+ neighbours' bytes) ----
-      uint32_t d[16];
-      if (L + 64 <= flen) {
-        const u32x4* q = (const u32x4*)(file + L);
+  auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
+    const uint64_t L = k * (uint64_t)TILE + 64ull * lane;
+    if (L + 64 <= flen) {
+      const u32x4* q = (const u32x4*)(file + L);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          u32x4 v = __builtin_nontemporal_load(q + j);
-          d[4 * j] = v[0]; d[4 * j + 1] = v[1]; d[4 * j + 2] = v[2]; d[4 * j + 3] = v[3];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 16; j++) d[j] = ld_dw_guarded(file, flen, L + 4 * j);
+      for (int j = 0; j < 4; j++) {
+        u32x4 v = __builtin_nontemporal_load(q + j);
+        o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
       }
-      uint32_t look[5];
+    } else {
 #pragma unroll
-      for (int j = 0; j < 5; j++) look[j] = __shfl_down(d[j], 1);
-      if (lane == 63) {
-#pragma unroll
-        for (int j = 0; j < 5; j++) look[j] = ld_dw_guarded(file, flen, B + TILE + 4 * j);
-      }
-      uint32_t prevdw = __shfl_up(d[15], 1);
-      if (lane == 0) prevdw = B >= 4 ? ld_dw_guarded(file, flen, B - 4) : 0u;
-
-      // ---- quick filter: any zero triple where a p-field's top bytes sit ----
-      uint32_t acc = 0;
-#pragma unroll
-      for (int i = 3; i < 20; i++) {
-        uint32_t wi = i < 16 ? d[i] : look[i - 16];
-        uint32_t wn = (i + 1) < 16 ? d[i + 1] : look[i + 1 - 16];
-        uint32_t x = wi | alignb(wn, wi, 8) | alignb(wn, wi, 16);
-        acc |= (x - 0x01010101u) & ~x;
-      }
-      uint64_t slow = __ballot((acc & 0x80808080u) != 0);
-
-      uint32_t ntc = 0;
-      int snapoff = 64;
-      while (slow) {
-        const int f = __builtin_ctzll(slow);
-        slow &= slow - 1;
-        if (lane == f) {
-          s_win[wv][0] = prevdw;
-#pragma unroll
-          for (int j = 0; j < 16; j++) s_win[wv][1 + j] = d[j];
-#pragma unroll
-          for (int j = 0; j < 5; j++) s_win[wv][17 + j] = look[j];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t b = lane;
-        const uint64_t m = B + 64ull * f + b;
-        const int base = 1 + (b >> 2);
-        const uint32_t sh = (b & 3) * 8;
-        uint32_t W[6];
-#pragma unroll
-        for (int i = 0; i < 6; i++) W[i] = s_win[wv][base + i];
-        const uint32_t tdw = s_win[wv][(3 + b) >> 2];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t tbyte = (tdw >> (((3 + b) & 3) * 8)) & 0xffu;
-        const uint32_t f0 = alignb(W[1], W[0], sh), f1 = alignb(W[2], W[1], sh);
-        const uint32_t f2 = alignb(W[3], W[2], sh), f3 = alignb(W[4], W[3], sh);
-        const uint32_t f4 = alignb(W[5], W[4], sh);
-        const uint64_t p = (uint64_t)f2 | ((uint64_t)f3 << 32);
-        const bool inrange = (m >= 1) && (m + 20 <= flen);
-        if (inrange && p == 0) rootmax = rootmax > m + 20 ? rootmax : m + 20;
-        const bool tomb = (m > p) && (m - p == 1) && tbyte == 0;
-        const uint64_t start = tomb ? p : p + prepad64(p);
-        const bool isnode = inrange && p != 0 && start < m && p < m && p >= 20;
-        const bool strong = isnode && (FULL || f4 != 0);
-        weak += (isnode && !strong) ? 1 : 0;
-        const uint64_t cm = __ballot(strong);
-        if (cm) {
-          const uint32_t nc = __popcll(cm);
-          const uint32_t rank = __popcll(cm & ((1ull << lane) - 1));
-          if (strong) {
-            const uint32_t idx = count + rank;
-            const uint32_t tl = ntc + rank;
-            const uint64_t t = m + 20;
-            const uint64_t s2 = t + prepad64(t);
-            const uint32_t js = (uint32_t)((s2 - B) >> 6);
-            if (idx < a.cap) {
-              const uint64_t gi = sp * a.cap + idx;
-              a.c_m[gi] = m;
-              a.c_p[gi] = p;
-              a.c_kh[gi] = (uint64_t)f0 | ((uint64_t)f1 << 32);
-              a.c_crc[gi] = f4;
-              if (tl >= TCAP) a.c_flags[gi] = (tomb ? F_TOMB : 0u) | (3u << F_SUF_SHIFT);
-            } else {
-              atomicOr(a.overflow, 1u);
-            }
-            if (tl < TCAP) {
-              s_tslot[wv][tl] = idx;
-              s_tinfo[wv][tl] = (uint32_t)f | (b << 8) | (js << 16) | (tomb ? 0x80000000u : 0u);
-            }
-          }
-          if (lane == f) snapoff = __builtin_ctzll(cm);
-          count += nc;
-          ntc += nc;
-        }
-      }
-
-      // ---- per-line raw CRC (slice-by-4, replicated LDS tables) ----
-      uint32_t s = 0, snap = 0, snapdw = 0;
-      const int snapw = snapoff >> 2;
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        if (j == snapw) { snap = s; snapdw = d[j]; }
-        s ^= d[j];
-        s = s_tab[((3 << 8) + (s & 0xff)) * REPL + cpy] ^ s_tab[((2 << 8) + ((s >> 8) & 0xff)) * REPL + cpy] ^
-            s_tab[((1 << 8) + ((s >> 16) & 0xff)) * REPL + cpy] ^ s_tab[((s >> 24)) * REPL + cpy];
-      }
-      uint32_t tailv = 0;
-      if (snapoff < 64) {
-        tailv = snap;
-        for (int q = 0; q < (snapoff & 3); q++)
-          tailv = s_tab[((tailv ^ (snapdw >> (8 * q))) & 0xff) * REPL + cpy] ^ (tailv >> 8);
-      }
-      // ---- lane weight + suffix XOR over the tile ----
-      uint32_t sx = mulp(lwl, s);
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        uint32_t v = __shfl_down(sx, o);
-        if (lane + o < 64) sx ^= v;
-      }
-      if (lane == 0) a.tileT[k] = sx;
-      if (lane == 1) a.tileSX1[k] = sx;
-
-      // ---- complete this tile's candidate records ----
-      const uint32_t nlist = ntc < TCAP ? ntc : TCAP;
-      for (uint32_t b0 = 0; b0 < nlist; b0 += 64) {
-        const uint32_t i = b0 + lane;
-        const bool act = i < nlist;
-        const uint32_t info = act ? s_tinfo[wv][i] : 0u;
-        const int f = info & 63, r = (info >> 8) & 63, js = (info >> 16) & 127;
-        const uint32_t sxm = __shfl(sx, f);
-        const uint32_t tl = __shfl(tailv, f);
-        const int so = __shfl(snapoff, f);
-        const uint32_t sufv = __shfl(sx, js & 63);
-        if (act) {
-          const uint32_t idx = s_tslot[wv][i];
-          if (idx < a.cap) {
-            const uint64_t gi = sp * a.cap + idx;
-            const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
-            a.c_sxm[gi] = sxm;
-            a.c_suf[gi] = sufv;
-            a.c_tail[gi] = tl;
-            a.c_flags[gi] = ((info >> 31) ? F_TOMB : 0u) | (so == r ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT);
-          }
-        }
-      }
+      for (int j = 0; j < 16; j++) o[j] = ld_dw_guarded(file, flen, L + 4 * j);
     }
-    if (lane == 0) a.span_count[sp] = count;
+  };
+
+  uint64_t sp = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
+  if (sp >= a.n_spans) return;
+  uint32_t d[16], nd[16];
+  load_tile(sp * SPAN_TILES, d);
+  uint32_t prev_last = 0;  // dword just before the current tile (for lane 0)
+  {
+    const uint64_t B = sp * SPAN_TILES * (uint64_t)TILE;
+    prev_last = B >= 4 ? ld_dw_guarded(file, flen, B - 4) : 0u;
+  }
+  uint32_t count = 0;
+  int tt = 0;
+  while (true) {
+    const uint64_t k = sp * SPAN_TILES + tt;
+    const uint64_t B = k * (uint64_t)TILE;
+    const bool last_in_span = (tt == SPAN_TILES - 1) || (k + 1 >= a.n_tiles);
+    // ---- prefetch the next tile of this wave ----
+    uint64_t nsp = sp, nk;
+    int ntt = tt + 1;
+    if (last_in_span) { nsp = sp + total_waves; ntt = 0; }
+    nk = nsp * SPAN_TILES + ntt;
+    const bool have_next = nsp < a.n_spans && nk < a.n_tiles;
+    if (have_next) load_tile(nk, nd);
+    // lookahead for lane 63 when the adjacent tile is not the prefetched one
+    uint32_t look_far[5] = {0, 0, 0, 0, 0};
+    if (last_in_span && lane == 63) {
+#pragma unroll
+      for (int j = 0; j < 5; j++) look_far[j] = ld_dw_guarded(file, flen, B + TILE + 4 * j);
+    }
+
+    // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
+    const uint32_t c = crc_line(d, lds.tab, cpy);
+    uint32_t sx = lane_weight(c, lds.nib, lane);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_down(sx, o);
+      if (lane + o < 64) sx ^= v;
+    }
+    if (lane < 2) a.tile[2 * k + lane] = sx;  // T = SX_0, SX_1
+
+    // ---- neighbour bytes ----
+    uint32_t look[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      const uint32_t dn = __shfl_down(d[j], 1);
+      const uint32_t nx = last_in_span ? look_far[j] : __shfl(nd[j], 0);
+      look[j] = lane == 63 ? nx : dn;
+    }
+    uint32_t prevdw = __shfl_up(d[15], 1);
+    if (lane == 0) prevdw = prev_last;
+
+    // ---- filter: a p-field's three top bytes (zero for p < 2^40) always
+    //      contain an aligned zero halfword ----
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 3; i < 20; i++) {
+      const uint32_t w = i < 16 ? d[i] : look[i - 16];
+      acc |= (w - 0x00010001u) & ~w;
+    }
+    uint64_t slow = __ballot((acc & 0x80008000u) != 0);
+
+    while (slow) {
+      const int f = __builtin_ctzll(slow);
+      slow &= slow - 1;
+      if (lane == f) {
+        win[3] = prevdw;
+#pragma unroll
+        for (int j = 0; j < 16; j++) win[4 + j] = d[j];
+#pragma unroll
+        for (int j = 0; j < 5; j++) win[20 + j] = look[j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t b = lane;
+      const uint64_t m = B + 64ull * f + b;
+      const int base = 4 + (b >> 2);
+      const uint32_t sh = (b & 3) * 8;
+      uint32_t W[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) W[i] = win[base + i];
+      const uint32_t tdw = win[(15 + b) >> 2];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t tbyte = (tdw >> (((15 + b) & 3) * 8)) & 0xffu;
+      const uint32_t f0 = alignb(W[1], W[0], sh), f1 = alignb(W[2], W[1], sh);
+      const uint32_t f2 = alignb(W[3], W[2], sh), f3 = alignb(W[4], W[3], sh);
+      const uint32_t f4 = alignb(W[5], W[4], sh);
+      const uint64_t p = (uint64_t)f2 | ((uint64_t)f3 << 32);
+      const bool inrange = (m >= 1) && (m + 20 <= flen);
+      if (inrange && p == 0) rootmax = rootmax > m + 20 ? rootmax : m + 20;
+      const bool tomb = (m > p) && (m - p == 1) && tbyte == 0;
+      const uint64_t start = tomb ? p : p + prepad64(p);
+      const bool isnode = inrange && p != 0 && start < m && p < m && p >= 20;
+      const bool strong = isnode && (FULL || f4 != 0);
+      weak += (isnode && !strong) ? 1 : 0;
+      const uint64_t t = m + 20;
+      const uint32_t js = (uint32_t)((t + prepad64(t) - B) >> 6);  // line of the next entry's start
+      const uint32_t sufv = __shfl(sx, (int)(js & 63));
+      const uint32_t sxm = __builtin_amdgcn_readlane(sx, f);
+      const uint64_t cm = __ballot(strong);
+      if (strong) {
+        const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
+        if (idx < a.cap) {
+          const uint64_t gi = sp * a.cap + idx;
+          const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
+          a.c_m[gi] = m;
+          a.c_rec[2 * gi] = u32x4{f2, f3, f0, f1};
+          a.c_rec[2 * gi + 1] = u32x4{f4, sxm, sufv,
+                                      (tomb ? F_TOMB : 0u) | (b == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT)};
+        } else {
+          atomicOr((unsigned int*)(a.counters + 2), 1u);
+        }
+      }
+      count += __popcll(cm);
+    }
+
+    if (last_in_span) {
+      if (lane == 0) a.span_count[sp] = count;
+      count = 0;
+      if (!have_next) break;
+      sp = nsp;
+      tt = 0;
+      const uint64_t NB = sp * SPAN_TILES * (uint64_t)TILE;
+      prev_last = ld_dw_guarded(file, flen, NB - 4);
+    } else {
+      prev_last = __builtin_amdgcn_readlane(d[15], 63);
+      tt++;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) d[j] = nd[j];
   }
   rootmax = wave_max_u64(rootmax);
   for (int o = 32; o > 0; o >>= 1) weak += __shfl_xor(weak, o);
   if (lane == 0) {
-    if (rootmax) atomicMax(a.max_root, (unsigned long long)rootmax);
-    if (weak) atomicAdd(a.n_weak, (unsigned long long)weak);
+    if (rootmax) atomicMax(a.counters + 0, (unsigned long long)rootmax);
+    if (weak) atomicAdd(a.counters + 1, (unsigned long long)weak);
   }
 }
 
@@ -312,7 +318,7 @@ struct LinkArgs {
   const uint32_t* span_count;
   const uint64_t* span_base;  // exclusive prefix of min(count, cap)
   const uint64_t* c_m;
-  const uint64_t* c_p;
+  const u32x4* c_rec;
   uint64_t* d_m;
   int64_t* d_par;
   uint64_t* d_slot;
@@ -324,7 +330,8 @@ __global__ __launch_bounds__(64) void link_kernel(LinkArgs a) {
   const uint64_t gb = a.span_base[sp];
   for (uint32_t i = threadIdx.x; i < n; i += 64) {
     const uint64_t gi = sp * a.cap + i;
-    const uint64_t m = a.c_m[gi], p = a.c_p[gi];
+    const u32x4 r0 = a.c_rec[2 * gi];
+    const uint64_t m = a.c_m[gi], p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     const uint64_t mp = p - 20;  // p >= 20 by construction
     const uint64_t sp2 = mp / SPAN_BYTES;
     int64_t par = PAR_MISS;
@@ -360,7 +367,7 @@ struct WalkState {
 
 // idx space: 0..n-1 ; par_of(i) gives par in the same space ; runhead[i]
 __global__ void walk_kernel(const int64_t* par, const uint64_t* runhead, const uint64_t* slot,
-                            const uint64_t* c_p, uint64_t* ints, WalkState* ws, uint64_t max_ints) {
+                            const u32x4* c_rec, uint64_t* ints, WalkState* ws, uint64_t max_ints) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint64_t x = ws->start, n = 0, len = 1;
   int64_t status = 1;
@@ -370,7 +377,11 @@ __global__ void walk_kernel(const int64_t* par, const uint64_t* runhead, const u
     n++;
     len += x - h + 1;
     int64_t q = par[h];
-    if (q == PAR_ROOT) { ws->root_t = c_p[slot[h]]; break; }
+    if (q == PAR_ROOT) {
+      const u32x4 r0 = c_rec[2 * slot[h]];
+      ws->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+      break;
+    }
     if (q < 0) { status = -1; break; }
     x = (uint64_t)q;
   }
@@ -483,19 +494,12 @@ struct FinArgs {
   const int64_t* par;        // dense g -> dense parent
   const WalkState* ws;
   const uint64_t* c_m;
-  const uint64_t* c_p;
-  const uint64_t* c_kh;
-  const uint32_t* c_crc;
-  const uint32_t* c_sxm;
-  const uint32_t* c_suf;
-  const uint32_t* c_tail;
-  const uint32_t* c_flags;
-  const uint32_t* tileT;
-  const uint32_t* tileSX1;
+  const u32x4* c_rec;
+  const uint32_t* tile;      // [2k] = T_k (SX_0), [2k+1] = SX_1
   int no_crc;
   // outputs
   uint64_t *o_mo, *o_kh, *o_prev, *o_start, *o_len;
-  uint32_t *o_crc_st, *o_crc, *o_pieces;  // o_pieces: bit0 suf ok, bit1 sxm ok, bit2 tail ok (slow path input)
+  uint32_t *o_crc_st, *o_crc, *o_pieces;  // o_pieces: bit0 suf ok, bit1 sxm ok (slow path input)
   uint32_t *o_suf, *o_sxm, *o_tail;
   uint8_t* o_ok;
   uint64_t* slow_list;
@@ -503,8 +507,23 @@ struct FinArgs {
   unsigned long long* n_bad;
 };
 
+// crc_raw of bytes [floor64(m), m) read from the file (<= 63 bytes)
+__device__ __forceinline__ uint32_t tail_crc(const uint8_t* file, uint64_t m) {
+  const uint64_t L = m & ~63ull;
+  const uint32_t r = (uint32_t)(m - L);
+  uint32_t s = 0;
+  uint32_t q = 0;
+  for (; q + 4 <= r; q += 4) {
+    s ^= *(const uint32_t*)(file + L + q);
+    s = g_tabs.tab[3][s & 0xff] ^ g_tabs.tab[2][(s >> 8) & 0xff] ^ g_tabs.tab[1][(s >> 16) & 0xff] ^
+        g_tabs.tab[0][s >> 24];
+  }
+  for (; q < r; q++) s = g_tabs.tab[0][(s ^ file[L + q]) & 0xff] ^ (s >> 8);
+  return s;
+}
+
 __device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint32_t suf, uint32_t sxm,
-                                                    uint32_t tail, const uint32_t* tileT) {
+                                                    uint32_t tail, const uint32_t* tile) {
   const uint64_t len = m - s;
   if (len < 64) return tail ^ g_tabs.zero_crc[len];
   const uint64_t k0 = s / TILE, k1 = m / TILE;
@@ -514,8 +533,8 @@ __device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint
   if (k0 == k1) {
     y = acc ^ sxm;
   } else {
-    for (uint64_t k = k0 + 1; k < k1; k++) acc = mulp(g_tabs.x32768, acc) ^ tileT[k];
-    y = mulp(g_tabs.x32768, acc) ^ tileT[k1] ^ sxm;
+    for (uint64_t k = k0 + 1; k < k1; k++) acc = mulp(g_tabs.x32768, acc) ^ tile[2 * k];
+    y = mulp(g_tabs.x32768, acc) ^ tile[2 * k1] ^ sxm;
   }
   const uint64_t dd = (k1 + 1) * TILE - m;
   return ~(mulp(g_tabs.invpow[dd], y) ^ tail);
@@ -535,31 +554,32 @@ __global__ void finalize_kernel(FinArgs a) {
     p = 0;
     tomb = false;  // start is 0 either way
     start = 0;
-    suf = a.tileT[0];
+    suf = a.tile[0];
     pieces = 1;
   } else {
     const uint64_t g = a.chain_g[c];
     const uint64_t gi = a.slot[g];
     mo = a.c_m[gi];
-    p = a.c_p[gi];
-    kh = a.c_kh[gi];
-    crc_st = a.c_crc[gi];
-    const uint32_t fl = a.c_flags[gi];
+    const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
+    p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+    kh = (uint64_t)r0[2] | ((uint64_t)r0[3] << 32);
+    crc_st = r1[0];
+    const uint32_t fl = r1[3];
     tomb = fl & F_TOMB;
     start = tomb ? p : p + prepad64(p);
-    if (fl & F_SXM) { sxm = a.c_sxm[gi]; pieces |= 2; }
-    if (fl & F_TAIL) { tail = a.c_tail[gi]; pieces |= 4; }
+    if (fl & F_SXM) { sxm = r1[1]; pieces |= 2; }
+    if (fl & F_TAIL) { tail = 0; pieces |= 4; }
     const int64_t pg = a.par[g];
     if (pg >= 0) {
       const uint64_t pgi = a.slot[pg];
-      const uint32_t pf = a.c_flags[pgi];
-      const uint32_t kind = (pf >> F_SUF_SHIFT) & 3;
+      const u32x4 pr1 = a.c_rec[2 * pgi + 1];
+      const uint32_t kind = (pr1[3] >> F_SUF_SHIFT) & 3;
       const uint64_t k0 = start / TILE;
-      if (kind == 0) { suf = a.c_suf[pgi]; pieces |= 1; }
-      else if (kind == 1) { suf = a.tileT[k0]; pieces |= 1; }
-      else if (kind == 2) { suf = a.tileSX1[k0]; pieces |= 1; }
+      if (kind == 0) { suf = pr1[2]; pieces |= 1; }
+      else if (kind == 1) { suf = a.tile[2 * k0]; pieces |= 1; }
+      else if (kind == 2) { suf = a.tile[2 * k0 + 1]; pieces |= 1; }
     } else if (start == 0) {
-      suf = a.tileT[0];
+      suf = a.tile[0];
       pieces |= 1;
     }
   }
@@ -578,11 +598,10 @@ __global__ void finalize_kernel(FinArgs a) {
     if (crc != crc_st) atomicAdd(a.n_bad, 1ull);
     return;
   }
-  // pieces needed: suf (if len>=64), sxm (if len>=64), tail (always)
+  if (!(pieces & 4)) tail = tail_crc(a.file, mo);  // re-read the partial last line
   const bool need_long = len >= 64;
-  const bool have = (pieces & 4) && (!need_long || ((pieces & 1) && (pieces & 2)));
-  if (have) {
-    const uint32_t crc = crc_from_pieces(start, mo, suf, sxm, tail, a.tileT);
+  if (!need_long || ((pieces & 1) && (pieces & 2))) {
+    const uint32_t crc = crc_from_pieces(start, mo, suf, sxm, tail, a.tile);
     a.o_crc[c] = crc;
     a.o_ok[c] = crc == crc_st;
     if (crc != crc_st) atomicAdd(a.n_bad, 1ull);
@@ -596,17 +615,14 @@ __global__ void finalize_kernel(FinArgs a) {
   }
 }
 
-// Recompute, with one wave, the per-tile values of tile k: SX at line j and
-// crc_raw of the first r bytes of line j (r in 0..63).
-__device__ void tile_probe(const uint8_t* file, uint64_t flen, uint64_t k, uint32_t j, uint32_t r,
-                           uint32_t* sx_out, uint32_t* tail_out) {
+// Recompute, with one wave, SX at line j of tile k.
+__device__ uint32_t tile_probe_sx(const uint8_t* file, uint64_t flen, uint64_t k, uint32_t j) {
   const int lane = threadIdx.x & 63;
   const uint64_t L = k * TILE + 64ull * lane;
-  uint32_t s = 0, tl = 0;
+  uint32_t s = 0;
   for (int q = 0; q < 64; q++) {
     const uint64_t o = L + q;
     const uint32_t byte = o < flen ? file[o] : 0u;
-    if (q == (int)r) tl = s;
     s = g_tabs.tab[0][(s ^ byte) & 0xff] ^ (s >> 8);
   }
   uint32_t sx = mulp(g_tabs.lw[lane], s);
@@ -614,29 +630,20 @@ __device__ void tile_probe(const uint8_t* file, uint64_t flen, uint64_t k, uint3
     uint32_t v = __shfl_down(sx, o);
     if (lane + o < 64) sx ^= v;
   }
-  *sx_out = __shfl(sx, (int)j);
-  *tail_out = __shfl(tl, (int)j);
+  return __shfl(sx, (int)j);
 }
 
-// one wave per slow entry
+// one wave per slow entry (a piece of the combine was not recorded)
 __global__ __launch_bounds__(64) void slow_kernel(FinArgs a) {
   const unsigned long long ns = *a.n_slow;
   for (uint64_t w = blockIdx.x; w < ns; w += gridDim.x) {
     const uint64_t c = a.slow_list[w];
     const uint64_t s = a.o_start[c], m = a.o_mo[c];
     uint32_t pieces = a.o_pieces[c], suf = a.o_suf[c], sxm = a.o_sxm[c], tail = a.o_tail[c];
-    uint32_t sxv, tv;
-    if (!(pieces & 1)) {
-      tile_probe(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64), 0, &sxv, &tv);
-      suf = sxv;
-    }
-    if (!(pieces & 6) || !(pieces & 2) || !(pieces & 4)) {
-      tile_probe(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64), (uint32_t)(m % 64), &sxv, &tv);
-      if (!(pieces & 2)) sxm = sxv;
-      if (!(pieces & 4)) tail = tv;
-    }
+    if (!(pieces & 1)) suf = tile_probe_sx(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64));
+    if (!(pieces & 2)) sxm = tile_probe_sx(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64));
     if ((threadIdx.x & 63) == 0) {
-      const uint32_t crc = crc_from_pieces(s, m, suf, sxm, tail, a.tileT);
+      const uint32_t crc = crc_from_pieces(s, m, suf, sxm, tail, a.tile);
       a.o_crc[c] = crc;
       a.o_ok[c] = crc == a.o_crc_st[c];
       if (crc != a.o_crc_st[c]) atomicAdd(a.n_bad, 1ull);
