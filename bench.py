@@ -95,7 +95,7 @@ def main():
 
     n, L = args.entries_per_gpu, args.payload
     size = S.synth_store_len(n, L)
-    store = torch.empty(size + 4096, dtype=torch.uint8, device=f"cuda:{local}")
+    store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
     S.synth_store_device(store.data_ptr(), n, L, ctx=ctx)
     torch.cuda.synchronize()
     bytes_alg = algorithmic_bytes(n, L)

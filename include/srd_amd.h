@@ -90,8 +90,15 @@ typedef struct {
   uint64_t *index_key_hash, *index_packed;
 } srd_device_result;
 
+/* Bytes the device buffer handed to srd_validate_index_device must be
+ * readable for: file_len rounded up to 4 KiB plus 8 KiB of slack (contents
+ * past file_len are ignored).  The streaming kernel loads whole 4 KiB tiles
+ * unconditionally so its prefetch ring never drains on a bounds branch. */
+uint64_t srd_padded_size(uint64_t file_len);
+
 /* Device-resident validate+index over `file_len` bytes at `d_file`
- * (device pointer; the bytes are the mmap'd store). */
+ * (device pointer, 16-byte aligned, readable to srd_padded_size(file_len);
+ * the bytes are the mmap'd store). */
 int srd_validate_index_device(srd_ctx *ctx, const uint8_t *d_file,
                               uint64_t file_len, uint32_t flags,
                               srd_device_result *out);

@@ -44,7 +44,7 @@ struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::vector<Buf> bufs;  // indexed by the enum below
-  uint32_t cap = 256;     // candidate slots per span
+  uint32_t cap = 64;      // candidate slots per span (4 tiles); grows x4 on overflow
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
   srd_device_result res{};
   // host-input staging
@@ -110,8 +110,13 @@ int upload_tables() {
   memcpy(t.invpow, g_host_tabs.invpow, sizeof t.invpow);
   for (int pos = 0; pos < 8; pos++)
     for (int nb = 0; nb < 16; nb++)
-      for (int l = 0; l < 64; l++)
-        t.nib[((pos * 16 + nb) << 6) + l] = mulp(g_host_tabs.lw[l], (uint32_t)nb << (4 * pos));
+      for (int l = 0; l < 32; l++)  // x^(512*(31-l)) = lw[l + 32]
+        t.nib[((pos * 16 + nb) << 5) + l] = mulp(g_host_tabs.lw[l + 32], (uint32_t)nb << (4 * pos));
+  {
+    const uint32_t x16k = host_xpow8(g_host_tabs, 2048);
+    for (int tb = 0; tb < 4; tb++)
+      for (int b = 0; b < 256; b++) t.m16k[tb][b] = mulp(x16k, (uint32_t)b << (8 * tb));
+  }
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_tabs), &t, sizeof t));
   uploaded |= 1ull << dev;
   (void)rc;
@@ -397,6 +402,10 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.c_m = P<uint64_t>(c, B_CM);
     a.c_rec = P<u32x4>(c, B_CREC);
     a.counters = (unsigned long long*)cnt;
+    {
+      const char* ab = getenv("SRD_SCAN_ABLATE");
+      a.ablate = ab ? (uint32_t)atoi(ab) : 0u;
+    }
     if (n_spans) {
       unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
@@ -605,14 +614,17 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
   return finish(c, d_file, flen, hw.chain_len, flags, out);
 }
 
+extern "C" uint64_t srd_padded_size(uint64_t flen) { return ((flen + TILE - 1) / TILE) * TILE + 2 * TILE; }
+
 // ---------------------------------------------------------------- host input
 static int stage_file(Ctx* c, const uint8_t* file, uint64_t flen, const uint8_t** d) {
-  if (c->file.n < flen + 64) {
+  const uint64_t need = srd_padded_size(flen);
+  if (c->file.n < need) {
     if (c->file.p) HIPCHK(hipFree(c->file.p));
     c->file.p = nullptr;
     c->file.n = 0;
-    if (hipMalloc(&c->file.p, flen + 64) != hipSuccess) { set_err("hipMalloc(file)"); return SRD_ERR_ALLOC; }
-    c->file.n = flen + 64;
+    if (hipMalloc(&c->file.p, need) != hipSuccess) { set_err("hipMalloc(file)"); return SRD_ERR_ALLOC; }
+    c->file.n = need;
   }
   if (flen) HIPCHK(hipMemcpyAsync(c->file.p, file, flen, hipMemcpyHostToDevice, c->stream));
   *d = (const uint8_t*)c->file.p;

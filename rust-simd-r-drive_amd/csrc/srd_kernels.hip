@@ -34,9 +34,15 @@ namespace srd {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int TILE = 4096;
-constexpr int SPAN_TILES = 16;
+constexpr int SPAN_TILES = 4;
 constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
-constexpr int REPL = 16;             // LDS table replication (bank spreading)
+#ifndef SRD_RING
+#define SRD_RING 2
+#endif
+#ifndef SRD_REPL
+#define SRD_REPL 32
+#endif
+constexpr int REPL = SRD_REPL;       // LDS table replication: lane l reads copy l%32 -> conflict-free
 constexpr int SCAN_WAVES = 8;        // waves per scan block
 constexpr int TCAP = 128;            // per-tile candidate list in LDS
 constexpr int64_t PAR_ROOT = -1;
@@ -54,7 +60,8 @@ struct DevTables {
   uint32_t x32768;
   uint32_t pow8[64];
   uint32_t invpow[4097];
-  uint32_t nib[8 * 16 * 64];       // lane-weight nibble tables
+  uint32_t nib[8 * 16 * 32];       // half-tile lane-weight nibble tables
+  uint32_t m16k[4][256];           // v -> v * x^16384 byte tables
 };
 __device__ DevTables g_tabs;
 
@@ -68,6 +75,7 @@ struct ScanArgs {
   uint64_t* c_m;                   // [n_spans*cap] candidate metadata offsets
   u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
   unsigned long long* counters;    // [0] max root tail, [1] weak, [2] overflow
+  uint32_t ablate;                 // timing experiments only (SRD_SCAN_ABLATE): 1 no CRC, 2 no slow path, 4 no filter
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -88,6 +96,12 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* f, uint64_t 
   return v;
 }
 __device__ __forceinline__ uint64_t prepad64(uint64_t o) { return (64 - (o & 63)) & 63; }
+// zero the bytes of dword v (file offset o) at or past n
+__device__ __forceinline__ uint32_t mask_past_end(uint32_t v, uint64_t o, uint64_t n) {
+  if (o + 4 <= n) return v;
+  if (o >= n) return 0u;
+  return v & ((1u << (8 * (uint32_t)(n - o))) - 1u);
+}
 
 __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t sh) {
   return __builtin_amdgcn_alignbit(hi, lo, sh);
@@ -110,123 +124,176 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // ((pos*16+nib)*64 + l): every lane its own bank, conflict-free) and one
 // 25-dword window per wave for the cooperative candidate check.
 constexpr int SCAN_WAVES_V2 = 16;
+constexpr int MREPL = 8;  // replication of the x^256 multiply table
 struct ScanLds {
-  uint32_t tab[4 * 256 * REPL];
-  uint32_t nib[8 * 16 * 64];
+  uint32_t tab[4 * 256 * 32];      // 128 KiB slice-by-4 tables, conflict-free (layout: tab_lookup)
+  uint32_t nib[8 * 16 * 32];       // 16 KiB: c -> c * x^(512*(31 - l%32)), bank = l%32
+  uint32_t m16k[4 * 256];          // v -> v * x^16384 (lower half -> tile end)
   uint32_t win[SCAN_WAVES_V2][28];
 };
 
-__device__ __forceinline__ uint32_t crc_line(const uint32_t (&d)[16], const uint32_t* __restrict__ tab,
-                                             uint32_t cpy) {
-  uint32_t s = 0;
+// Slice-by-4 with v_perm addressing.  LDS layout of the 4 tables: word
+// b*64 + (t&1)*32 + c (+ 16384*(t>>1)), c = lane%32 -> byte address
+// [t>>1 : b : (t&1)*128 + 4c], so the lookup address of byte j of s is ONE
+// v_perm_b32(s, R_t) and every 32-lane group hits 32 distinct banks.
+__device__ __forceinline__ uint32_t tab_lookup(const ScanLds& L, uint32_t s, uint32_t R, uint32_t sel) {
+  const uint32_t addr = __builtin_amdgcn_perm(s, R, sel);
+  return *(const uint32_t*)((const char*)L.tab + addr);
+}
+__device__ __forceinline__ uint32_t crc_line1(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
+  // byte j of S0 = selector 4+j; S1 bytes 0 and 2 = selectors 0 and 2; 0x0c = zero
+  constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
+  uint32_t s = d[0];
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    s ^= d[j];
-    s = tab[((3 << 8) + (s & 0xff)) * REPL + cpy] ^ tab[((2 << 8) + ((s >> 8) & 0xff)) * REPL + cpy] ^
-        tab[((1 << 8) + ((s >> 16) & 0xff)) * REPL + cpy] ^ tab[(s >> 24) * REPL + cpy];
+    const uint32_t t3 = tab_lookup(L, s, R[3], SEL0), t2 = tab_lookup(L, s, R[2], SEL1);
+    const uint32_t t1 = tab_lookup(L, s, R[1], SEL2), t0 = tab_lookup(L, s, R[0], SEL3);
+    s = t3 ^ t2 ^ t1 ^ t0 ^ (j < 15 ? d[j < 15 ? j + 1 : 15] : 0u);
   }
   return s;
 }
 
-// c * x^(512*(63-lane)) via 8 nibble lookups
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+constexpr int DPP_WAVE_SHL1 = 0x130;  // lane i <- lane i+1 (0 past the end)
+constexpr int DPP_WAVE_SHR1 = 0x138;  // lane i <- lane i-1
+constexpr int DPP_ROW_SHL = 0x100;    // + n: lane i <- lane i+n inside a row of 16
+
+// XOR of u over lanes >= lane (64-lane suffix scan: DPP inside rows,
+// readlane for the row totals)
+__device__ __forceinline__ uint32_t suffix_xor(uint32_t v, int lane) {
+  v ^= dpp<DPP_ROW_SHL + 1>(v);
+  v ^= dpp<DPP_ROW_SHL + 2>(v);
+  v ^= dpp<DPP_ROW_SHL + 4>(v);
+  v ^= dpp<DPP_ROW_SHL + 8>(v);
+  const uint32_t t1 = __builtin_amdgcn_readlane(v, 16), t2 = __builtin_amdgcn_readlane(v, 32),
+                 t3 = __builtin_amdgcn_readlane(v, 48);
+  const int row = lane >> 4;
+  const uint32_t add = row == 0 ? (t1 ^ t2 ^ t3) : row == 1 ? (t2 ^ t3) : row == 2 ? t3 : 0u;
+  return v ^ add;
+}
+
+// c * x^(512*(31 - lane%32)) via 8 nibble lookups: the lane weight relative
+// to the end of the lane's HALF of the tile (lanes >= 32: relative to the
+// tile end, i.e. final; lanes < 32: relative to line 31, corrected on use).
 __device__ __forceinline__ uint32_t lane_weight(uint32_t c, const uint32_t* __restrict__ nib, int lane) {
   uint32_t u = 0;
+  const int t = lane & 31;
 #pragma unroll
-  for (int pos = 0; pos < 8; pos++) u ^= nib[((pos * 16 + ((c >> (4 * pos)) & 15)) << 6) + lane];
+  for (int pos = 0; pos < 8; pos++) u ^= nib[((pos * 16 + ((c >> (4 * pos)) & 15)) << 5) + t];
   return u;
+}
+__device__ __forceinline__ uint32_t mul16k(uint32_t v, const uint32_t* __restrict__ m) {
+  return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
+}
+// Half-tile suffix XOR: lanes >= 32 get XOR_{i>=l} u_i (the true SX_l);
+// lanes < 32 get XOR_{l<=i<32} u_i (true SX_l = mul16k(.) ^ SX_32).
+__device__ __forceinline__ uint32_t half_suffix_xor(uint32_t v, int lane) {
+  v ^= dpp<DPP_ROW_SHL + 1>(v);
+  v ^= dpp<DPP_ROW_SHL + 2>(v);
+  v ^= dpp<DPP_ROW_SHL + 4>(v);
+  v ^= dpp<DPP_ROW_SHL + 8>(v);
+  const uint32_t t1 = __builtin_amdgcn_readlane(v, 16), t3 = __builtin_amdgcn_readlane(v, 48);
+  const int row = lane >> 4;
+  return v ^ (row == 0 ? t1 : row == 2 ? t3 : 0u);
 }
 
 template <bool FULL>
 __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
   __shared__ ScanLds lds;
-  for (int i = threadIdx.x; i < 4 * 256 * REPL; i += blockDim.x) lds.tab[i] = (&g_tabs.tab[0][0])[i / REPL];
-  for (int i = threadIdx.x; i < 8 * 16 * 64; i += blockDim.x) lds.nib[i] = g_tabs.nib[i];
+  for (int i = threadIdx.x; i < 4 * 256 * 32; i += blockDim.x) {
+    const int hi = i >> 14, b = (i >> 6) & 255, t = hi * 2 + ((i >> 5) & 1);
+    lds.tab[i] = g_tabs.tab[t][b];
+  }
+  for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) lds.nib[i] = g_tabs.nib[i];
+  for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) lds.m16k[i] = (&g_tabs.m16k[0][0])[i];
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const uint32_t cpy = lane & (REPL - 1);
-  const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES_V2;
+  uint32_t R[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
   const uint8_t* __restrict__ file = a.file;
   const uint64_t flen = a.flen;
   uint32_t* win = lds.win[wv];
 
-  uint64_t rootmax = 0, weak = 0;
+  // balanced contiguous tile range per wave (whole spans)
+  const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES_V2;
+  const uint64_t w = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
+  const uint64_t spw = (a.n_spans + total_waves - 1) / total_waves;
+  const uint64_t s0 = w * spw;
+  const uint64_t k0 = s0 * SPAN_TILES;
+  const uint64_t k1 = min((s0 + spw) * SPAN_TILES, a.n_tiles);
+  if (k0 >= k1) return;
 
+  uint64_t rootmax = 0, weak = 0;
+  uint32_t count = 0;
+
+  // Unconditional loads: the buffer is readable to srd_padded_size(flen)
+  // (no loads under divergent/uniform branches, so the compiler's vmcnt
+  // waits never have to drain the prefetch ring).
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
-    const uint64_t L = k * (uint64_t)TILE + 64ull * lane;
-    if (L + 64 <= flen) {
-      const u32x4* q = (const u32x4*)(file + L);
+    const u32x4* q = (const u32x4*)(file + k * (uint64_t)TILE + 64ull * lane);
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        u32x4 v = __builtin_nontemporal_load(q + j);
-        o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 16; j++) o[j] = ld_dw_guarded(file, flen, L + 4 * j);
+    for (int j = 0; j < 4; j++) {
+      const u32x4 v = q[j];  // plain loads: this 64 B-per-lane pattern runs at ~3.8 TB/s with nt, ~6.1 without
+      o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
     }
   };
 
-  uint64_t sp = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
-  if (sp >= a.n_spans) return;
-  uint32_t d[16], nd[16];
-  load_tile(sp * SPAN_TILES, d);
-  uint32_t prev_last = 0;  // dword just before the current tile (for lane 0)
-  {
-    const uint64_t B = sp * SPAN_TILES * (uint64_t)TILE;
-    prev_last = B >= 4 ? ld_dw_guarded(file, flen, B - 4) : 0u;
-  }
-  uint32_t count = 0;
-  int tt = 0;
-  while (true) {
-    const uint64_t k = sp * SPAN_TILES + tt;
+  uint32_t prev_last = k0 ? ld_dw_guarded(file, flen, k0 * (uint64_t)TILE - 4) : 0u;
+
+  // process tile k held in d[]; nx[] holds tile k+1 when k+1 < k1
+  auto process = [&](uint64_t k, uint32_t (&d)[16], const uint32_t (&nx)[16]) {
     const uint64_t B = k * (uint64_t)TILE;
-    const bool last_in_span = (tt == SPAN_TILES - 1) || (k + 1 >= a.n_tiles);
-    // ---- prefetch the next tile of this wave ----
-    uint64_t nsp = sp, nk;
-    int ntt = tt + 1;
-    if (last_in_span) { nsp = sp + total_waves; ntt = 0; }
-    nk = nsp * SPAN_TILES + ntt;
-    const bool have_next = nsp < a.n_spans && nk < a.n_tiles;
-    if (have_next) load_tile(nk, nd);
-    // lookahead for lane 63 when the adjacent tile is not the prefetched one
-    uint32_t look_far[5] = {0, 0, 0, 0, 0};
-    if (last_in_span && lane == 63) {
+    const uint64_t span = k / SPAN_TILES;
+    const bool tail_tile = B + TILE + 64 > flen;  // uniform; bytes >= flen read as 0
+    if (tail_tile) {
+      const uint64_t L = B + 64ull * lane;
 #pragma unroll
-      for (int j = 0; j < 5; j++) look_far[j] = ld_dw_guarded(file, flen, B + TILE + 4 * j);
+      for (int j = 0; j < 16; j++) d[j] = mask_past_end(d[j], L + 4 * j, flen);
     }
 
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
-    const uint32_t c = crc_line(d, lds.tab, cpy);
-    uint32_t sx = lane_weight(c, lds.nib, lane);
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t v = __shfl_down(sx, o);
-      if (lane + o < 64) sx ^= v;
-    }
-    if (lane < 2) a.tile[2 * k + lane] = sx;  // T = SX_0, SX_1
+    const uint32_t c = (a.ablate & 1) ? (d[0] ^ d[5] ^ d[15]) : crc_line1(d, lds, R);
+    const uint32_t hx = (a.ablate & 1) ? c : half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
+    const uint32_t sx32 = __builtin_amdgcn_readlane(hx, 32);  // true SX_32
+    if (lane < 2) a.tile[2 * k + lane] = mul16k(hx, lds.m16k) ^ sx32;  // T = SX_0, SX_1
 
     // ---- neighbour bytes ----
     uint32_t look[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) {
-      const uint32_t dn = __shfl_down(d[j], 1);
-      const uint32_t nx = last_in_span ? look_far[j] : __shfl(nd[j], 0);
-      look[j] = lane == 63 ? nx : dn;
+      const uint32_t dn = dpp<DPP_WAVE_SHL1>(d[j]);
+      // lane 63: first bytes of tile k+1 = lane 0 of the prefetched buffer (it is
+      // the OLDER of the two tiles in flight, so waiting for it keeps k+2 flying)
+      uint32_t nxv = __builtin_amdgcn_readlane(nx[j], 0);
+      if (tail_tile) nxv = mask_past_end(nxv, B + TILE + 4 * j, flen);
+      look[j] = lane == 63 ? nxv : dn;
     }
-    uint32_t prevdw = __shfl_up(d[15], 1);
+    uint32_t prevdw = dpp<DPP_WAVE_SHR1>(d[15]);
     if (lane == 0) prevdw = prev_last;
+    prev_last = __builtin_amdgcn_readlane(d[15], 63);
 
-    // ---- filter: a p-field's three top bytes (zero for p < 2^40) always
-    //      contain an aligned zero halfword ----
-    uint32_t acc = 0;
+    // ---- filter: a node at m has zero bytes m+13..m+15 (the top of p < 2^40).
+    //      Exact zero-triple test for triple starts q = m+13 in [L+13, L+76]. ----
+    uint32_t acc = 0, acc3 = 0, acc19 = 0;
 #pragma unroll
     for (int i = 3; i < 20; i++) {
-      const uint32_t w = i < 16 ? d[i] : look[i - 16];
-      acc |= (w - 0x00010001u) & ~w;
+      const uint32_t wd = i < 16 ? d[i] : look[i - 16];
+      const uint32_t wn = (i + 1) < 16 ? d[i + 1] : look[i + 1 - 16];
+      const uint32_t x = wd | alignb(wn, wd, 8) | alignb(wn, wd, 16);
+      const uint32_t z = (x - 0x01010101u) & ~x;  // bit 7 of byte k: a zero byte at/below k
+      if (i == 3) acc3 = z;
+      else if (i == 19) acc19 = z;
+      else acc |= z;
     }
-    uint64_t slow = __ballot((acc & 0x80008000u) != 0);
+    acc = (acc & 0x80808080u) | (acc3 & 0x80808000u) | (acc19 & 0x00000080u);
+    uint64_t slow = __ballot(acc != 0);
+    if (a.ablate & 2) slow = 0;
 
     while (slow) {
       const int f = __builtin_ctzll(slow);
@@ -266,13 +333,15 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       weak += (isnode && !strong) ? 1 : 0;
       const uint64_t t = m + 20;
       const uint32_t js = (uint32_t)((t + prepad64(t) - B) >> 6);  // line of the next entry's start
-      const uint32_t sufv = __shfl(sx, (int)(js & 63));
-      const uint32_t sxm = __builtin_amdgcn_readlane(sx, f);
+      const uint32_t hs = __shfl(hx, (int)(js & 63));
+      const uint32_t sufv = (js & 63) >= 32 ? hs : (mul16k(hs, lds.m16k) ^ sx32);
+      const uint32_t hm = __builtin_amdgcn_readlane(hx, f);
+      const uint32_t sxm = f >= 32 ? hm : (mul16k(hm, lds.m16k) ^ sx32);
       const uint64_t cm = __ballot(strong);
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
         if (idx < a.cap) {
-          const uint64_t gi = sp * a.cap + idx;
+          const uint64_t gi = span * a.cap + idx;
           const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
           a.c_m[gi] = m;
           a.c_rec[2 * gi] = u32x4{f2, f3, f0, f1};
@@ -284,22 +353,42 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       }
       count += __popcll(cm);
     }
-
-    if (last_in_span) {
-      if (lane == 0) a.span_count[sp] = count;
+    if ((k + 1) % SPAN_TILES == 0 || k + 1 == k1) {
+      if (lane == 0) a.span_count[span] = count;
       count = 0;
-      if (!have_next) break;
-      sp = nsp;
-      tt = 0;
-      const uint64_t NB = sp * SPAN_TILES * (uint64_t)TILE;
-      prev_last = ld_dw_guarded(file, flen, NB - 4);
-    } else {
-      prev_last = __builtin_amdgcn_readlane(d[15], 63);
-      tt++;
     }
-#pragma unroll
-    for (int j = 0; j < 16; j++) d[j] = nd[j];
+  };
+
+#if SRD_RING == 3
+  // 3-buffer register ring: two tiles in flight while one is processed.
+  // Tile k1 (first tile of the next wave's range, inside the padding at the
+  // end) is loaded too: its lane 0 supplies the last tile's lookahead.
+  uint32_t A[16], Bv[16], Cv[16];
+  load_tile(k0, A);
+  load_tile(k0 + 1, Bv);
+  for (uint64_t k = k0; k < k1; k += 3) {
+    if (k + 2 <= k1) load_tile(k + 2, Cv);
+    process(k, A, Bv);
+    if (k + 1 >= k1) break;
+    if (k + 3 <= k1) load_tile(k + 3, A);
+    process(k + 1, Bv, Cv);
+    if (k + 2 >= k1) break;
+    if (k + 4 <= k1) load_tile(k + 4, Bv);
+    process(k + 2, Cv, A);
   }
+#else
+  // 2-buffer ring: tile k+1 in flight while k is processed
+  uint32_t A[16], Bv[16];
+  load_tile(k0, A);
+  for (uint64_t k = k0; k < k1; k += 2) {
+    load_tile(k + 1, Bv);
+    process(k, A, Bv);
+    if (k + 1 >= k1) break;
+    load_tile(k + 2, A);
+    process(k + 1, Bv, A);
+  }
+#endif
+
   rootmax = wave_max_u64(rootmax);
   for (int o = 32; o > 0; o >>= 1) weak += __shfl_xor(weak, o);
   if (lane == 0) {

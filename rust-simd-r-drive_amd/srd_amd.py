@@ -41,7 +41,7 @@ EXPORTS = [
     "srd_validate_index_device", "srd_validate_index", "srd_result_free",
     "srd_recover_valid_chain", "srd_key_indexer_build", "srd_crc32_batch",
     "srd_crc32_batch_device", "srd_xxh3_64_batch", "srd_xxh3_64_batch_device",
-    "srd_synth_store_device", "srd_selftest_host",
+    "srd_synth_store_device", "srd_selftest_host", "srd_padded_size",
 ]
 
 
@@ -96,9 +96,12 @@ def lib():
         L.srd_crc32_batch_device.argtypes = [vp, vp, vp, vp, u64, vp, vp]
         L.srd_xxh3_64_batch.argtypes = [vp, vp, u64, vp, vp, u64, vp]
         L.srd_xxh3_64_batch_device.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+        L.srd_padded_size.argtypes = [u64]
+        L.srd_padded_size.restype = u64
         L.srd_synth_store_device.argtypes = [vp, vp, u64, u64, vp, u64, C.POINTER(u64)]
         for f in EXPORTS:
-            if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error"):
+            if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
+                         "srd_padded_size"):
                 getattr(L, f).restype = i32
         _lib = L
     return _lib
@@ -374,6 +377,11 @@ class DataStore:
 
     def len(self) -> int:
         return len(self.key_indexer)
+
+
+def padded_size(file_len: int) -> int:
+    """Bytes a device buffer for validate_index_device must be readable for."""
+    return int(lib().srd_padded_size(file_len))
 
 
 def synth_store_len(n_entries: int, payload_len: int = 4096, lens=None) -> int:

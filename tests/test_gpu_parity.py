@@ -100,7 +100,7 @@ def test_crc32_batch(ref_goldens, ctx):
 def _device_synth(n, payload_len=4096, lens=None):
     import torch
     size = S.synth_store_len(n, payload_len, lens)
-    t = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
     S.synth_store_device(t.data_ptr(), n, payload_len, lens)
     torch.cuda.synchronize()
     return t[:size].cpu().numpy()
@@ -191,7 +191,7 @@ def test_full_size_c2_properties(ctx):
     import torch
     n = 1 << 20
     size = S.synth_store_len(n)
-    t = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
     S.synth_store_device(t.data_ptr(), n, 4096, ctx=ctx)
     torch.cuda.synchronize()
     r = S.validate_index_device(t.data_ptr(), size, 0, ctx)
