@@ -36,6 +36,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int TILE = 4096;
 constexpr int SPAN_TILES = 4;
 constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
+#ifndef SRD_CRC_LINE
+#define SRD_CRC_LINE crc_line4
+#endif
 #ifndef SRD_RING
 #define SRD_RING 2
 #endif
@@ -62,6 +65,8 @@ struct DevTables {
   uint32_t invpow[4097];
   uint32_t nib[8 * 16 * 32];       // half-tile lane-weight nibble tables
   uint32_t m16k[4][256];           // v -> v * x^16384 byte tables
+  uint32_t m128[4][256];
+  uint32_t m256[4][256];
 };
 __device__ DevTables g_tabs;
 
@@ -129,6 +134,8 @@ struct ScanLds {
   uint32_t tab[4 * 256 * 32];      // 128 KiB slice-by-4 tables, conflict-free (layout: tab_lookup)
   uint32_t nib[8 * 16 * 32];       // 16 KiB: c -> c * x^(512*(31 - l%32)), bank = l%32
   uint32_t m16k[4 * 256];          // v -> v * x^16384 (lower half -> tile end)
+  uint32_t m128[4 * 256];          // v -> v * x^128  (join 16-byte chains)
+  uint32_t m256[4 * 256];          // v -> v * x^256  (join 32-byte halves)
   uint32_t win[SCAN_WAVES_V2][28];
 };
 
@@ -151,6 +158,28 @@ __device__ __forceinline__ uint32_t crc_line1(const uint32_t (&d)[16], const Sca
     s = t3 ^ t2 ^ t1 ^ t0 ^ (j < 15 ? d[j < 15 ? j + 1 : 15] : 0u);
   }
   return s;
+}
+
+__device__ __forceinline__ uint32_t mulfix(uint32_t v, const uint32_t* __restrict__ m) {
+  return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
+}
+// Same CRC as crc_line1 with 4 independent 16-byte chains (4 dependent LDS
+// round trips instead of 16), joined by c = (a*x^128 ^ b)*x^256 ^ (c*x^128 ^ d).
+__device__ __forceinline__ uint32_t crc_line4(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
+  constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
+  uint32_t s[4] = {d[0], d[4], d[8], d[12]};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t t3 = tab_lookup(L, s[q], R[3], SEL0), t2 = tab_lookup(L, s[q], R[2], SEL1);
+      const uint32_t t1 = tab_lookup(L, s[q], R[1], SEL2), t0 = tab_lookup(L, s[q], R[0], SEL3);
+      s[q] = t3 ^ t2 ^ t1 ^ t0 ^ (j < 3 ? d[4 * q + (j < 3 ? j + 1 : 3)] : 0u);
+    }
+  }
+  const uint32_t ab = mulfix(s[0], L.m128) ^ s[1];
+  const uint32_t cd = mulfix(s[2], L.m128) ^ s[3];
+  return mulfix(ab, L.m256) ^ cd;
 }
 
 template <int CTRL>
@@ -208,11 +237,17 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     lds.tab[i] = g_tabs.tab[t][b];
   }
   for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) lds.nib[i] = g_tabs.nib[i];
-  for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) lds.m16k[i] = (&g_tabs.m16k[0][0])[i];
+  for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) {
+    lds.m16k[i] = (&g_tabs.m16k[0][0])[i];
+    lds.m128[i] = (&g_tabs.m128[0][0])[i];
+    lds.m256[i] = (&g_tabs.m256[0][0])[i];
+  }
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  // wave id via readfirstlane: provably uniform, so all tile bookkeeping
+  // below (k, B, span, bounds) stays in SGPRs / scalar branches
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t R[4];
 #pragma unroll
   for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
@@ -258,7 +293,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
 
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
-    const uint32_t c = (a.ablate & 1) ? (d[0] ^ d[5] ^ d[15]) : crc_line1(d, lds, R);
+    const uint32_t c = (a.ablate & 1) ? (d[0] ^ d[5] ^ d[15]) : SRD_CRC_LINE(d, lds, R);
     const uint32_t hx = (a.ablate & 1) ? c : half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
     const uint32_t sx32 = __builtin_amdgcn_readlane(hx, 32);  // true SX_32
     if (lane < 2) a.tile[2 * k + lane] = mul16k(hx, lds.m16k) ^ sx32;  // T = SX_0, SX_1
