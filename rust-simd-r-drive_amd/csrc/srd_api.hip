@@ -17,6 +17,7 @@
 
 #include "srd_amd.h"
 #include "srd_kernels.hip"
+#include "srd_glue.hip"
 
 using namespace srd;
 
@@ -53,6 +54,11 @@ struct Ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   double scan_ms = 0, total_ms = 0;
   int scan_launches = 0;
+  // sync-free optimistic pass
+  uint64_t capK = 0;    // dense candidate capacity (grows on ST_CAPK)
+  uint32_t gen = 0;     // generation tag of has_child / childof
+  uint64_t last_n = 0;  // chain length of the previous call (index bucket sizing)
+  Plan* h_plan = nullptr;  // pinned host copy
 };
 
 enum BufId {
@@ -66,6 +72,7 @@ enum BufId {
   B_O_PIECES, B_O_SUF, B_O_SXM, B_O_TAIL, B_SLOW,
   B_HKEYS, B_HVALS, B_LATEST, B_IPOS, B_IKEY, B_IPACKED,
   B_CUB_TMP,
+  B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
   B_COUNT_
 };
 
@@ -86,6 +93,16 @@ int ensure(Ctx* c, BufId id, size_t bytes) {
 }
 template <class T>
 T* P(Ctx* c, BufId id) { return (T*)c->bufs[id].p; }
+
+// ensure + zero-fill whenever the buffer is (re)allocated
+int ensure_z(Ctx* c, BufId id, size_t bytes) {
+  void* before = c->bufs[id].p;
+  size_t nb = c->bufs[id].n;
+  int r = ensure(c, id, bytes);
+  if (r) return r;
+  if (c->bufs[id].p != before || c->bufs[id].n != nb) HIPCHK(hipMemsetAsync(c->bufs[id].p, 0, c->bufs[id].n, c->stream));
+  return 0;
+}
 
 std::once_flag g_tab_once;
 CrcTables g_host_tabs;
@@ -214,6 +231,7 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   int r = upload_tables();
   if (r) { delete c; return r; }
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipHostMalloc((void**)&c->h_plan, sizeof(Plan), hipHostMallocDefault));
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->scan_blocks = (unsigned)ncu;
@@ -229,6 +247,7 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
   if (c->file.p) hipFree(c->file.p);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
+  if (c->h_plan) hipHostFree(c->h_plan);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -276,16 +295,70 @@ static int alloc_out(Ctx* c, uint64_t n) {
   TRY(ensure(c, B_O_SXM, n * 4));
   TRY(ensure(c, B_O_TAIL, n * 4));
   TRY(ensure(c, B_SLOW, n * 8));
+  TRY(ensure(c, B_IKEY, n * 8));
+  TRY(ensure(c, B_IPACKED, n * 8));
+  return 0;
+}
+
+// global-table KeyIndexer::build workspace (full pass / skewed-bucket fallback)
+static int alloc_hash(Ctx* c, uint64_t n) {
   uint64_t hc = 64;
   while (hc < 2 * n) hc <<= 1;
   TRY(ensure(c, B_HKEYS, hc * 8));
   TRY(ensure(c, B_HVALS, hc * 8));
   TRY(ensure(c, B_LATEST, (n + 1) * 4));
   TRY(ensure(c, B_IPOS, (n + 1) * 4));
-  TRY(ensure(c, B_IKEY, n * 8));
-  TRY(ensure(c, B_IPACKED, n * 8));
   TRY(ensure_cub(c, n + 1));
   return 0;
+}
+
+// KeyIndexer::build over the n chain entries in B_O_KH / B_O_MO with one
+// global open-addressing table (device-wide atomics); syncs for the count
+static int index_global(Ctx* c, uint64_t n, uint64_t* n_index) {
+  TRY(alloc_hash(c, n));
+  uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
+  uint64_t hc = 64;
+  while (hc < 2 * n) hc <<= 1;
+  HIPCHK(hipMemsetAsync(P<void>(c, B_HKEYS), 0xff, hc * 8, c->stream));
+  HIPCHK(hipMemsetAsync(P<void>(c, B_HVALS), 0, hc * 8, c->stream));
+  HIPCHK(hipMemsetAsync(cnt + 7, 0, 8, c->stream));
+  HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_LATEST) + n, 0, 4, c->stream));
+  if (n) {
+    index_insert_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
+        P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_HKEYS),
+        P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7));
+    index_latest_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
+        P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_HKEYS),
+        P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7), P<uint32_t>(c, B_LATEST));
+    HIPCHK(hipGetLastError());
+  }
+  size_t tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_LATEST),
+                                          P<uint32_t>(c, B_IPOS), (int)(n + 1), c->stream));
+  if (n) {
+    index_emit_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO),
+                                                             P<uint32_t>(c, B_LATEST), P<uint32_t>(c, B_IPOS), n,
+                                                             P<uint64_t>(c, B_IKEY), P<uint64_t>(c, B_IPACKED));
+    HIPCHK(hipGetLastError());
+  }
+  uint32_t nidx = 0;
+  HIPCHK(hipMemcpyAsync(&nidx, P<uint32_t>(c, B_IPOS) + n, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *n_index = nidx;
+  return 0;
+}
+
+static void set_out_ptrs(Ctx* c, srd_device_result* out) {
+  out->meta_off = P<uint64_t>(c, B_O_MO);
+  out->key_hash = P<uint64_t>(c, B_O_KH);
+  out->prev_offset = P<uint64_t>(c, B_O_PREV);
+  out->payload_start = P<uint64_t>(c, B_O_START);
+  out->payload_len = P<uint64_t>(c, B_O_LEN);
+  out->crc_stored = P<uint32_t>(c, B_O_CRCST);
+  out->crc_computed = P<uint32_t>(c, B_O_CRC);
+  out->crc_ok = P<uint8_t>(c, B_O_OK);
+  out->index_key_hash = P<uint64_t>(c, B_IKEY);
+  out->index_packed = P<uint64_t>(c, B_IPACKED);
 }
 
 // finalize + index for a chain of n entries whose chain_g / walk state are set
@@ -330,60 +403,14 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
     }
   }
   // ---- KeyIndexer::build ----
-  uint64_t hc = 64;
-  while (hc < 2 * n) hc <<= 1;
-  HIPCHK(hipMemsetAsync(P<void>(c, B_HKEYS), 0xff, hc * 8, c->stream));
-  HIPCHK(hipMemsetAsync(P<void>(c, B_HVALS), 0, hc * 8, c->stream));
-  HIPCHK(hipMemsetAsync(cnt + 7, 0, 8, c->stream));
-  HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_LATEST) + n, 0, 4, c->stream));
-  if (n) {
-    index_insert_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
-        P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_HKEYS),
-        P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7));
-    index_latest_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
-        P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_HKEYS),
-        P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7), P<uint32_t>(c, B_LATEST));
-    HIPCHK(hipGetLastError());
-  }
-  size_t tb = c->bufs[B_CUB_TMP].n;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_LATEST),
-                                          P<uint32_t>(c, B_IPOS), (int)(n + 1), c->stream));
-  if (n) {
-    index_emit_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO),
-                                                             P<uint32_t>(c, B_LATEST), P<uint32_t>(c, B_IPOS), n,
-                                                             P<uint64_t>(c, B_IKEY), P<uint64_t>(c, B_IPACKED));
-    HIPCHK(hipGetLastError());
-  }
-  uint32_t nidx = 0;
-  HIPCHK(hipMemcpyAsync(&nidx, P<uint32_t>(c, B_IPOS) + n, 4, hipMemcpyDeviceToHost, c->stream));
+  uint64_t nidx = 0;
+  TRY(index_global(c, n, &nidx));
   uint64_t h[8];
   TRY(read_counters(c, h));
   out->n_index = nidx;
   out->n_crc_bad = h[6];
   out->n_chain = n;
-  out->meta_off = P<uint64_t>(c, B_O_MO);
-  out->key_hash = P<uint64_t>(c, B_O_KH);
-  out->prev_offset = P<uint64_t>(c, B_O_PREV);
-  out->payload_start = P<uint64_t>(c, B_O_START);
-  out->payload_len = P<uint64_t>(c, B_O_LEN);
-  out->crc_stored = P<uint32_t>(c, B_O_CRCST);
-  out->crc_computed = P<uint32_t>(c, B_O_CRC);
-  out->crc_ok = P<uint8_t>(c, B_O_OK);
-  out->index_key_hash = P<uint64_t>(c, B_IKEY);
-  out->index_packed = P<uint64_t>(c, B_IPACKED);
-  return 0;
-}
-
-// is the 8-byte p-field of tail t zero (t is a root)?  host reads 8 bytes
-static int tail_is_root(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t t, bool* is_root) {
-  *is_root = false;
-  if (t < 21 || t > flen) return 0;
-  uint8_t b[8];
-  HIPCHK(hipMemcpyAsync(b, d_file + t - 12, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  uint64_t v;
-  memcpy(&v, b, 8);
-  *is_root = v == 0;
+  set_out_ptrs(c, out);
   return 0;
 }
 
@@ -395,7 +422,8 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     TRY(ensure_cub(c, n_spans + 1));
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
     HIPCHK(hipMemsetAsync(cnt, 0, 64, c->stream));
-    HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT), 0, (n_spans + 1) * 4, c->stream));
+    // the scan writes every span's count; only the scan sentinel needs a zero
+    HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT) + n_spans, 0, 4, c->stream));
     ScanArgs a{};
     a.file = d_file;
     a.flen = flen;
@@ -473,6 +501,230 @@ static int set_single_root(Ctx* c, uint64_t t) {
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// Optimistic pass, sync-free: scan (strong candidates only) -> link -> shape
+// check -> chain scatter -> finalize -> bucketed index, all counts on the
+// device; one host sync at the end.  *done=false sends the call to the full
+// pass (the check could not prove the chain from file_len).
+static int alloc_fast(Ctx* c, uint64_t capK, uint32_t log2_nbk) {
+  TRY(ensure(c, B_DM, capK * 8));
+  TRY(ensure(c, B_DPAR, capK * 8));
+  TRY(ensure(c, B_DSLOT, capK * 8));
+  TRY(ensure_z(c, B_HASCHILD, capK * 4));
+  TRY(ensure_z(c, B_CHILDOF, capK * 8));
+  TRY(ensure(c, B_FLAG, capK));
+  TRY(ensure(c, B_CHAIN_G, (capK + 1) * 8));
+  TRY(ensure(c, B_PART, GLUE_BLOCKS * 4));
+  TRY(ensure(c, B_PARTEX, GLUE_BLOCKS * 4));
+  TRY(ensure(c, B_PLAN, sizeof(Plan)));
+  TRY(alloc_out(c, capK + 1));
+  const uint64_t nh = ((uint64_t)1 << log2_nbk) * IDX_HBLOCKS + 1;
+  TRY(ensure(c, B_HIST, nh * 4));
+  TRY(ensure(c, B_HOFF, nh * 4));
+  TRY(ensure(c, B_SKEY, (capK + 1) * 8));
+  TRY(ensure(c, B_SIDX, (capK + 1) * 4));
+  TRY(ensure(c, B_LATEST8, capK + 1));
+  TRY(ensure_cub(c, nh));
+  return 0;
+}
+
+static int optimistic_pass(Ctx* c, const uint8_t* d_file, uint64_t flen, uint32_t flags, srd_device_result* out,
+                           bool* done) {
+  *done = false;
+  const uint64_t n_tiles = (flen + TILE - 1) / TILE;
+  const uint64_t n_spans = (n_tiles + SPAN_TILES - 1) / SPAN_TILES;
+  for (int attempt = 0; attempt < 6; attempt++) {
+    if (!c->capK) c->capK = flen / 1024 + 4096;
+    const uint64_t capK = c->capK;
+    if (capK >= (1ull << 32) - 2) { set_err("too many chain candidates"); return SRD_ERR_INTERNAL; }
+    // index buckets: ~IDX_BUCKET_AVG chain entries per bucket
+    const uint64_t n_est = std::max<uint64_t>(c->last_n ? c->last_n : capK / 4, 1);
+    uint32_t log2_nbk = 1;  // >= 1: the bucket is the hash's top log2_nbk bits
+    while (log2_nbk < 14 && ((uint64_t)IDX_BUCKET_AVG << log2_nbk) < n_est) log2_nbk++;
+    TRY(alloc_scan(c, n_tiles, n_spans));
+    TRY(ensure_cub(c, n_spans + 1));
+    TRY(alloc_fast(c, capK, log2_nbk));
+    if (++c->gen == 0) {  // tag wrap: clear the marks once
+      c->gen = 1;
+      HIPCHK(hipMemsetAsync(P<void>(c, B_HASCHILD), 0, c->bufs[B_HASCHILD].n, c->stream));
+      HIPCHK(hipMemsetAsync(P<void>(c, B_CHILDOF), 0, c->bufs[B_CHILDOF].n, c->stream));
+    }
+    Plan* pl = P<Plan>(c, B_PLAN);
+    uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
+    HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
+    HIPCHK(hipMemsetAsync(cnt, 0, 64, c->stream));
+    // the scan writes every span's count; only the scan sentinel needs a zero
+    HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT) + n_spans, 0, 4, c->stream));
+    ScanArgs a{};
+    a.file = d_file;
+    a.flen = flen;
+    a.n_tiles = n_tiles;
+    a.n_spans = n_spans;
+    a.cap = c->cap;
+    a.tile = P<uint32_t>(c, B_TILE);
+    a.span_count = P<uint32_t>(c, B_SPAN_COUNT);
+    a.c_m = P<uint64_t>(c, B_CM);
+    a.c_rec = P<u32x4>(c, B_CREC);
+    a.counters = (unsigned long long*)cnt;
+    {
+      const char* ab = getenv("SRD_SCAN_ABLATE");
+      a.ablate = ab ? (uint32_t)atoi(ab) : 0u;
+    }
+    const unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    scan_kernel<false><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    size_t tb = c->bufs[B_CUB_TMP].n;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_SPAN_COUNT),
+                                            P<uint64_t>(c, B_SPAN_BASE), (int)(n_spans + 1), c->stream));
+    Link2Args l{};
+    l.file = d_file;
+    l.flen = flen;
+    l.n_spans = n_spans;
+    l.capK = capK;
+    l.cap = c->cap;
+    l.gen = c->gen;
+    l.span_count = P<uint32_t>(c, B_SPAN_COUNT);
+    l.span_base = P<uint64_t>(c, B_SPAN_BASE);
+    l.c_m = P<uint64_t>(c, B_CM);
+    l.c_rec = P<u32x4>(c, B_CREC);
+    l.d_m = P<uint64_t>(c, B_DM);
+    l.d_par = P<int64_t>(c, B_DPAR);
+    l.d_slot = P<uint64_t>(c, B_DSLOT);
+    l.has_child = P<uint32_t>(c, B_HASCHILD);
+    link2_kernel<<<blocks(n_spans, 64), 256, 0, c->stream>>>(l);
+    ShapeArgs sa{};
+    sa.file = d_file;
+    sa.flen = flen;
+    sa.capK = capK;
+    sa.gen = c->gen;
+    sa.Kp = P<uint64_t>(c, B_SPAN_BASE) + n_spans;
+    sa.d_m = l.d_m;
+    sa.d_par = l.d_par;
+    sa.d_slot = l.d_slot;
+    sa.c_rec = l.c_rec;
+    sa.has_child = l.has_child;
+    sa.childof = P<uint64_t>(c, B_CHILDOF);
+    sa.flag = P<uint8_t>(c, B_FLAG);
+    sa.part = P<uint32_t>(c, B_PART);
+    sa.part_ex = P<uint32_t>(c, B_PARTEX);
+    sa.chain_g = P<uint64_t>(c, B_CHAIN_G);
+    sa.counters = (const unsigned long long*)cnt;
+    sa.plan = pl;
+    child2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
+    check_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
+    plan_kernel<<<1, 1024, 0, c->stream>>>(sa);
+    scatter2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
+    HIPCHK(hipGetLastError());
+    // ---- finalize (per chain entry outputs + CRC) ----
+    FinArgs f{};
+    f.file = d_file;
+    f.flen = flen;
+    f.n_chain = 0;
+    f.chain_g = sa.chain_g;
+    f.slot = l.d_slot;
+    f.par = l.d_par;
+    f.ws = nullptr;
+    f.c_m = l.c_m;
+    f.c_rec = l.c_rec;
+    f.tile = a.tile;
+    f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
+    f.d_n_chain = &pl->n_chain;
+    f.d_root_t = &pl->root_t;
+    f.d_status = &pl->status;
+    f.o_mo = P<uint64_t>(c, B_O_MO);
+    f.o_kh = P<uint64_t>(c, B_O_KH);
+    f.o_prev = P<uint64_t>(c, B_O_PREV);
+    f.o_start = P<uint64_t>(c, B_O_START);
+    f.o_len = P<uint64_t>(c, B_O_LEN);
+    f.o_crc_st = P<uint32_t>(c, B_O_CRCST);
+    f.o_crc = P<uint32_t>(c, B_O_CRC);
+    f.o_pieces = P<uint32_t>(c, B_O_PIECES);
+    f.o_suf = P<uint32_t>(c, B_O_SUF);
+    f.o_sxm = P<uint32_t>(c, B_O_SXM);
+    f.o_tail = P<uint32_t>(c, B_O_TAIL);
+    f.o_ok = P<uint8_t>(c, B_O_OK);
+    f.slow_list = P<uint64_t>(c, B_SLOW);
+    f.n_slow = (unsigned long long*)&pl->n_slow;
+    f.n_bad = (unsigned long long*)&pl->n_bad;
+    finalize_kernel<<<2048, 256, 0, c->stream>>>(f);
+    if (!f.no_crc) slow_kernel<<<256, 64, 0, c->stream>>>(f);
+    HIPCHK(hipGetLastError());
+    // ---- KeyIndexer::build (bucketed) ----
+    IdxArgs ia{};
+    ia.kh = f.o_kh;
+    ia.mo = f.o_mo;
+    ia.n_dev = &pl->n_chain;
+    ia.status = &pl->status;
+    ia.log2_nbk = log2_nbk;
+    ia.histT = P<uint32_t>(c, B_HIST);
+    ia.hoff = P<uint32_t>(c, B_HOFF);
+    ia.skey = P<uint64_t>(c, B_SKEY);
+    ia.sidx = P<uint32_t>(c, B_SIDX);
+    ia.latest = P<uint8_t>(c, B_LATEST8);
+    ia.part = sa.part;
+    ia.part_ex = sa.part_ex;
+    ia.okey = P<uint64_t>(c, B_IKEY);
+    ia.opacked = P<uint64_t>(c, B_IPACKED);
+    ia.plan = pl;
+    const uint32_t nbk = 1u << log2_nbk;
+    const int nh = (int)((uint64_t)nbk * IDX_HBLOCKS + 1);
+    idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+    tb = c->bufs[B_CUB_TMP].n;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, ia.histT, ia.hoff, nh, c->stream));
+    idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+    idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
+    idx_count_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
+    idx_scan_kernel<<<1, 1024, 0, c->stream>>>(ia);
+    idx_emit_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const Plan hp = *c->h_plan;
+    if (getenv("SRD_DEBUG")) {
+      std::vector<uint32_t> ho(std::min(nh, 300));
+      hipMemcpy(ho.data(), ia.hoff, ho.size() * 4, hipMemcpyDeviceToHost);
+      fprintf(stderr, "plan K=%lu n_chain=%lu root_t=%lu start=%lu n_index=%lu bad=%lu slow=%lu st=%u nroot=%u troot=%u idxov=%u log2nbk=%u capK=%lu\n",
+              (unsigned long)hp.K, (unsigned long)hp.n_chain, (unsigned long)hp.root_t, (unsigned long)hp.start,
+              (unsigned long)hp.n_index, (unsigned long)hp.n_bad, (unsigned long)hp.n_slow, hp.status, hp.nroot,
+              hp.troot, hp.idx_overflow, log2_nbk, (unsigned long)capK);
+      fprintf(stderr, "hoff:");
+      for (size_t i = 0; i < ho.size(); i += 16) fprintf(stderr, " %u", ho[i]);
+      fprintf(stderr, " last=%u\n", ho.back());
+    }
+    {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+      c->scan_ms += ms;
+      c->scan_launches++;
+    }
+    out->n_candidates = hp.K;
+    out->n_weak = hp.n_weak;
+    if (hp.status & ST_OVERFLOW) {
+      if (c->cap >= SPAN_BYTES) { set_err("candidate overflow"); return SRD_ERR_INTERNAL; }
+      c->cap = (uint32_t)std::min<uint64_t>((uint64_t)c->cap * 4, SPAN_BYTES);
+      continue;
+    }
+    if (hp.status & ST_CAPK) {
+      c->capK = hp.cap_need + hp.cap_need / 4 + 4096;
+      continue;
+    }
+    if (hp.status) return 0;  // not provable here -> full pass
+    out->final_len = flen;
+    out->n_chain = hp.n_chain;
+    out->n_crc_bad = hp.n_bad;
+    out->n_index = hp.n_index;
+    c->last_n = hp.n_chain;
+    if (hp.idx_overflow) TRY(index_global(c, hp.n_chain, &out->n_index));
+    set_out_ptrs(c, out);
+    *done = true;
+    return 0;
+  }
+  return 0;
+}
+
 static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen, uint32_t flags,
                                 srd_device_result* out);
 
@@ -514,36 +766,12 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
   }
   bool full = flags & SRD_FLAG_FORCE_FULL;
   uint64_t K = 0, h[8];
-  // ---- optimistic pass: strong candidates only; valid iff the walk from
-  //      file_len reaches a root through recorded nodes ----
+  // ---- optimistic pass: strong candidates only; valid iff the chain from
+  //      file_len is proven through recorded nodes ----
   if (!full) {
-    TRY(run_scan(c, d_file, flen, false, &K, h));
-    out->n_candidates = K;
-    out->n_weak = h[1];
-    bool root = false;
-    TRY(tail_is_root(c, d_file, flen, flen, &root));
-    if (root) {
-      TRY(set_single_root(c, flen));
-      out->final_len = flen;
-      return finish(c, d_file, flen, 1, flags, out);
-    }
-    uint64_t lastm = ~0ull;
-    if (K) {
-      HIPCHK(hipMemcpyAsync(&lastm, P<uint64_t>(c, B_DM) + K - 1, 8, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
-    }
-    if (K && lastm == flen - 20) {
-      WalkState w{};
-      w.start = K - 1;
-      HIPCHK(hipMemcpyAsync(P<WalkState>(c, B_WALK), &w, sizeof w, hipMemcpyHostToDevice, c->stream));
-      WalkState hw{};
-      TRY(walk_and_mark(c, P<int64_t>(c, B_DPAR), P<uint64_t>(c, B_DSLOT), K, nullptr, &hw));
-      if (hw.status == 1) {
-        out->final_len = flen;
-        return finish(c, d_file, flen, hw.chain_len, flags, out);
-      }
-    }
-    full = true;  // could not conclude: every candidate is needed
+    bool done = false;
+    TRY(optimistic_pass(c, d_file, flen, flags, out, &done));
+    if (done) return 0;
   }
   // ---- full pass ----
   out->mode = 1;

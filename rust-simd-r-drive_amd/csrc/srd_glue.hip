@@ -1,0 +1,409 @@
+// srd_glue.hip -- sync-free glue of the optimistic pass (included by srd_api.hip
+// after srd_kernels.hip).
+//
+// Everything between the streaming scan and the final result runs with the
+// counts kept in device memory (struct Plan), so the host enqueues the whole
+// pass and synchronises once at the end:
+//
+//   link2   parent lookup per candidate (4 lanes per span), marks has_child
+//   child2  every core node (has a child, or is the start node at file_len-20)
+//           publishes itself as its parent's child: childof[p] = gen:g
+//   check   shape test + per-block core counts: the core nodes must form ONE
+//           chain from the start down to a root (each core node's parent
+//           names it as the child, every core node but the start has a core
+//           child, exactly one core node links to a root).  Leaves (false
+//           candidates nobody links to) are ignored -- the same pruning as
+//           recover_valid_chain's walk only ever following back-pointers
+//           from file_len (data_store.rs:404-470).  A failed test sends the
+//           call to the full pass; it never changes a result.
+//   plan    one block: scans the block counts, decides n_chain / status
+//   scatter chain_g[1 + rank] = record slot of core node g (file order)
+//   finalize / slow (srd_kernels.hip) with n_chain read from the plan
+//   index   KeyIndexer::build (key_indexer.rs:98-124) as a bucketed build:
+//           hist -> exclusive scan -> scatter into XXH3 buckets -> one block
+//           per bucket dedups in an LDS open-addressing table (latest wins)
+//           -> count / scan / emit in chain order.
+//
+// Generation tags (gen:g in one u64, gen in has_child) make the per-node
+// marks self-invalidating between calls, so no per-call memsets are needed.
+#pragma once
+
+namespace srd {
+
+struct Plan {
+  uint64_t K;          // dense candidates
+  uint64_t n_chain;    // chain entries incl. the root entry
+  uint64_t root_t;     // tail of the root entry
+  uint64_t start;      // dense index of the node at file_len - 20, or ~0
+  uint64_t n_index;
+  uint64_t n_bad;      // chain entries whose CRC mismatches
+  uint64_t n_slow;     // finalize entries handed to slow_kernel
+  uint64_t chain_core; // core nodes (n_chain - 1 on success)
+  uint64_t max_root, n_weak, overflow;  // copies of the scan counters
+  uint64_t cap_need;   // K when it exceeds the dense capacity
+  uint32_t status;     // ST_* bits; 0 = the optimistic result is final
+  uint32_t nroot;      // core nodes linking to a root
+  uint32_t troot;      // file_len itself is a root tail
+  uint32_t idx_overflow;
+};
+constexpr uint32_t ST_NOSTART = 1, ST_SHAPE = 2, ST_ROOTS = 4, ST_CAPK = 8, ST_OVERFLOW = 16;
+constexpr uint64_t NO_NODE = ~0ull;
+
+constexpr int GLUE_BLOCKS = 1024;  // chunked grid of the count/scatter kernels
+constexpr int GLUE_THREADS = 256;
+
+// rank of `f` among the 256 flags of this block iteration (exclusive) and the
+// iteration's total; wsum is LDS[4]
+__device__ __forceinline__ uint32_t block_rank256(bool f, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t bal = __ballot(f);
+  const uint32_t pre = (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+  if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t v = wsum[i];
+    off += i < w ? v : 0u;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + pre;
+}
+
+__device__ __forceinline__ uint32_t block_sum256(uint32_t v, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+  if (lane == 0) wsum[w] = v;
+  __syncthreads();
+  const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ void chunk_of(uint64_t n, uint64_t* lo, uint64_t* hi) {
+  const uint64_t ch = (n + gridDim.x - 1) / gridDim.x;
+  *lo = min(n, (uint64_t)blockIdx.x * ch);
+  *hi = min(n, *lo + ch);
+}
+
+// exclusive scan of up to 1024 partials with one 1024-thread block
+__device__ uint64_t block_scan_partials(const uint32_t* part, uint32_t np, uint32_t* part_ex) {
+  __shared__ uint64_t s[1024];
+  const uint32_t t = threadIdx.x;
+  uint64_t v = t < np ? part[t] : 0;
+  s[t] = v;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    const uint64_t a = t >= o ? s[t - o] : 0;
+    __syncthreads();
+    s[t] += a;
+    __syncthreads();
+  }
+  if (t < np) part_ex[t] = (uint32_t)(s[t] - v);
+  const uint64_t total = s[1023];
+  __syncthreads();
+  return total;
+}
+
+// --------------------------------------------------------------------------
+struct Link2Args {
+  const uint8_t* file;
+  uint64_t flen, n_spans, capK;
+  uint32_t cap, gen;
+  const uint32_t* span_count;
+  const uint64_t* span_base;
+  const uint64_t* c_m;
+  const u32x4* c_rec;
+  uint64_t* d_m;
+  int64_t* d_par;
+  uint64_t* d_slot;
+  uint32_t* has_child;
+};
+
+__global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
+  const uint64_t sp = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  if (sp >= a.n_spans) return;
+  const uint32_t n = min(a.span_count[sp], a.cap);
+  const uint64_t gb = a.span_base[sp];
+  for (uint32_t i = threadIdx.x & 3; i < n; i += 4) {
+    const uint64_t gi = sp * a.cap + i, g = gb + i;
+    if (g >= a.capK) return;  // plan_kernel reports ST_CAPK
+    const u32x4 r0 = a.c_rec[2 * gi];
+    const uint64_t m = a.c_m[gi], p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+    const uint64_t mp = p - 20;  // p >= 20 by construction
+    const uint64_t sp2 = mp / SPAN_BYTES;
+    int64_t par = PAR_MISS;
+    if (sp2 < a.n_spans) {
+      const uint32_t n2 = min(a.span_count[sp2], a.cap);
+      uint32_t lo = 0, hi = n2;
+      const uint64_t* cm = a.c_m + sp2 * a.cap;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cm[mid] < mp) lo = mid + 1; else hi = mid;
+      }
+      if (lo < n2 && cm[lo] == mp) par = (int64_t)(a.span_base[sp2] + lo);
+    }
+    if (par == PAR_MISS && p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) par = PAR_ROOT;
+    a.d_m[g] = m;
+    a.d_par[g] = par;
+    a.d_slot[g] = gi;
+    if (par >= 0 && (uint64_t)par < a.capK) a.has_child[par] = a.gen;
+  }
+}
+
+struct ShapeArgs {
+  const uint8_t* file;
+  uint64_t flen, capK;
+  uint32_t gen;
+  const uint64_t* Kp;  // span_base + n_spans
+  const uint64_t* d_m;
+  const int64_t* d_par;
+  const uint64_t* d_slot;
+  const u32x4* c_rec;
+  const uint32_t* has_child;
+  uint64_t* childof;
+  uint8_t* flag;
+  uint32_t* part;
+  uint32_t* part_ex;
+  uint64_t* chain_g;
+  const unsigned long long* counters;
+  Plan* plan;
+};
+
+__device__ __forceinline__ uint64_t start_node(const ShapeArgs& a, uint64_t K) {
+  return (K && a.d_m[K - 1] == a.flen - 20) ? K - 1 : NO_NODE;
+}
+
+__global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
+  const uint64_t K = *a.Kp;
+  if (K > a.capK) return;
+  const uint64_t start = start_node(a, K);
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x) {
+    const bool core = a.has_child[g] == a.gen || g == start;
+    const int64_t p = a.d_par[g];
+    if (core && p >= 0) a.childof[p] = ((uint64_t)a.gen << 32) | g;
+  }
+}
+
+__global__ __launch_bounds__(256) void check_kernel(ShapeArgs a) {
+  __shared__ uint32_t wsum[4];
+  const uint64_t K = *a.Kp;
+  if (K > a.capK) return;
+  const uint64_t start = start_node(a, K);
+  const uint64_t tag = (uint64_t)a.gen << 32;
+  uint64_t lo, hi;
+  chunk_of(K, &lo, &hi);
+  uint32_t cnt = 0;
+  bool fail = false;
+  for (uint64_t g = lo + threadIdx.x; g < hi; g += blockDim.x) {
+    const bool core = a.has_child[g] == a.gen || g == start;
+    a.flag[g] = core;
+    if (!core) continue;
+    cnt++;
+    const int64_t p = a.d_par[g];
+    if (p == PAR_ROOT) {
+      atomicAdd(&a.plan->nroot, 1u);
+      const u32x4 r0 = a.c_rec[2 * a.d_slot[g]];
+      a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+    } else if (p < 0) {
+      fail = true;  // dangling: the chain through g is broken
+    } else if (a.childof[p] != (tag | g)) {
+      fail = true;  // branch: another core node claims the same parent
+    }
+    if (g != start && (a.childof[g] & ~0xffffffffull) != tag) fail = true;  // core node without a core child
+  }
+  const uint32_t tot = block_sum256(cnt, wsum);
+  if (__syncthreads_or(fail) && threadIdx.x == 0) atomicOr(&a.plan->status, ST_SHAPE);
+  if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
+}
+
+// one block of 1024 threads
+__global__ __launch_bounds__(1024) void plan_kernel(ShapeArgs a) {
+  const uint64_t K = *a.Kp;
+  const bool capk = K > a.capK;
+  const uint64_t total = block_scan_partials(a.part, capk ? 0u : (uint32_t)GLUE_BLOCKS, a.part_ex);
+  if (threadIdx.x) return;
+  Plan* pl = a.plan;
+  uint32_t st = pl->status;
+  pl->K = K;
+  pl->max_root = a.counters[0];
+  pl->n_weak = a.counters[1];
+  pl->overflow = a.counters[2];
+  const bool troot = ld_u64_unaligned(a.file, a.flen - 12) == 0;  // flen >= 21 here
+  pl->troot = troot;
+  if (troot) {  // file_len is itself a root tail: chain = that one entry
+    pl->status = 0;
+    pl->n_chain = 1;
+    pl->root_t = a.flen;
+    pl->chain_core = 0;
+    return;
+  }
+  if (capk) { st |= ST_CAPK; pl->cap_need = K; }
+  if (a.counters[2]) st |= ST_OVERFLOW;
+  const uint64_t start = capk ? NO_NODE : start_node(a, K);
+  pl->start = start;
+  if (start == NO_NODE) st |= ST_NOSTART;
+  if (pl->nroot != 1) st |= ST_ROOTS;
+  pl->status = st;
+  pl->chain_core = total;
+  pl->n_chain = st ? 0 : 1 + total;
+}
+
+__global__ __launch_bounds__(256) void scatter2_kernel(ShapeArgs a) {
+  __shared__ uint32_t wsum[4];
+  if (a.plan->status || a.plan->troot) return;
+  const uint64_t K = *a.Kp;
+  uint64_t lo, hi;
+  chunk_of(K, &lo, &hi);
+  uint64_t run = 1 + (uint64_t)a.part_ex[blockIdx.x];
+  for (uint64_t base = lo; base < hi; base += blockDim.x) {
+    const uint64_t g = base + threadIdx.x;
+    const bool f = g < hi && a.flag[g];
+    uint32_t tot;
+    const uint32_t r = block_rank256(f, wsum, &tot);
+    if (f) a.chain_g[run + r] = a.d_slot[g];  // chain entry -> candidate record slot
+    run += tot;
+  }
+}
+
+// --------------------------------------------------------------------------
+// KeyIndexer::build, bucketed
+// --------------------------------------------------------------------------
+constexpr int IDX_HBLOCKS = 512;     // histogram / scatter blocks
+constexpr int IDX_TSLOTS = 4096;     // LDS open-addressing slots per bucket block (max)
+constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
+constexpr int IDX_BUCKET_AVG = 1024; // host sizes the bucket count for this average
+constexpr uint64_t IDX_EMPTY = ~0ull;
+
+struct IdxArgs {
+  const uint64_t* kh;    // chain key hashes (o_kh)
+  const uint64_t* mo;    // chain meta offsets (o_mo)
+  const uint64_t* n_dev; // &plan->n_chain
+  const uint32_t* status;
+  uint32_t log2_nbk;
+  uint32_t* histT;       // [nbk * IDX_HBLOCKS + 1]
+  uint32_t* hoff;        // exclusive scan of histT
+  uint64_t* skey;        // bucket-ordered keys
+  uint32_t* sidx;        // bucket-ordered chain indices
+  uint8_t* latest;       // [n] 1 = latest entry of its key
+  uint32_t* part;
+  uint32_t* part_ex;
+  uint64_t* okey;
+  uint64_t* opacked;
+  Plan* plan;
+};
+
+__device__ __forceinline__ uint64_t idx_n(const IdxArgs& a) { return *a.status ? 0 : *a.n_dev; }
+
+__global__ __launch_bounds__(256) void idx_hist_kernel(IdxArgs a) {
+  extern __shared__ uint32_t lds_u32[];
+  const uint32_t nbk = 1u << a.log2_nbk;
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.histT[(uint64_t)nbk * IDX_HBLOCKS] = 0;  // scan -> total
+  __syncthreads();
+  uint64_t lo, hi;
+  chunk_of(idx_n(a), &lo, &hi);
+  for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x)
+    atomicAdd(&lds_u32[xxh3_64_u64(a.kh[c]) >> (64 - a.log2_nbk)], 1u);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) a.histT[(uint64_t)k * IDX_HBLOCKS + blockIdx.x] = lds_u32[k];
+}
+
+__global__ __launch_bounds__(256) void idx_scatter_kernel(IdxArgs a) {
+  extern __shared__ uint32_t lds_u32[];
+  const uint32_t nbk = 1u << a.log2_nbk;
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = a.hoff[(uint64_t)k * IDX_HBLOCKS + blockIdx.x];
+  __syncthreads();
+  uint64_t lo, hi;
+  chunk_of(idx_n(a), &lo, &hi);
+  for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) {
+    const uint64_t k = a.kh[c];
+    const uint32_t pos = atomicAdd(&lds_u32[xxh3_64_u64(k) >> (64 - a.log2_nbk)], 1u);
+    a.skey[pos] = k;
+    a.sidx[pos] = (uint32_t)c;
+  }
+}
+
+// one block per bucket: latest-wins dedup in LDS
+__global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
+  __shared__ unsigned long long keys[IDX_TSLOTS];
+  __shared__ uint32_t vals[IDX_TSLOTS];
+  __shared__ uint32_t special;
+  if (*a.status) return;
+  const uint32_t k = blockIdx.x;
+  const uint64_t lo = a.hoff[(uint64_t)k * IDX_HBLOCKS], hi = a.hoff[(uint64_t)(k + 1) * IDX_HBLOCKS];
+  if (hi == lo) return;
+  if (hi - lo > IDX_TCAP) {  // skewed bucket: the host reruns the global-table build
+    if (threadIdx.x == 0) a.plan->idx_overflow = 1;
+    return;
+  }
+  uint32_t slots = 64;
+  while (slots < 2 * (hi - lo)) slots <<= 1;  // load <= 1/2
+  const uint32_t M = slots - 1;
+  for (uint32_t i = threadIdx.x; i < slots; i += blockDim.x) { keys[i] = IDX_EMPTY; vals[i] = 0; }
+  if (threadIdx.x == 0) special = 0;
+  __syncthreads();
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint64_t key = a.skey[i];
+    const uint32_t v = a.sidx[i] + 1;
+    if (key == IDX_EMPTY) { atomicMax(&special, v); continue; }
+    uint32_t s = (uint32_t)xxh3_64_u64(key) & M;
+    while (true) {
+      const unsigned long long old = atomicCAS(&keys[s], (unsigned long long)IDX_EMPTY, (unsigned long long)key);
+      if (old == IDX_EMPTY || old == key) { atomicMax(&vals[s], v); break; }
+      s = (s + 1) & M;
+    }
+  }
+  __syncthreads();
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint64_t key = a.skey[i];
+    const uint32_t c = a.sidx[i];
+    uint32_t best;
+    if (key == IDX_EMPTY) best = special;
+    else {
+      uint32_t s = (uint32_t)xxh3_64_u64(key) & M;
+      while (keys[s] != key) s = (s + 1) & M;
+      best = vals[s];
+    }
+    a.latest[c] = best == c + 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void idx_count_kernel(IdxArgs a) {
+  __shared__ uint32_t wsum[4];
+  uint64_t lo, hi;
+  chunk_of(idx_n(a), &lo, &hi);
+  uint32_t cnt = 0;
+  for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) cnt += a.latest[c];
+  const uint32_t t = block_sum256(cnt, wsum);
+  if (threadIdx.x == 0) a.part[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(1024) void idx_scan_kernel(IdxArgs a) {
+  const uint64_t total = block_scan_partials(a.part, GLUE_BLOCKS, a.part_ex);
+  if (threadIdx.x == 0) a.plan->n_index = total;
+}
+
+__global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
+  __shared__ uint32_t wsum[4];
+  uint64_t lo, hi;
+  chunk_of(idx_n(a), &lo, &hi);
+  uint64_t run = a.part_ex[blockIdx.x];
+  for (uint64_t base = lo; base < hi; base += blockDim.x) {
+    const uint64_t c = base + threadIdx.x;
+    const bool f = c < hi && a.latest[c];
+    uint32_t tot;
+    const uint32_t r = block_rank256(f, wsum, &tot);
+    if (f) {
+      const uint64_t key = a.kh[c];
+      a.okey[run + r] = key;
+      a.opacked[run + r] = ((key >> 48) << 48) | (a.mo[c] & 0xFFFFFFFFFFFFull);  // key_indexer.rs:79-85
+    }
+    run += tot;
+  }
+}
+
+}  // namespace srd

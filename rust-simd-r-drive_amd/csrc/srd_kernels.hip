@@ -621,6 +621,12 @@ struct FinArgs {
   const u32x4* c_rec;
   const uint32_t* tile;      // [2k] = T_k (SX_0), [2k+1] = SX_1
   int no_crc;
+  // device-side plan (sync-free path): when set, n_chain / root_t come from
+  // device memory and a nonzero *status disables the kernel
+  // and chain_g holds record slots (the parent of chain entry c >= 2 is entry c-1)
+  const uint64_t* d_n_chain;
+  const uint64_t* d_root_t;
+  const uint32_t* d_status;
   // outputs
   uint64_t *o_mo, *o_kh, *o_prev, *o_start, *o_len;
   uint32_t *o_crc_st, *o_crc, *o_pieces;  // o_pieces: bit0 suf ok, bit1 sxm ok (slow path input)
@@ -664,14 +670,25 @@ __device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint
   return ~(mulp(g_tabs.invpow[dd], y) ^ tail);
 }
 
+__device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t);
 __global__ void finalize_kernel(FinArgs a) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.n_chain) return;
+  uint64_t n = a.n_chain, root_t = 0;
+  if (a.d_status) {
+    if (*a.d_status) return;
+    n = *a.d_n_chain;
+    root_t = *a.d_root_t;
+  } else if (a.ws) {
+    root_t = a.ws->root_t;
+  }
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (uint64_t)gridDim.x * blockDim.x)
+    finalize_one(a, c, root_t);
+}
+__device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
   uint64_t mo, kh, p, start, len;
   uint32_t crc_st, suf = 0, sxm = 0, tail = 0, pieces = 0;
   bool tomb;
   if (c == 0) {
-    const uint64_t t = a.ws->root_t;
+    const uint64_t t = root_t;
     mo = t - 20;
     kh = ld_u64_unaligned(a.file, mo);
     crc_st = ld_u32_unaligned(a.file, mo + 16);
@@ -682,7 +699,7 @@ __global__ void finalize_kernel(FinArgs a) {
     pieces = 1;
   } else {
     const uint64_t g = a.chain_g[c];
-    const uint64_t gi = a.slot[g];
+    const uint64_t gi = a.d_status ? g : a.slot[g];
     mo = a.c_m[gi];
     const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
     p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
@@ -693,9 +710,9 @@ __global__ void finalize_kernel(FinArgs a) {
     start = tomb ? p : p + prepad64(p);
     if (fl & F_SXM) { sxm = r1[1]; pieces |= 2; }
     if (fl & F_TAIL) { tail = 0; pieces |= 4; }
-    const int64_t pg = a.par[g];
+    const int64_t pg = a.d_status ? (c >= 2 ? 0 : PAR_ROOT) : a.par[g];
     if (pg >= 0) {
-      const uint64_t pgi = a.slot[pg];
+      const uint64_t pgi = a.d_status ? a.chain_g[c - 1] : a.slot[pg];
       const u32x4 pr1 = a.c_rec[2 * pgi + 1];
       const uint32_t kind = (pr1[3] >> F_SUF_SHIFT) & 3;
       const uint64_t k0 = start / TILE;
@@ -739,15 +756,24 @@ __global__ void finalize_kernel(FinArgs a) {
   }
 }
 
-// Recompute, with one wave, SX at line j of tile k.
-__device__ uint32_t tile_probe_sx(const uint8_t* file, uint64_t flen, uint64_t k, uint32_t j) {
+// Recompute, with one wave, SX at line j of tile k (bytes past flen read as 0;
+// the buffer is readable to srd_padded_size).  tab = the 4x256 CRC table in LDS.
+__device__ uint32_t tile_probe_sx(const uint8_t* file, uint64_t flen, uint64_t k, uint32_t j, const uint32_t* tab) {
   const int lane = threadIdx.x & 63;
   const uint64_t L = k * TILE + 64ull * lane;
+  const u32x4* p = (const u32x4*)(file + L);
   uint32_t s = 0;
-  for (int q = 0; q < 64; q++) {
-    const uint64_t o = L + q;
-    const uint32_t byte = o < flen ? file[o] : 0u;
-    s = g_tabs.tab[0][(s ^ byte) & 0xff] ^ (s >> 8);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const u32x4 v = p[q];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const uint64_t o = L + 16 * q + 4 * e;
+      uint32_t w = v[e];
+      if (o + 4 > flen) w = o >= flen ? 0u : (w & (0xffffffffu >> (8 * (4 - (uint32_t)(flen - o)))));
+      s ^= w;
+      s = tab[768 + (s & 0xff)] ^ tab[512 + ((s >> 8) & 0xff)] ^ tab[256 + ((s >> 16) & 0xff)] ^ tab[s >> 24];
+    }
   }
   uint32_t sx = mulp(g_tabs.lw[lane], s);
   for (int o = 1; o < 64; o <<= 1) {
@@ -759,13 +785,17 @@ __device__ uint32_t tile_probe_sx(const uint8_t* file, uint64_t flen, uint64_t k
 
 // one wave per slow entry (a piece of the combine was not recorded)
 __global__ __launch_bounds__(64) void slow_kernel(FinArgs a) {
+  __shared__ uint32_t tab[1024];
   const unsigned long long ns = *a.n_slow;
+  if (blockIdx.x >= ns) return;
+  for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = g_tabs.tab[i >> 8][i & 255];
+  __syncthreads();
   for (uint64_t w = blockIdx.x; w < ns; w += gridDim.x) {
     const uint64_t c = a.slow_list[w];
     const uint64_t s = a.o_start[c], m = a.o_mo[c];
     uint32_t pieces = a.o_pieces[c], suf = a.o_suf[c], sxm = a.o_sxm[c], tail = a.o_tail[c];
-    if (!(pieces & 1)) suf = tile_probe_sx(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64));
-    if (!(pieces & 2)) sxm = tile_probe_sx(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64));
+    if (!(pieces & 1)) suf = tile_probe_sx(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64), tab);
+    if (!(pieces & 2)) sxm = tile_probe_sx(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64), tab);
     if ((threadIdx.x & 63) == 0) {
       const uint32_t crc = crc_from_pieces(s, m, suf, sxm, tail, a.tile);
       a.o_crc[c] = crc;
