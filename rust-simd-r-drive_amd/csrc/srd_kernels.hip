@@ -37,10 +37,10 @@ constexpr int TILE = 4096;
 constexpr int SPAN_TILES = 4;
 constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
 #ifndef SRD_CRC_LINE
-#define SRD_CRC_LINE crc_line4
+#define SRD_CRC_LINE crc_line1
 #endif
 #ifndef SRD_RING
-#define SRD_RING 2
+#define SRD_RING 3
 #endif
 #ifndef SRD_REPL
 #define SRD_REPL 32
@@ -54,6 +54,9 @@ constexpr int64_t PAR_MISS = -2;
 // flags of a candidate record
 constexpr uint32_t F_TOMB = 1u, F_TAIL = 2u, F_SXM = 4u;
 constexpr int F_SUF_SHIFT = 3;        // 2 bits: 0 value, 1 next-tile T, 2 next-tile SX1, 3 missing
+// the recorded sxm / suf value is a lower-half partial (line < 32): true value =
+// mul16k(v) ^ SX_32 of the tile holding m (sxm) or the entry start (suf kind 0) -- see lo_fix()
+constexpr uint32_t F_SXM_LO = 32u, F_SUF_LO = 64u;
 
 struct DevTables {
   uint32_t tab[4][256];
@@ -75,12 +78,13 @@ struct ScanArgs {
   uint64_t flen;
   uint64_t n_tiles, n_spans;
   uint32_t cap;
-  uint32_t* tile;                  // [2*n_tiles]: SX_0 (= tile CRC), SX_1
+  uint32_t* tile;                  // [4*n_tiles]: half-tile partials h_0, h_1, SX_32 (tile_sx())
   uint32_t* span_count;
   uint64_t* c_m;                   // [n_spans*cap] candidate metadata offsets
   u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
   unsigned long long* counters;    // [0] max root tail, [1] weak, [2] overflow
   uint32_t ablate;                 // timing experiments only (SRD_SCAN_ABLATE): 1 no CRC, 2 no slow path, 4 no filter
+  uint32_t filt_mask;              // byte mask M (x4): a node's p-byte 4 has (byte & M) == 0 since p < file_len
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -106,6 +110,11 @@ __device__ __forceinline__ uint32_t mask_past_end(uint32_t v, uint64_t o, uint64
   if (o + 4 <= n) return v;
   if (o >= n) return 0u;
   return v & ((1u << (8 * (uint32_t)(n - o))) - 1u);
+}
+__device__ __forceinline__ uint32_t mask_past_end32(uint32_t v, uint32_t o, uint32_t n) {
+  if (o + 4 <= n) return v;
+  if (o >= n) return 0u;
+  return v & ((1u << (8 * (n - o))) - 1u);
 }
 
 __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t sh) {
@@ -133,7 +142,6 @@ constexpr int MREPL = 8;  // replication of the x^256 multiply table
 struct ScanLds {
   uint32_t tab[4 * 256 * 32];      // 128 KiB slice-by-4 tables, conflict-free (layout: tab_lookup)
   uint32_t nib[8 * 16 * 32];       // 16 KiB: c -> c * x^(512*(31 - l%32)), bank = l%32
-  uint32_t m16k[4 * 256];          // v -> v * x^16384 (lower half -> tile end)
   uint32_t m128[4 * 256];          // v -> v * x^128  (join 16-byte chains)
   uint32_t m256[4 * 256];          // v -> v * x^256  (join 32-byte halves)
   uint32_t win[SCAN_WAVES_V2][28];
@@ -209,9 +217,12 @@ __device__ __forceinline__ uint32_t suffix_xor(uint32_t v, int lane) {
 // tile end, i.e. final; lanes < 32: relative to line 31, corrected on use).
 __device__ __forceinline__ uint32_t lane_weight(uint32_t c, const uint32_t* __restrict__ nib, int lane) {
   uint32_t u = 0;
-  const int t = lane & 31;
+  const char* base = (const char*)(nib + (lane & 31));
 #pragma unroll
-  for (int pos = 0; pos < 8; pos++) u ^= nib[((pos * 16 + ((c >> (4 * pos)) & 15)) << 5) + t];
+  for (int pos = 0; pos < 8; pos++) {
+    const uint32_t nb = __builtin_amdgcn_ubfe(c, 4 * pos, 4);
+    u ^= *(const uint32_t*)(base + pos * 2048 + (nb << 7));  // nib[((pos*16 + nb) << 5) + lane%32]
+  }
   return u;
 }
 __device__ __forceinline__ uint32_t mul16k(uint32_t v, const uint32_t* __restrict__ m) {
@@ -238,7 +249,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   }
   for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) lds.nib[i] = g_tabs.nib[i];
   for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) {
-    lds.m16k[i] = (&g_tabs.m16k[0][0])[i];
     lds.m128[i] = (&g_tabs.m128[0][0])[i];
     lds.m256[i] = (&g_tabs.m256[0][0])[i];
   }
@@ -264,7 +274,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   const uint64_t k1 = min((s0 + spw) * SPAN_TILES, a.n_tiles);
   if (k0 >= k1) return;
 
-  uint64_t rootmax = 0, weak = 0;
   uint32_t count = 0;
 
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
@@ -281,52 +290,60 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 
   uint32_t prev_last = k0 ? ld_dw_guarded(file, flen, k0 * (uint64_t)TILE - 4) : 0u;
 
+  const uint32_t M = a.filt_mask;
+  uint64_t rootmax = 0;
+  uint32_t weak = 0;
+
   // process tile k held in d[]; nx[] holds tile k+1 when k+1 < k1
   auto process = [&](uint64_t k, uint32_t (&d)[16], const uint32_t (&nx)[16]) {
     const uint64_t B = k * (uint64_t)TILE;
     const uint64_t span = k / SPAN_TILES;
-    const bool tail_tile = B + TILE + 64 > flen;  // uniform; bytes >= flen read as 0
+    // bytes left in the file from B (uniform, 32-bit: every in-tile test below
+    // is relative to B, so the uniform bookkeeping stays on the scalar unit)
+    const uint32_t remu = (uint32_t)min(flen - B, (uint64_t)0xFFFFFFFFu);
+    const bool tail_tile = TILE + 64 > remu;  // uniform; bytes >= flen read as 0
     if (tail_tile) {
-      const uint64_t L = B + 64ull * lane;
 #pragma unroll
-      for (int j = 0; j < 16; j++) d[j] = mask_past_end(d[j], L + 4 * j, flen);
+      for (int j = 0; j < 16; j++) d[j] = mask_past_end32(d[j], 64u * lane + 4 * j, remu);
     }
 
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
     const uint32_t c = (a.ablate & 1) ? (d[0] ^ d[5] ^ d[15]) : SRD_CRC_LINE(d, lds, R);
     const uint32_t hx = (a.ablate & 1) ? c : half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
-    const uint32_t sx32 = __builtin_amdgcn_readlane(hx, 32);  // true SX_32
-    if (lane < 2) a.tile[2 * k + lane] = mul16k(hx, lds.m16k) ^ sx32;  // T = SX_0, SX_1
+    // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32
+    if (lane < 2 || lane == 32) a.tile[4 * k + (lane == 32 ? 2 : lane)] = hx;
 
     // ---- neighbour bytes ----
     uint32_t look[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) {
-      const uint32_t dn = dpp<DPP_WAVE_SHL1>(d[j]);
-      // lane 63: first bytes of tile k+1 = lane 0 of the prefetched buffer (it is
-      // the OLDER of the two tiles in flight, so waiting for it keeps k+2 flying)
+      // lane 63: first bytes of tile k+1 = lane 0 of the prefetched buffer (the
+      // OLDER of the tiles in flight)
       uint32_t nxv = __builtin_amdgcn_readlane(nx[j], 0);
-      if (tail_tile) nxv = mask_past_end(nxv, B + TILE + 4 * j, flen);
+      if (tail_tile) nxv = mask_past_end32(nxv, TILE + 4 * j, remu);
+      const uint32_t dn = dpp<DPP_WAVE_SHL1>(d[j]);
       look[j] = lane == 63 ? nxv : dn;
     }
     uint32_t prevdw = dpp<DPP_WAVE_SHR1>(d[15]);
     if (lane == 0) prevdw = prev_last;
     prev_last = __builtin_amdgcn_readlane(d[15], 63);
 
-    // ---- filter: a node at m has zero bytes m+13..m+15 (the top of p < 2^40).
-    //      Exact zero-triple test for triple starts q = m+13 in [L+13, L+76]. ----
-    uint32_t acc = 0, acc3 = 0, acc19 = 0;
+    // ---- filter: a node at m has p = le64(m+8..m+16) < file_len < 2^40, so
+    //      bytes m+13..m+15 are zero and byte m+12 & M is zero.  Runs are
+    //      tested by their first byte s = m+12 in [L+12, L+75]:
+    //      x = (b[s] & M) | b[s+1] | b[s+2] | b[s+3] per byte lane. ----
+    auto wd_at = [&](int i) -> uint32_t { return i < 16 ? d[i] : look[i - 16]; };
+    uint32_t acc = 0;
+    uint32_t r2 = wd_at(3) | alignb(wd_at(4), wd_at(3), 8);  // b[s] | b[s+1]
 #pragma unroll
-    for (int i = 3; i < 20; i++) {
-      const uint32_t wd = i < 16 ? d[i] : look[i - 16];
-      const uint32_t wn = (i + 1) < 16 ? d[i + 1] : look[i + 1 - 16];
-      const uint32_t x = wd | alignb(wn, wd, 8) | alignb(wn, wd, 16);
-      const uint32_t z = (x - 0x01010101u) & ~x;  // bit 7 of byte k: a zero byte at/below k
-      if (i == 3) acc3 = z;
-      else if (i == 19) acc19 = z;
-      else acc |= z;
+    for (int i = 3; i < 19; i++) {  // s = 4i..4i+3, exactly [12, 75]
+      const uint32_t wd = wd_at(i), wn = wd_at(i + 1), wnn = wd_at(i + 2);
+      const uint32_t r2n = wn | alignb(wnn, wn, 8);
+      const uint32_t x = (wd & M) | alignb(wn, wd, 8) | alignb(r2n, r2, 16);
+      r2 = r2n;
+      acc |= (x - 0x01010101u) & ~x;  // bit 7 of byte k set somewhere <=> x has a zero byte
     }
-    acc = (acc & 0x80808080u) | (acc3 & 0x80808000u) | (acc19 & 0x00000080u);
+    acc &= 0x80808080u;
     uint64_t slow = __ballot(acc != 0);
     if (a.ablate & 2) slow = 0;
 
@@ -344,7 +361,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const uint32_t b = lane;
-      const uint64_t m = B + 64ull * f + b;
+      const uint32_t r = 64u * f + b;  // m - B
       const int base = 4 + (b >> 2);
       const uint32_t sh = (b & 3) * 8;
       uint32_t W[6];
@@ -358,30 +375,33 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint32_t f0 = alignb(W[1], W[0], sh), f1 = alignb(W[2], W[1], sh);
       const uint32_t f2 = alignb(W[3], W[2], sh), f3 = alignb(W[4], W[3], sh);
       const uint32_t f4 = alignb(W[5], W[4], sh);
+      // recover_valid_chain's node test (data_store.rs:404-470) at m = B + r
+      const bool inrange = (r + 20 <= remu) && (B != 0 || r != 0);
+      const uint64_t roots = __ballot(inrange && (f2 | f3) == 0);
+      if (roots) rootmax = B + 64u * f + (63 - __builtin_clzll(roots)) + 20;  // increasing in (k, f)
+      const uint64_t m = B + r;
       const uint64_t p = (uint64_t)f2 | ((uint64_t)f3 << 32);
-      const bool inrange = (m >= 1) && (m + 20 <= flen);
-      if (inrange && p == 0) rootmax = rootmax > m + 20 ? rootmax : m + 20;
-      const bool tomb = (m > p) && (m - p == 1) && tbyte == 0;
-      const uint64_t start = tomb ? p : p + prepad64(p);
-      const bool isnode = inrange && p != 0 && start < m && p < m && p >= 20;
+      const uint64_t dp = m - p;
+      const bool tomb = dp == 1 && tbyte == 0;
+      const uint32_t pp = (0u - f2) & 63u;  // prepad(p)
+      const bool isnode = inrange && p >= 20 && p < m && (tomb || dp > pp);
       const bool strong = isnode && (FULL || f4 != 0);
-      weak += (isnode && !strong) ? 1 : 0;
-      const uint64_t t = m + 20;
-      const uint32_t js = (uint32_t)((t + prepad64(t) - B) >> 6);  // line of the next entry's start
+      weak += (uint32_t)__popcll(__ballot(isnode && !strong));
+      const uint32_t t = r + 20;
+      const uint32_t js = (t + ((0u - t) & 63u)) >> 6;  // line of the next entry's start
       const uint32_t hs = __shfl(hx, (int)(js & 63));
-      const uint32_t sufv = (js & 63) >= 32 ? hs : (mul16k(hs, lds.m16k) ^ sx32);
       const uint32_t hm = __builtin_amdgcn_readlane(hx, f);
-      const uint32_t sxm = f >= 32 ? hm : (mul16k(hm, lds.m16k) ^ sx32);
       const uint64_t cm = __ballot(strong);
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
         if (idx < a.cap) {
           const uint64_t gi = span * a.cap + idx;
           const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
+          const uint32_t fl = (tomb ? F_TOMB : 0u) | (b == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT) |
+                              (f < 32 ? F_SXM_LO : 0u) | ((js & 63) < 32 ? F_SUF_LO : 0u);
           a.c_m[gi] = m;
           a.c_rec[2 * gi] = u32x4{f2, f3, f0, f1};
-          a.c_rec[2 * gi + 1] = u32x4{f4, sxm, sufv,
-                                      (tomb ? F_TOMB : 0u) | (b == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT)};
+          a.c_rec[2 * gi + 1] = u32x4{f4, hm, hs, fl};
         } else {
           atomicOr((unsigned int*)(a.counters + 2), 1u);
         }
@@ -424,8 +444,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   }
 #endif
 
-  rootmax = wave_max_u64(rootmax);
-  for (int o = 32; o > 0; o >>= 1) weak += __shfl_xor(weak, o);
+  // rootmax / weak are wave-uniform already
   if (lane == 0) {
     if (rootmax) atomicMax(a.counters + 0, (unsigned long long)rootmax);
     if (weak) atomicAdd(a.counters + 1, (unsigned long long)weak);
@@ -619,7 +638,7 @@ struct FinArgs {
   const WalkState* ws;
   const uint64_t* c_m;
   const u32x4* c_rec;
-  const uint32_t* tile;      // [2k] = T_k (SX_0), [2k+1] = SX_1
+  const uint32_t* tile;      // [4k..4k+2] per-tile values (tile_T / tile_SX1)
   int no_crc;
   // device-side plan (sync-free path): when set, n_chain / root_t come from
   // device memory and a nonzero *status disables the kernel
@@ -652,6 +671,21 @@ __device__ __forceinline__ uint32_t tail_crc(const uint8_t* file, uint64_t m) {
   return s;
 }
 
+// per-tile values: tile[4k] / tile[4k+1] = half-tile partials of lines 0 / 1,
+// tile[4k+2] = SX_32.  A lower-half partial v becomes the true suffix value
+// SX_j = v * x^16384 ^ SX_32.
+__device__ __forceinline__ uint32_t mul16k_g(uint32_t v) {
+  return g_tabs.m16k[0][v & 0xff] ^ g_tabs.m16k[1][(v >> 8) & 0xff] ^ g_tabs.m16k[2][(v >> 16) & 0xff] ^
+         g_tabs.m16k[3][v >> 24];
+}
+__device__ __forceinline__ uint32_t lo_fix(const uint32_t* tile, uint64_t k, uint32_t v) {
+  return mul16k_g(v) ^ tile[4 * k + 2];
+}
+__device__ __forceinline__ uint32_t tile_T(const uint32_t* tile, uint64_t k) { return lo_fix(tile, k, tile[4 * k]); }
+__device__ __forceinline__ uint32_t tile_SX1(const uint32_t* tile, uint64_t k) {
+  return lo_fix(tile, k, tile[4 * k + 1]);
+}
+
 __device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint32_t suf, uint32_t sxm,
                                                     uint32_t tail, const uint32_t* tile) {
   const uint64_t len = m - s;
@@ -663,8 +697,8 @@ __device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint
   if (k0 == k1) {
     y = acc ^ sxm;
   } else {
-    for (uint64_t k = k0 + 1; k < k1; k++) acc = mulp(g_tabs.x32768, acc) ^ tile[2 * k];
-    y = mulp(g_tabs.x32768, acc) ^ tile[2 * k1] ^ sxm;
+    for (uint64_t k = k0 + 1; k < k1; k++) acc = mulp(g_tabs.x32768, acc) ^ tile_T(tile, k);
+    y = mulp(g_tabs.x32768, acc) ^ tile_T(tile, k1) ^ sxm;
   }
   const uint64_t dd = (k1 + 1) * TILE - m;
   return ~(mulp(g_tabs.invpow[dd], y) ^ tail);
@@ -695,7 +729,7 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
     p = 0;
     tomb = false;  // start is 0 either way
     start = 0;
-    suf = a.tile[0];
+    suf = tile_T(a.tile, 0);
     pieces = 1;
   } else {
     const uint64_t g = a.chain_g[c];
@@ -708,19 +742,22 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
     const uint32_t fl = r1[3];
     tomb = fl & F_TOMB;
     start = tomb ? p : p + prepad64(p);
-    if (fl & F_SXM) { sxm = r1[1]; pieces |= 2; }
+    if (fl & F_SXM) {
+      sxm = (fl & F_SXM_LO) ? lo_fix(a.tile, mo / TILE, r1[1]) : r1[1];
+      pieces |= 2;
+    }
     if (fl & F_TAIL) { tail = 0; pieces |= 4; }
     const int64_t pg = a.d_status ? (c >= 2 ? 0 : PAR_ROOT) : a.par[g];
     if (pg >= 0) {
       const uint64_t pgi = a.d_status ? a.chain_g[c - 1] : a.slot[pg];
       const u32x4 pr1 = a.c_rec[2 * pgi + 1];
       const uint32_t kind = (pr1[3] >> F_SUF_SHIFT) & 3;
-      const uint64_t k0 = start / TILE;
-      if (kind == 0) { suf = pr1[2]; pieces |= 1; }
-      else if (kind == 1) { suf = a.tile[2 * k0]; pieces |= 1; }
-      else if (kind == 2) { suf = a.tile[2 * k0 + 1]; pieces |= 1; }
+      const uint64_t k0 = start / TILE;  // kind 0: the parent's tile; 1, 2: the next one
+      if (kind == 0) { suf = (pr1[3] & F_SUF_LO) ? lo_fix(a.tile, k0, pr1[2]) : pr1[2]; pieces |= 1; }
+      else if (kind == 1) { suf = tile_T(a.tile, k0); pieces |= 1; }
+      else if (kind == 2) { suf = tile_SX1(a.tile, k0); pieces |= 1; }
     } else if (start == 0) {
-      suf = a.tile[0];
+      suf = tile_T(a.tile, 0);
       pieces |= 1;
     }
   }
