@@ -145,14 +145,6 @@ int upload_tables() {
   return 0;
 }
 
-// scan filter byte mask: p < file_len bounds p's byte 4 by (file_len-1) >> 32
-uint32_t filt_mask(uint64_t flen) {
-  const uint64_t hb = (flen ? flen - 1 : 0) >> 32;
-  uint32_t bits = 0;
-  while (bits < 8 && (hb >> bits)) bits++;
-  return ((0xFFu << bits) & 0xFFu) * 0x01010101u;
-}
-
 inline unsigned blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 #define TRY(x)                 \
@@ -443,7 +435,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.c_m = P<uint64_t>(c, B_CM);
     a.c_rec = P<u32x4>(c, B_CREC);
     a.counters = (unsigned long long*)cnt;
-    a.filt_mask = filt_mask(flen);
+    a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
     {
       const char* ab = getenv("SRD_SCAN_ABLATE");
       a.ablate = ab ? (uint32_t)atoi(ab) : 0u;
@@ -576,7 +568,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_file, uint64_t flen, uint32_
     a.c_m = P<uint64_t>(c, B_CM);
     a.c_rec = P<u32x4>(c, B_CREC);
     a.counters = (unsigned long long*)cnt;
-    a.filt_mask = filt_mask(flen);
+    a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
     {
       const char* ab = getenv("SRD_SCAN_ABLATE");
       a.ablate = ab ? (uint32_t)atoi(ab) : 0u;

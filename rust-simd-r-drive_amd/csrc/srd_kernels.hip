@@ -32,6 +32,7 @@
 namespace srd {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int TILE = 4096;
 constexpr int SPAN_TILES = 4;
@@ -84,7 +85,7 @@ struct ScanArgs {
   u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
   unsigned long long* counters;    // [0] max root tail, [1] weak, [2] overflow
   uint32_t ablate;                 // timing experiments only (SRD_SCAN_ABLATE): 1 no CRC, 2 no slow path, 4 no filter
-  uint32_t filt_mask;              // byte mask M (x4): a node's p-byte 4 has (byte & M) == 0 since p < file_len
+  uint32_t filt_hb;                // (file_len-1) >> 32: bound of a node's p-byte 4 (p < file_len < 2^40)
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -155,6 +156,9 @@ __device__ __forceinline__ uint32_t tab_lookup(const ScanLds& L, uint32_t s, uin
   const uint32_t addr = __builtin_amdgcn_perm(s, R, sel);
   return *(const uint32_t*)((const char*)L.tab + addr);
 }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // one v_bitop3_b32
+}
 __device__ __forceinline__ uint32_t crc_line1(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
   // byte j of S0 = selector 4+j; S1 bytes 0 and 2 = selectors 0 and 2; 0x0c = zero
   constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
@@ -163,7 +167,7 @@ __device__ __forceinline__ uint32_t crc_line1(const uint32_t (&d)[16], const Sca
   for (int j = 0; j < 16; j++) {
     const uint32_t t3 = tab_lookup(L, s, R[3], SEL0), t2 = tab_lookup(L, s, R[2], SEL1);
     const uint32_t t1 = tab_lookup(L, s, R[1], SEL2), t0 = tab_lookup(L, s, R[0], SEL3);
-    s = t3 ^ t2 ^ t1 ^ t0 ^ (j < 15 ? d[j < 15 ? j + 1 : 15] : 0u);
+    s = xor3(xor3(t3, t2, j < 15 ? d[j < 15 ? j + 1 : 15] : 0u), t1, t0);  // 2 VALU per step
   }
   return s;
 }
@@ -216,14 +220,14 @@ __device__ __forceinline__ uint32_t suffix_xor(uint32_t v, int lane) {
 // to the end of the lane's HALF of the tile (lanes >= 32: relative to the
 // tile end, i.e. final; lanes < 32: relative to line 31, corrected on use).
 __device__ __forceinline__ uint32_t lane_weight(uint32_t c, const uint32_t* __restrict__ nib, int lane) {
-  uint32_t u = 0;
+  uint32_t v[8];
   const char* base = (const char*)(nib + (lane & 31));
 #pragma unroll
   for (int pos = 0; pos < 8; pos++) {
     const uint32_t nb = __builtin_amdgcn_ubfe(c, 4 * pos, 4);
-    u ^= *(const uint32_t*)(base + pos * 2048 + (nb << 7));  // nib[((pos*16 + nb) << 5) + lane%32]
+    v[pos] = *(const uint32_t*)(base + pos * 2048 + (nb << 7));  // nib[((pos*16 + nb) << 5) + lane%32]
   }
-  return u;
+  return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6] ^ v[7]);
 }
 __device__ __forceinline__ uint32_t mul16k(uint32_t v, const uint32_t* __restrict__ m) {
   return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
@@ -290,7 +294,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 
   uint32_t prev_last = k0 ? ld_dw_guarded(file, flen, k0 * (uint64_t)TILE - 4) : 0u;
 
-  const uint32_t M = a.filt_mask;
+  const uint32_t hb = a.filt_hb;
   uint64_t rootmax = 0;
   uint32_t weak = 0;
 
@@ -300,7 +304,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     const uint64_t span = k / SPAN_TILES;
     // bytes left in the file from B (uniform, 32-bit: every in-tile test below
     // is relative to B, so the uniform bookkeeping stays on the scalar unit)
-    const uint32_t remu = (uint32_t)min(flen - B, (uint64_t)0xFFFFFFFFu);
+    const uint64_t rem64 = flen - B;
+    const uint32_t remu = (rem64 >> 32) ? 0xFFFFFFFFu : (uint32_t)rem64;
     const bool tail_tile = TILE + 64 > remu;  // uniform; bytes >= flen read as 0
     if (tail_tile) {
 #pragma unroll
@@ -329,22 +334,22 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     prev_last = __builtin_amdgcn_readlane(d[15], 63);
 
     // ---- filter: a node at m has p = le64(m+8..m+16) < file_len < 2^40, so
-    //      bytes m+13..m+15 are zero and byte m+12 & M is zero.  Runs are
-    //      tested by their first byte s = m+12 in [L+12, L+75]:
-    //      x = (b[s] & M) | b[s+1] | b[s+2] | b[s+3] per byte lane. ----
+    //      bytes m+13..m+15 are zero and byte m+12 <= hb = (file_len-1) >> 32:
+    //      the byte sum of the window b[m+12..m+15] is <= hb.  One
+    //      v_qsad_pk_u16_u8 gives the four window sums starting in a dword;
+    //      windows start at s = m+12 in [12, 75] = dwords 3..18. ----
     auto wd_at = [&](int i) -> uint32_t { return i < 16 ? d[i] : look[i - 16]; };
-    uint32_t acc = 0;
-    uint32_t r2 = wd_at(3) | alignb(wd_at(4), wd_at(3), 8);  // b[s] | b[s+1]
+    u16x2 mlo = {0xFFFF, 0xFFFF}, mhi = {0xFFFF, 0xFFFF};
 #pragma unroll
-    for (int i = 3; i < 19; i++) {  // s = 4i..4i+3, exactly [12, 75]
-      const uint32_t wd = wd_at(i), wn = wd_at(i + 1), wnn = wd_at(i + 2);
-      const uint32_t r2n = wn | alignb(wnn, wn, 8);
-      const uint32_t x = (wd & M) | alignb(wn, wd, 8) | alignb(r2n, r2, 16);
-      r2 = r2n;
-      acc |= (x - 0x01010101u) & ~x;  // bit 7 of byte k set somewhere <=> x has a zero byte
+    for (int i = 3; i < 19; i++) {
+      const uint64_t pr = ((uint64_t)wd_at(i + 1) << 32) | wd_at(i);
+      const uint64_t q = __builtin_amdgcn_qsad_pk_u16_u8(pr, 0u, 0ull);
+      mlo = __builtin_elementwise_min(mlo, __builtin_bit_cast(u16x2, (uint32_t)q));
+      mhi = __builtin_elementwise_min(mhi, __builtin_bit_cast(u16x2, (uint32_t)(q >> 32)));
     }
-    acc &= 0x80808080u;
-    uint64_t slow = __ballot(acc != 0);
+    const u16x2 mm = __builtin_elementwise_min(mlo, mhi);
+    const bool acc = min((uint32_t)mm[0], (uint32_t)mm[1]) <= hb;
+    uint64_t slow = __ballot(acc);
     if (a.ablate & 2) slow = 0;
 
     while (slow) {
