@@ -333,23 +333,20 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     if (lane == 0) prevdw = prev_last;
     prev_last = __builtin_amdgcn_readlane(d[15], 63);
 
-    // ---- filter: a node at m has p = le64(m+8..m+16) < file_len < 2^40, so
-    //      bytes m+13..m+15 are zero and byte m+12 <= hb = (file_len-1) >> 32:
-    //      the byte sum of the window b[m+12..m+15] is <= hb.  One
-    //      v_qsad_pk_u16_u8 gives the four window sums starting in a dword;
-    //      windows start at s = m+12 in [12, 75] = dwords 3..18. ----
+    // ---- filter, level 1: a node at m has p = le64(m+8..m+16) < file_len
+    //      < 2^40, so bytes m+13..m+15 are zero and contain an aligned zero
+    //      halfword inside [L+14, L+77] (m in [L, L+63]).  16-bit has-zero
+    //      test, 2 VALU per dword; the exact test (p >> 32 <= hb) runs per
+    //      position in the slow path. ----
     auto wd_at = [&](int i) -> uint32_t { return i < 16 ? d[i] : look[i - 16]; };
-    u16x2 mlo = {0xFFFF, 0xFFFF}, mhi = {0xFFFF, 0xFFFF};
+    uint32_t acc = 0;
 #pragma unroll
-    for (int i = 3; i < 19; i++) {
-      const uint64_t pr = ((uint64_t)wd_at(i + 1) << 32) | wd_at(i);
-      const uint64_t q = __builtin_amdgcn_qsad_pk_u16_u8(pr, 0u, 0ull);
-      mlo = __builtin_elementwise_min(mlo, __builtin_bit_cast(u16x2, (uint32_t)q));
-      mhi = __builtin_elementwise_min(mhi, __builtin_bit_cast(u16x2, (uint32_t)(q >> 32)));
+    for (int i = 3; i < 20; i++) {  // dword 3: high half (14,15) only; dword 19: low half (76,77) only
+      const uint32_t w = i == 3 ? (wd_at(i) | 0x0000FFFFu) : i == 19 ? (wd_at(i) | 0xFFFF0000u) : wd_at(i);
+      acc |= (w + 0xFFFEFFFFu) & ~w;  // one v_add + one v_bitop3
     }
-    const u16x2 mm = __builtin_elementwise_min(mlo, mhi);
-    const bool acc = min((uint32_t)mm[0], (uint32_t)mm[1]) <= hb;
-    uint64_t slow = __ballot(acc);
+    acc &= 0x80008000u;
+    uint64_t slow = __ballot(acc != 0);
     if (a.ablate & 2) slow = 0;
 
     while (slow) {
@@ -376,9 +373,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // level 2, exact: p >> 32 <= (file_len-1) >> 32 (roots: p == 0 pass too)
+      const uint32_t f3 = alignb(W[4], W[3], sh);
+      if (!__ballot(f3 <= hb)) continue;
       const uint32_t tbyte = (tdw >> (((15 + b) & 3) * 8)) & 0xffu;
       const uint32_t f0 = alignb(W[1], W[0], sh), f1 = alignb(W[2], W[1], sh);
-      const uint32_t f2 = alignb(W[3], W[2], sh), f3 = alignb(W[4], W[3], sh);
+      const uint32_t f2 = alignb(W[3], W[2], sh);
       const uint32_t f4 = alignb(W[5], W[4], sh);
       // recover_valid_chain's node test (data_store.rs:404-470) at m = B + r
       const bool inrange = (r + 20 <= remu) && (B != 0 || r != 0);
