@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     const u32x4 r0 = a.c_rec[2 * gi];
     const uint64_t m = a.c_m[gi], p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     const uint64_t mp = p - 20;  // p >= 20 by construction
-    const uint64_t sp2 = mp / SPAN_BYTES;
+    const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
     int64_t par = PAR_MISS;
     if (sp2 < a.n_spans) {
       const uint32_t n2 = min(a.span_count[sp2], a.cap);

@@ -84,7 +84,7 @@ struct ScanArgs {
   uint64_t* c_m;                   // [n_spans*cap] candidate metadata offsets
   u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
   unsigned long long* counters;    // [0] max root tail, [1] weak, [2] overflow
-  uint32_t ablate;                 // timing experiments only (SRD_SCAN_ABLATE): 1 no CRC, 2 no slow path, 4 no filter
+  uint32_t ablate;                 // timing experiments only (SRD_SCAN_ABLATE): 1 no CRC, 2 no slow path, 4 slow path stops after the exact test
   uint32_t filt_hb;                // (file_len-1) >> 32: bound of a node's p-byte 4 (p < file_len < 2^40)
 };
 
@@ -145,7 +145,7 @@ struct ScanLds {
   uint32_t nib[8 * 16 * 32];       // 16 KiB: c -> c * x^(512*(31 - l%32)), bank = l%32
   uint32_t m128[4 * 256];          // v -> v * x^128  (join 16-byte chains)
   uint32_t m256[4 * 256];          // v -> v * x^256  (join 32-byte halves)
-  uint32_t win[SCAN_WAVES_V2][28];
+  uint32_t win[SCAN_WAVES_V2][24];
 };
 
 // Slice-by-4 with v_perm addressing.  LDS layout of the 4 tables: word
@@ -186,12 +186,27 @@ __device__ __forceinline__ uint32_t crc_line4(const uint32_t (&d)[16], const Sca
     for (int q = 0; q < 4; q++) {
       const uint32_t t3 = tab_lookup(L, s[q], R[3], SEL0), t2 = tab_lookup(L, s[q], R[2], SEL1);
       const uint32_t t1 = tab_lookup(L, s[q], R[1], SEL2), t0 = tab_lookup(L, s[q], R[0], SEL3);
-      s[q] = t3 ^ t2 ^ t1 ^ t0 ^ (j < 3 ? d[4 * q + (j < 3 ? j + 1 : 3)] : 0u);
+      s[q] = xor3(xor3(t3, t2, j < 3 ? d[4 * q + (j < 3 ? j + 1 : 3)] : 0u), t1, t0);
     }
   }
   const uint32_t ab = mulfix(s[0], L.m128) ^ s[1];
   const uint32_t cd = mulfix(s[2], L.m128) ^ s[3];
   return mulfix(ab, L.m256) ^ cd;
+}
+// 2 independent 32-byte chains joined by c = a*x^256 ^ b
+__device__ __forceinline__ uint32_t crc_line2(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
+  constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
+  uint32_t s[2] = {d[0], d[8]};
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint32_t t3 = tab_lookup(L, s[q], R[3], SEL0), t2 = tab_lookup(L, s[q], R[2], SEL1);
+      const uint32_t t1 = tab_lookup(L, s[q], R[1], SEL2), t0 = tab_lookup(L, s[q], R[0], SEL3);
+      s[q] = xor3(xor3(t3, t2, j < 7 ? d[8 * q + (j < 7 ? j + 1 : 7)] : 0u), t1, t0);
+    }
+  }
+  return mulfix(s[0], L.m256) ^ s[1];
 }
 
 template <int CTRL>
@@ -292,13 +307,36 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
   };
 
-  uint32_t prev_last = k0 ? ld_dw_guarded(file, flen, k0 * (uint64_t)TILE - 4) : 0u;
-
+  // Candidate coverage: lane l of tile k tests the positions
+  // m in [L-14, L+49] (L = B + 64 l): a node's zero bytes m+13..m+15 hold an
+  // aligned zero halfword inside the lane's OWN line, so no lookahead is
+  // needed.  Tile k covers [B-14, B+4082), span s covers
+  // [16 KiB s - 14, 16 KiB (s+1) - 14) -- link2_kernel looks parents up in
+  // span (m + 14) / 16 KiB.  The slow path stages the 22-dword window
+  // [L-16, L+72) in LDS: win[0..3] the previous line's tail, win[4..19] the
+  // line, win[20..21] the next line's head; win[22] holds the previous
+  // tile's SX partial of line 63 (= its true SX_63).
   const uint32_t hb = a.filt_hb;
   uint64_t rootmax = 0;
   uint32_t weak = 0;
+  {
+    // the line just before this wave's first tile: its tail bytes and its raw
+    // CRC (= SX_63 of tile k0-1) seed the window; all lanes load it
+    uint32_t pl[16];
+    const u32x4* q = (const u32x4*)(file + (k0 ? k0 * (uint64_t)TILE - 64 : 0));
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const u32x4 v = q[j];
+      pl[4 * j] = v[0]; pl[4 * j + 1] = v[1]; pl[4 * j + 2] = v[2]; pl[4 * j + 3] = v[3];
+    }
+    const uint32_t cp = SRD_CRC_LINE(pl, lds, R);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) win[j] = k0 ? pl[12 + j] : 0u;
+      win[22] = k0 ? cp : 0u;
+    }
+  }
 
-  // process tile k held in d[]; nx[] holds tile k+1 when k+1 < k1
   auto process = [&](uint64_t k, uint32_t (&d)[16], const uint32_t (&nx)[16]) {
     const uint64_t B = k * (uint64_t)TILE;
     const uint64_t span = k / SPAN_TILES;
@@ -318,73 +356,66 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32
     if (lane < 2 || lane == 32) a.tile[4 * k + (lane == 32 ? 2 : lane)] = hx;
 
-    // ---- neighbour bytes ----
-    uint32_t look[5];
-#pragma unroll
-    for (int j = 0; j < 5; j++) {
-      // lane 63: first bytes of tile k+1 = lane 0 of the prefetched buffer (the
-      // OLDER of the tiles in flight)
-      uint32_t nxv = __builtin_amdgcn_readlane(nx[j], 0);
-      if (tail_tile) nxv = mask_past_end32(nxv, TILE + 4 * j, remu);
-      const uint32_t dn = dpp<DPP_WAVE_SHL1>(d[j]);
-      look[j] = lane == 63 ? nxv : dn;
-    }
-    uint32_t prevdw = dpp<DPP_WAVE_SHR1>(d[15]);
-    if (lane == 0) prevdw = prev_last;
-    prev_last = __builtin_amdgcn_readlane(d[15], 63);
-
-    // ---- filter, level 1: a node at m has p = le64(m+8..m+16) < file_len
-    //      < 2^40, so bytes m+13..m+15 are zero and contain an aligned zero
-    //      halfword inside [L+14, L+77] (m in [L, L+63]).  16-bit has-zero
-    //      test, 2 VALU per dword; the exact test (p >> 32 <= hb) runs per
-    //      position in the slow path. ----
-    auto wd_at = [&](int i) -> uint32_t { return i < 16 ? d[i] : look[i - 16]; };
+    // ---- filter, level 1: any aligned zero halfword in the lane's line
+    //      (16-bit has-zero, 2 VALU per dword); level 2 (exact, per
+    //      position) in the slow path: p >> 32 <= hb = (file_len-1) >> 32 ----
     uint32_t acc = 0;
 #pragma unroll
-    for (int i = 3; i < 20; i++) {  // dword 3: high half (14,15) only; dword 19: low half (76,77) only
-      const uint32_t w = i == 3 ? (wd_at(i) | 0x0000FFFFu) : i == 19 ? (wd_at(i) | 0xFFFF0000u) : wd_at(i);
-      acc |= (w + 0xFFFEFFFFu) & ~w;  // one v_add + one v_bitop3
-    }
-    acc &= 0x80008000u;
-    uint64_t slow = __ballot(acc != 0);
+    for (int i = 0; i < 16; i++) acc |= (d[i] + 0xFFFEFFFFu) & ~d[i];
+    uint64_t slow = __ballot((acc & 0x80008000u) != 0);
     if (a.ablate & 2) slow = 0;
 
     while (slow) {
       const int f = __builtin_ctzll(slow);
       slow &= slow - 1;
+      // stage [L-16, L+72): lane f-1 (or the saved tail for f == 0), f, f+1
+      // (or the prefetched next tile's lane 0 for f == 63)
+      if (f > 0 && lane == f - 1) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) win[j] = d[12 + j];
+      }
       if (lane == f) {
-        win[3] = prevdw;
 #pragma unroll
         for (int j = 0; j < 16; j++) win[4 + j] = d[j];
-#pragma unroll
-        for (int j = 0; j < 5; j++) win[20 + j] = look[j];
+      }
+      if (f < 63 ? lane == f + 1 : lane == 0) {
+        uint32_t n0 = f < 63 ? d[0] : nx[0], n1 = f < 63 ? d[1] : nx[1];
+        if (f == 63 && tail_tile) {
+          n0 = mask_past_end32(n0, TILE, remu);
+          n1 = mask_past_end32(n1, TILE + 4, remu);
+        }
+        win[20] = n0;
+        win[21] = n1;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const uint32_t b = lane;
-      const uint32_t r = 64u * f + b;  // m - B
-      const int base = 4 + (b >> 2);
-      const uint32_t sh = (b & 3) * 8;
+      const int r = 64 * f + (int)b - 14;  // m - B, in [-14, 4081]
+      const uint32_t o = b + 2;            // m's byte offset in the window
+      const int base = (int)(o >> 2);
+      const uint32_t sh = (o & 3) * 8;
       uint32_t W[6];
 #pragma unroll
       for (int i = 0; i < 6; i++) W[i] = win[base + i];
-      const uint32_t tdw = win[(15 + b) >> 2];
+      const uint32_t tdw = win[(o - 1) >> 2];
+      const uint32_t hxp = win[22];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // level 2, exact: p >> 32 <= (file_len-1) >> 32 (roots: p == 0 pass too)
       const uint32_t f3 = alignb(W[4], W[3], sh);
-      if (!__ballot(f3 <= hb)) continue;
-      const uint32_t tbyte = (tdw >> (((15 + b) & 3) * 8)) & 0xffu;
+      if (!__ballot(f3 <= hb) || (a.ablate & 4)) continue;
+      const uint32_t tbyte = (tdw >> (((o - 1) & 3) * 8)) & 0xffu;
       const uint32_t f0 = alignb(W[1], W[0], sh), f1 = alignb(W[2], W[1], sh);
       const uint32_t f2 = alignb(W[3], W[2], sh);
       const uint32_t f4 = alignb(W[5], W[4], sh);
       // recover_valid_chain's node test (data_store.rs:404-470) at m = B + r
-      const bool inrange = (r + 20 <= remu) && (B != 0 || r != 0);
+      const uint32_t u = (uint32_t)(r + 20);  // t - B >= 6
+      const bool inrange = (u <= remu) && (B != 0 || r >= 1);
       const uint64_t roots = __ballot(inrange && (f2 | f3) == 0);
-      if (roots) rootmax = B + 64u * f + (63 - __builtin_clzll(roots)) + 20;  // increasing in (k, f)
-      const uint64_t m = B + r;
+      if (roots) rootmax = B + (uint64_t)(64 * f - 14 + 20) + (63 - __builtin_clzll(roots));  // increasing in (k, f)
+      const uint64_t m = B + (int64_t)r;
       const uint64_t p = (uint64_t)f2 | ((uint64_t)f3 << 32);
       const uint64_t dp = m - p;
       const bool tomb = dp == 1 && tbyte == 0;
@@ -392,18 +423,20 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const bool isnode = inrange && p >= 20 && p < m && (tomb || dp > pp);
       const bool strong = isnode && (FULL || f4 != 0);
       weak += (uint32_t)__popcll(__ballot(isnode && !strong));
-      const uint32_t t = r + 20;
-      const uint32_t js = (t + ((0u - t) & 63u)) >> 6;  // line of the next entry's start
-      const uint32_t hs = __shfl(hx, (int)(js & 63));
-      const uint32_t hm = __builtin_amdgcn_readlane(hx, f);
       const uint64_t cm = __ballot(strong);
+      if (!cm) continue;
+      const uint32_t js = (u + ((0u - u) & 63u)) >> 6;  // line of the next entry's start
+      const uint32_t hs = __shfl(hx, (int)(js & 63));
+      const int lm = r >> 6;                             // m's line (-1: previous tile's line 63)
+      const uint32_t hm0 = __shfl(hx, lm & 63);
+      const uint32_t hm = lm < 0 ? hxp : hm0;
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
         if (idx < a.cap) {
           const uint64_t gi = span * a.cap + idx;
           const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
-          const uint32_t fl = (tomb ? F_TOMB : 0u) | (b == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT) |
-                              (f < 32 ? F_SXM_LO : 0u) | ((js & 63) < 32 ? F_SUF_LO : 0u);
+          const uint32_t fl = (tomb ? F_TOMB : 0u) | ((r & 63) == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT) |
+                              (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) | ((js & 63) < 32 ? F_SUF_LO : 0u);
           a.c_m[gi] = m;
           a.c_rec[2 * gi] = u32x4{f2, f3, f0, f1};
           a.c_rec[2 * gi + 1] = u32x4{f4, hm, hs, fl};
@@ -413,41 +446,34 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       }
       count += __popcll(cm);
     }
+    // carry the last line's tail and SX_63 into the next tile's window
+    if (lane == 63) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) win[j] = d[12 + j];
+      win[22] = hx;
+    }
     if ((k + 1) % SPAN_TILES == 0 || k + 1 == k1) {
       if (lane == 0) a.span_count[span] = count;
       count = 0;
     }
   };
 
-#if SRD_RING == 3
   // 3-buffer register ring: two tiles in flight while one is processed.
-  // Tile k1 (first tile of the next wave's range, inside the padding at the
-  // end) is loaded too: its lane 0 supplies the last tile's lookahead.
+  // Loads are clamped, never skipped (tiles up to n_tiles+1 are readable).
+  const uint32_t nk = (uint32_t)(k1 - k0);
   uint32_t A[16], Bv[16], Cv[16];
   load_tile(k0, A);
   load_tile(k0 + 1, Bv);
-  for (uint64_t k = k0; k < k1; k += 3) {
-    if (k + 2 <= k1) load_tile(k + 2, Cv);
-    process(k, A, Bv);
-    if (k + 1 >= k1) break;
-    if (k + 3 <= k1) load_tile(k + 3, A);
-    process(k + 1, Bv, Cv);
-    if (k + 2 >= k1) break;
-    if (k + 4 <= k1) load_tile(k + 4, Bv);
-    process(k + 2, Cv, A);
+  for (uint32_t j = 0; j < nk; j += 3) {
+    load_tile(k0 + min(j + 2, nk), Cv);
+    process(k0 + j, A, Bv);
+    if (j + 1 >= nk) break;
+    load_tile(k0 + min(j + 3, nk), A);
+    process(k0 + j + 1, Bv, Cv);
+    if (j + 2 >= nk) break;
+    load_tile(k0 + min(j + 4, nk), Bv);
+    process(k0 + j + 2, Cv, A);
   }
-#else
-  // 2-buffer ring: tile k+1 in flight while k is processed
-  uint32_t A[16], Bv[16];
-  load_tile(k0, A);
-  for (uint64_t k = k0; k < k1; k += 2) {
-    load_tile(k + 1, Bv);
-    process(k, A, Bv);
-    if (k + 1 >= k1) break;
-    load_tile(k + 2, A);
-    process(k + 1, Bv, A);
-  }
-#endif
 
   // rootmax / weak are wave-uniform already
   if (lane == 0) {
@@ -481,7 +507,7 @@ __global__ __launch_bounds__(64) void link_kernel(LinkArgs a) {
     const u32x4 r0 = a.c_rec[2 * gi];
     const uint64_t m = a.c_m[gi], p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     const uint64_t mp = p - 20;  // p >= 20 by construction
-    const uint64_t sp2 = mp / SPAN_BYTES;
+    const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // span s holds m in [16 KiB s - 14, 16 KiB (s+1) - 14)
     int64_t par = PAR_MISS;
     if (sp2 < a.n_spans) {
       uint32_t lo = 0, hi = min(a.span_count[sp2], a.cap);

@@ -9,7 +9,7 @@ t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
 S.synth_store_device(t.data_ptr(), n, 4096, ctx=ctx)
 torch.cuda.synchronize()
 res = {}
-for ab in [0, 1, 2, 3]:
+for ab in [int(x) for x in os.environ.get('ABL', '0,1,2,3,4').split(',')]:
     os.environ["SRD_SCAN_ABLATE"] = str(ab)
     ts = []
     for i in range(8):
