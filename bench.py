@@ -9,9 +9,14 @@ payload + compare (is_valid_checksum), and the latest-wins index rebuild
 (KeyIndexer::build).  value = algorithmic bytes sum(payload_len + 20) over all
 ranks / max-over-ranks wall time of K steps.
 
-N>1 (torchrun): each rank validates its own store of --entries-per-gpu entries
-on its GPU (weak scaling, no data-path collective); only the step timing is
-reduced (MAX) over ranks.
+N>1 (torchrun, one process per GPU): ONE global store of N x --entries-per-gpu
+entries, sharded by entry range (SURVEY.md 8(e), config C4 at N=8 with 2^21
+entries per GPU): rank r holds entries [r*n, (r+1)*n) in its HBM and a step
+is srd_shard.sharded_validate_index -- its shard's validate+index
+(srd_validate_span_device), the boundary composition check (all_gather) and
+the owner-partitioned index exchange (all_to_all over RCCL, 16 B per key) +
+owner-side KeyIndexer build.  Weak scaling; the step time is the MAX over
+ranks.
 
 Also prints: roofline of the dominant kernel (scan_kernel, HIP events on the
 library's stream) and a CPU baseline (oracle/, the C restatement of the
@@ -87,26 +92,47 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if os.environ.get("SRD_BENCH_SAME_DEVICE"):  # rehearsal of N>1 on a 1-GPU box (gloo, all ranks on cuda:0)
+        local = 0
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(os.environ.get("SRD_DIST_BACKEND", "nccl"), init_method="env://")
     torch.cuda.set_device(local)
     ctx = S.Context(local)
 
     n, L = args.entries_per_gpu, args.payload
-    size = S.synth_store_len(n, L)
-    store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
-    S.synth_store_device(store.data_ptr(), n, L, ctx=ctx)
+    if world == 1:
+        size = S.synth_store_len(n, L)
+        store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
+        S.synth_store_device(store.data_ptr(), n, L, ctx=ctx)
+        span = (0, 0, size)
+
+        def step():
+            r = S.validate_index_device(store.data_ptr(), size, 0, ctx)
+            return r.final_len, r.n_chain, r.n_crc_bad, r.n_index
+        expect = (size, n, 0, n)
+    else:
+        import srd_shard as SH
+        first, cnt = SH.plan_entry_shards(n * world, world)[rank]
+        lo, hi = S.synth_span(None, 0, first, cnt, L)
+        file_len = S.synth_store_len(n * world, L)
+        span_off = lo - lo % S.SPAN_ALIGN
+        size = hi - span_off
+        store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
+        S.synth_span(store.data_ptr(), span_off, first, cnt, L, ctx=ctx)
+        span = (span_off, lo, hi)
+        backend = SH.HipBackend(ctx, local)
+
+        def step():
+            r = SH.sharded_validate_index(backend, store, span_off, lo, hi, file_len)
+            return r.final_len, r.n_chain, r.n_crc_bad, r.n_index
+        expect = (file_len, n * world, 0, n * world)
     torch.cuda.synchronize()
     bytes_alg = algorithmic_bytes(n, L)
 
-    def step():
-        return S.validate_index_device(store.data_ptr(), size, 0, ctx)
-
     for _ in range(args.warmup):
-        r = step()
-    assert r.final_len == size and r.n_chain == n and r.n_crc_bad == 0 and r.n_index == n, (
-        r.final_len, r.n_chain, r.n_crc_bad, r.n_index)
+        got = step()
+    assert got == expect, (got, expect)
 
     if dist:
         dist.barrier()
@@ -123,7 +149,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], device=f"cuda:{local}")
+        t = torch.tensor([dt], device="cpu" if dist.get_backend() == "gloo" else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -133,7 +159,7 @@ def main():
     achieved = bytes_alg / (scan_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tf):
+    if os.path.exists(tf) and world == 1 and n == 1 << 20 and L == 4096:  # measured on the C2 workload only
         try:
             traffic = json.load(open(tf)).get("scan_kernel_hbm_bytes_per_launch")
         except Exception:
@@ -153,13 +179,17 @@ def main():
         "dtype": "u8",
         "data": "synthetic (counter-mode splitmix64 payloads, keys bench-key-{i}), generated in HBM",
         "config": {
-            "workload": f"C2: {n} x {L} B entries, {size} B store per GPU, validate+index "
-                        f"(recover_valid_chain + CRC-32 every payload + KeyIndexer::build)",
+            "workload": (f"C2: {n} x {L} B entries, {size} B store, validate+index "
+                         f"(recover_valid_chain + CRC-32 every payload + KeyIndexer::build)") if world == 1 else
+                        (f"{n * world} x {L} B entries, one store sharded by entry range over {world} GPUs "
+                         f"({n} entries per GPU), validate+index + index exchange"),
             "entries_per_gpu": n,
             "payload_bytes": L,
-            "store_bytes_per_gpu": size,
+            "store_bytes_per_gpu": span[2] - span[1],
             "algorithmic_bytes_per_gpu": bytes_alg,
-            "parallelism": f"{world} independent GPU stores (entry-range shards), no collective",
+            "parallelism": "1 GPU" if world == 1 else
+                           f"{world} entry-range shards, one per GPU; all_gather (boundaries) + "
+                           f"all_to_all (index owners) over RCCL",
         },
         "roofline": {
             "bound": "hbm",

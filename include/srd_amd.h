@@ -53,6 +53,11 @@ extern "C" {
 #define SRD_ERR_ARG (-3)
 #define SRD_ERR_INTERNAL (-4)
 
+/* srd_device_result.mode */
+#define SRD_MODE_OPTIMISTIC 0      /* the chain from file_len was proven through recorded nodes */
+#define SRD_MODE_FULL 1            /* full pass (torn tail / corrupt store / unusual structure) */
+#define SRD_MODE_SPAN_UNPROVEN 3   /* span mode: the shard's chain was not proven; use the whole-file path */
+
 /* option flags */
 #define SRD_FLAG_FORCE_FULL 1u   /* skip the optimistic (strong-candidate) pass */
 #define SRD_FLAG_NO_CRC 2u       /* structural recovery + index only */
@@ -103,6 +108,43 @@ int srd_validate_index_device(srd_ctx *ctx, const uint8_t *d_file,
                               uint64_t file_len, uint32_t flags,
                               srd_device_result *out);
 
+/* Entry-range shard of a store (multi-GPU, one process per GPU; no
+ * collective inside).  `d_span` holds file bytes [span_off, hi) -- span_off a
+ * multiple of 16 KiB and <= lo, readable to srd_padded_size(hi - span_off) --
+ * where lo and hi are entry tails: lo = the previous shard's last tail, hi =
+ * this shard's last tail (hi = file_len for the last shard).  Proves that the
+ * backward chain from hi reaches an entry whose prev_offset == lo and returns
+ * that chain segment (file order, absolute offsets), every payload's CRC and
+ * the shard-local latest-wins index.  final_len = hi when proven; otherwise
+ * mode = SRD_MODE_SPAN_UNPROVEN, final_len = 0 and the caller falls back to
+ * the whole-file path (a torn tail, for example, can only be recovered there,
+ * recover_valid_chain's byte-wise outer loop is global).  The shards' chains
+ * compose to the whole file's chain when shard 0 has lo = 0 (whole-file rule)
+ * and each shard's lo equals the previous shard's hi.  lo == 0 with
+ * span_off == 0 is exactly srd_validate_index_device. */
+int srd_validate_span_device(srd_ctx *ctx, const uint8_t *d_span,
+                             uint64_t span_off, uint64_t lo, uint64_t hi,
+                             uint32_t flags, srd_device_result *out);
+
+/* Index exchange between shards (KeyIndexer semantics, key_indexer.rs:98-124).
+ * Partition n (key_hash, value) pairs (device arrays) by owner rank
+ * owner = ((key_hash >> 32) * world) >> 32 into d_out_pairs ([2n] u64,
+ * interleaved key,value; grouped by owner, input order kept inside a group);
+ * counts[world] (host) receives the group sizes.  Synchronises. */
+int srd_index_partition_device(srd_ctx *ctx, const uint64_t *d_keys,
+                               const uint64_t *d_vals, uint64_t n,
+                               uint32_t world, uint64_t *d_out_pairs,
+                               uint64_t *counts);
+
+/* KeyIndexer::build over n interleaved (key_hash, meta_off or packed) device
+ * pairs in file order (the latest position of a key wins; tombstones are
+ * entries like any other).  Writes the index (key_hash, pack(tag16,
+ * offset48)) in file order of each key's latest entry to the caller's device
+ * arrays (capacity n each); *n_index = its size.  Synchronises. */
+int srd_index_build_device(srd_ctx *ctx, const uint64_t *d_pairs, uint64_t n,
+                           uint64_t *d_out_keys, uint64_t *d_out_packed,
+                           uint64_t *n_index);
+
 /* Same result with host-memory arrays (malloc'd; free with srd_result_free).
  * `file` is host memory (e.g. the mmap); it is staged to HBM inside. */
 typedef srd_device_result srd_result;
@@ -144,6 +186,16 @@ int srd_xxh3_64_batch_device(srd_ctx *ctx, const uint8_t *d_keys,
 int srd_synth_store_device(srd_ctx *ctx, uint8_t *d_out, uint64_t n_entries,
                            uint64_t fixed_len, const uint64_t *lens,
                            uint64_t seed, uint64_t *len_out);
+
+/* The shard [lo, hi) of that synthetic store holding entries
+ * [first, first + n) (lens, if given, holds the lengths of entries
+ * 0 .. first + n - 1), written into d_span = file bytes [span_off, hi)
+ * (span_off a multiple of 16 KiB, <= lo; bytes of earlier entries at or past
+ * span_off are written too).  d_span == NULL only computes lo / hi. */
+int srd_synth_span_device(srd_ctx *ctx, uint8_t *d_span, uint64_t span_off,
+                          uint64_t first, uint64_t n, uint64_t fixed_len,
+                          const uint64_t *lens, uint64_t seed,
+                          uint64_t *lo_out, uint64_t *hi_out);
 
 /* Library self-test of the CRC algebra tables (host only, no GPU). */
 int srd_selftest_host(void);

@@ -73,6 +73,7 @@ enum BufId {
   B_HKEYS, B_HVALS, B_LATEST, B_IPOS, B_IKEY, B_IPACKED,
   B_CUB_TMP,
   B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
+  B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF,
   B_COUNT_
 };
 
@@ -312,10 +313,14 @@ static int alloc_hash(Ctx* c, uint64_t n) {
   return 0;
 }
 
-// KeyIndexer::build over the n chain entries in B_O_KH / B_O_MO with one
-// global open-addressing table (device-wide atomics); syncs for the count
-static int index_global(Ctx* c, uint64_t n, uint64_t* n_index) {
+// KeyIndexer::build over n (key_hash, meta_off) pairs in file order with one
+// global open-addressing table (device-wide atomics); syncs for the count.
+// Default pairs: the chain in B_O_KH / B_O_MO -> B_IKEY / B_IPACKED.
+static int index_global(Ctx* c, uint64_t n, uint64_t* n_index, const uint64_t* kh = nullptr,
+                        const uint64_t* mo = nullptr, uint64_t* okey = nullptr, uint64_t* opacked = nullptr) {
+  if (!kh) { kh = P<uint64_t>(c, B_O_KH); mo = P<uint64_t>(c, B_O_MO); }
   TRY(alloc_hash(c, n));
+  if (!okey) { okey = P<uint64_t>(c, B_IKEY); opacked = P<uint64_t>(c, B_IPACKED); }
   uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
   uint64_t hc = 64;
   while (hc < 2 * n) hc <<= 1;
@@ -325,20 +330,18 @@ static int index_global(Ctx* c, uint64_t n, uint64_t* n_index) {
   HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_LATEST) + n, 0, 4, c->stream));
   if (n) {
     index_insert_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
-        P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_HKEYS),
-        P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7));
+        kh, mo, n, P<uint64_t>(c, B_HKEYS), P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7));
     index_latest_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
-        P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_HKEYS),
-        P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7), P<uint32_t>(c, B_LATEST));
+        kh, mo, n, P<uint64_t>(c, B_HKEYS), P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7),
+        P<uint32_t>(c, B_LATEST));
     HIPCHK(hipGetLastError());
   }
   size_t tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_LATEST),
                                           P<uint32_t>(c, B_IPOS), (int)(n + 1), c->stream));
   if (n) {
-    index_emit_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO),
-                                                             P<uint32_t>(c, B_LATEST), P<uint32_t>(c, B_IPOS), n,
-                                                             P<uint64_t>(c, B_IKEY), P<uint64_t>(c, B_IPACKED));
+    index_emit_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(kh, mo, P<uint32_t>(c, B_LATEST), P<uint32_t>(c, B_IPOS),
+                                                             n, okey, opacked);
     HIPCHK(hipGetLastError());
   }
   uint32_t nidx = 0;
@@ -379,6 +382,7 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
   f.c_rec = P<u32x4>(c, B_CREC);
   f.tile = P<uint32_t>(c, B_TILE);
   f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
+  f.coff = 1;
   f.o_mo = P<uint64_t>(c, B_O_MO);
   f.o_kh = P<uint64_t>(c, B_O_KH);
   f.o_prev = P<uint64_t>(c, B_O_PREV);
@@ -503,6 +507,60 @@ static int set_single_root(Ctx* c, uint64_t t) {
 }
 
 
+// KeyIndexer::build (key_indexer.rs:98-124) as a bucketed build over the
+// pairs (kh[i], mo[i]), i < *n_dev, in file order (latest = last position);
+// *status != 0 disables it.  Scratch: B_HIST/B_HOFF/B_SKEY/B_SIDX/B_LATEST8,
+// B_PART/B_PARTEX (alloc_index).  pl->n_index / pl->idx_overflow are written.
+static int alloc_index(Ctx* c, uint64_t n_cap, uint32_t log2_nbk) {
+  const uint64_t nh = ((uint64_t)1 << log2_nbk) * IDX_HBLOCKS + 1;
+  TRY(ensure(c, B_HIST, nh * 4));
+  TRY(ensure(c, B_HOFF, nh * 4));
+  TRY(ensure(c, B_SKEY, (n_cap + 1) * 8));
+  TRY(ensure(c, B_SIDX, (n_cap + 1) * 4));
+  TRY(ensure(c, B_LATEST8, n_cap + 1));
+  TRY(ensure(c, B_PART, GLUE_BLOCKS * 4));
+  TRY(ensure(c, B_PARTEX, GLUE_BLOCKS * 4));
+  TRY(ensure_cub(c, nh));
+  return 0;
+}
+static uint32_t index_log2_buckets(uint64_t n_est) {
+  uint32_t log2_nbk = 1;  // >= 1: the bucket is the hash's top log2_nbk bits
+  while (log2_nbk < 14 && ((uint64_t)IDX_BUCKET_AVG << log2_nbk) < n_est) log2_nbk++;
+  return log2_nbk;
+}
+static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
+                                 const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
+                                 Plan* pl) {
+  IdxArgs ia{};
+  ia.kh = kh;
+  ia.mo = mo;
+  ia.n_dev = n_dev;
+  ia.status = status;
+  ia.log2_nbk = log2_nbk;
+  ia.histT = P<uint32_t>(c, B_HIST);
+  ia.hoff = P<uint32_t>(c, B_HOFF);
+  ia.skey = P<uint64_t>(c, B_SKEY);
+  ia.sidx = P<uint32_t>(c, B_SIDX);
+  ia.latest = P<uint8_t>(c, B_LATEST8);
+  ia.part = P<uint32_t>(c, B_PART);
+  ia.part_ex = P<uint32_t>(c, B_PARTEX);
+  ia.okey = okey;
+  ia.opacked = opacked;
+  ia.plan = pl;
+  const uint32_t nbk = 1u << log2_nbk;
+  const int nh = (int)((uint64_t)nbk * IDX_HBLOCKS + 1);
+  idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+  size_t tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, ia.histT, ia.hoff, nh, c->stream));
+  idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+  idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
+  idx_count_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
+  idx_scan_kernel<<<1, 1024, 0, c->stream>>>(ia);
+  idx_emit_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // Optimistic pass, sync-free: scan (strong candidates only) -> link -> shape
 // check -> chain scatter -> finalize -> bucketed index, all counts on the
@@ -520,31 +578,31 @@ static int alloc_fast(Ctx* c, uint64_t capK, uint32_t log2_nbk) {
   TRY(ensure(c, B_PARTEX, GLUE_BLOCKS * 4));
   TRY(ensure(c, B_PLAN, sizeof(Plan)));
   TRY(alloc_out(c, capK + 1));
-  const uint64_t nh = ((uint64_t)1 << log2_nbk) * IDX_HBLOCKS + 1;
-  TRY(ensure(c, B_HIST, nh * 4));
-  TRY(ensure(c, B_HOFF, nh * 4));
-  TRY(ensure(c, B_SKEY, (capK + 1) * 8));
-  TRY(ensure(c, B_SIDX, (capK + 1) * 4));
-  TRY(ensure(c, B_LATEST8, capK + 1));
-  TRY(ensure_cub(c, nh));
+  TRY(alloc_index(c, capK, log2_nbk));
   return 0;
 }
 
-static int optimistic_pass(Ctx* c, const uint8_t* d_file, uint64_t flen, uint32_t flags, srd_device_result* out,
-                           bool* done) {
+// Span mode (lo > 0): d_span holds file bytes [span_off, flen) (span_off a
+// multiple of SPAN_BYTES, <= lo); the chain must run from flen down to an
+// entry whose prev == lo.  Whole file: span_off = lo = 0.
+static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uint64_t lo, uint64_t flen,
+                           uint32_t flags, srd_device_result* out, bool* done) {
   *done = false;
+  const uint8_t* d_file = d_span - span_off;  // absolute file offsets index d_file (only [span_off, ..) is read)
   const uint64_t n_tiles = (flen + TILE - 1) / TILE;
   const uint64_t n_spans = (n_tiles + SPAN_TILES - 1) / SPAN_TILES;
+  const uint64_t k_lo = span_off / TILE, s_lo = k_lo / SPAN_TILES;
+  const uint64_t nt_rel = n_tiles - k_lo, ns_rel = n_spans - s_lo;
+  const uint32_t coff = lo ? 0u : 1u;
   for (int attempt = 0; attempt < 6; attempt++) {
-    if (!c->capK) c->capK = flen / 1024 + 4096;
+    if (!c->capK) c->capK = (flen - span_off) / 1024 + 4096;
     const uint64_t capK = c->capK;
     if (capK >= (1ull << 32) - 2) { set_err("too many chain candidates"); return SRD_ERR_INTERNAL; }
     // index buckets: ~IDX_BUCKET_AVG chain entries per bucket
     const uint64_t n_est = std::max<uint64_t>(c->last_n ? c->last_n : capK / 4, 1);
-    uint32_t log2_nbk = 1;  // >= 1: the bucket is the hash's top log2_nbk bits
-    while (log2_nbk < 14 && ((uint64_t)IDX_BUCKET_AVG << log2_nbk) < n_est) log2_nbk++;
-    TRY(alloc_scan(c, n_tiles, n_spans));
-    TRY(ensure_cub(c, n_spans + 1));
+    const uint32_t log2_nbk = index_log2_buckets(n_est);
+    TRY(alloc_scan(c, nt_rel, ns_rel));
+    TRY(ensure_cub(c, ns_rel + 1));
     TRY(alloc_fast(c, capK, log2_nbk));
     if (++c->gen == 0) {  // tag wrap: clear the marks once
       c->gen = 1;
@@ -556,31 +614,35 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_file, uint64_t flen, uint32_
     HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
     HIPCHK(hipMemsetAsync(cnt, 0, 64, c->stream));
     // the scan writes every span's count; only the scan sentinel needs a zero
-    HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT) + n_spans, 0, 4, c->stream));
+    HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT) + ns_rel, 0, 4, c->stream));
+    // per-tile / per-span arrays hold the resident range only: their base
+    // pointers are shifted so kernels index them by absolute tile / span
     ScanArgs a{};
     a.file = d_file;
     a.flen = flen;
     a.n_tiles = n_tiles;
     a.n_spans = n_spans;
     a.cap = c->cap;
-    a.tile = P<uint32_t>(c, B_TILE);
-    a.span_count = P<uint32_t>(c, B_SPAN_COUNT);
-    a.c_m = P<uint64_t>(c, B_CM);
-    a.c_rec = P<u32x4>(c, B_CREC);
+    a.tile = P<uint32_t>(c, B_TILE) - 4 * k_lo;
+    a.span_count = P<uint32_t>(c, B_SPAN_COUNT) - s_lo;
+    a.c_m = P<uint64_t>(c, B_CM) - s_lo * c->cap;
+    a.c_rec = P<u32x4>(c, B_CREC) - 2 * s_lo * c->cap;
     a.counters = (unsigned long long*)cnt;
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
+    a.k_lo = k_lo;
+    a.m_lo = lo;
     {
       const char* ab = getenv("SRD_SCAN_ABLATE");
       a.ablate = ab ? (uint32_t)atoi(ab) : 0u;
     }
-    const unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
+    const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     scan_kernel<false><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     size_t tb = c->bufs[B_CUB_TMP].n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_SPAN_COUNT),
-                                            P<uint64_t>(c, B_SPAN_BASE), (int)(n_spans + 1), c->stream));
+                                            P<uint64_t>(c, B_SPAN_BASE), (int)(ns_rel + 1), c->stream));
     Link2Args l{};
     l.file = d_file;
     l.flen = flen;
@@ -588,21 +650,24 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_file, uint64_t flen, uint32_
     l.capK = capK;
     l.cap = c->cap;
     l.gen = c->gen;
-    l.span_count = P<uint32_t>(c, B_SPAN_COUNT);
-    l.span_base = P<uint64_t>(c, B_SPAN_BASE);
-    l.c_m = P<uint64_t>(c, B_CM);
-    l.c_rec = P<u32x4>(c, B_CREC);
+    l.span_count = a.span_count;
+    l.span_base = P<uint64_t>(c, B_SPAN_BASE) - s_lo;
+    l.c_m = a.c_m;
+    l.c_rec = a.c_rec;
     l.d_m = P<uint64_t>(c, B_DM);
     l.d_par = P<int64_t>(c, B_DPAR);
     l.d_slot = P<uint64_t>(c, B_DSLOT);
     l.has_child = P<uint32_t>(c, B_HASCHILD);
-    link2_kernel<<<blocks(n_spans, 64), 256, 0, c->stream>>>(l);
+    l.s_lo = s_lo;
+    l.span_lo = lo;
+    link2_kernel<<<blocks(ns_rel, 64), 256, 0, c->stream>>>(l);
     ShapeArgs sa{};
     sa.file = d_file;
     sa.flen = flen;
     sa.capK = capK;
     sa.gen = c->gen;
-    sa.Kp = P<uint64_t>(c, B_SPAN_BASE) + n_spans;
+    sa.Kp = P<uint64_t>(c, B_SPAN_BASE) + ns_rel;
+    sa.coff = coff;
     sa.d_m = l.d_m;
     sa.d_par = l.d_par;
     sa.d_slot = l.d_slot;
@@ -636,6 +701,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_file, uint64_t flen, uint32_
     f.d_n_chain = &pl->n_chain;
     f.d_root_t = &pl->root_t;
     f.d_status = &pl->status;
+    f.coff = coff;
     f.o_mo = P<uint64_t>(c, B_O_MO);
     f.o_kh = P<uint64_t>(c, B_O_KH);
     f.o_prev = P<uint64_t>(c, B_O_PREV);
@@ -655,39 +721,15 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_file, uint64_t flen, uint32_
     if (!f.no_crc) slow_kernel<<<256, 64, 0, c->stream>>>(f);
     HIPCHK(hipGetLastError());
     // ---- KeyIndexer::build (bucketed) ----
-    IdxArgs ia{};
-    ia.kh = f.o_kh;
-    ia.mo = f.o_mo;
-    ia.n_dev = &pl->n_chain;
-    ia.status = &pl->status;
-    ia.log2_nbk = log2_nbk;
-    ia.histT = P<uint32_t>(c, B_HIST);
-    ia.hoff = P<uint32_t>(c, B_HOFF);
-    ia.skey = P<uint64_t>(c, B_SKEY);
-    ia.sidx = P<uint32_t>(c, B_SIDX);
-    ia.latest = P<uint8_t>(c, B_LATEST8);
-    ia.part = sa.part;
-    ia.part_ex = sa.part_ex;
-    ia.okey = P<uint64_t>(c, B_IKEY);
-    ia.opacked = P<uint64_t>(c, B_IPACKED);
-    ia.plan = pl;
-    const uint32_t nbk = 1u << log2_nbk;
-    const int nh = (int)((uint64_t)nbk * IDX_HBLOCKS + 1);
-    idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
-    tb = c->bufs[B_CUB_TMP].n;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, ia.histT, ia.hoff, nh, c->stream));
-    idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
-    idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
-    idx_count_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
-    idx_scan_kernel<<<1, 1024, 0, c->stream>>>(ia);
-    idx_emit_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
-    HIPCHK(hipGetLastError());
+    TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
+                              P<uint64_t>(c, B_IPACKED), pl));
     HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     const Plan hp = *c->h_plan;
     if (getenv("SRD_DEBUG")) {
+      const int nh = (int)(((uint64_t)1 << log2_nbk) * IDX_HBLOCKS + 1);
       std::vector<uint32_t> ho(std::min(nh, 300));
-      hipMemcpy(ho.data(), ia.hoff, ho.size() * 4, hipMemcpyDeviceToHost);
+      hipMemcpy(ho.data(), P<uint32_t>(c, B_HOFF), ho.size() * 4, hipMemcpyDeviceToHost);
       fprintf(stderr, "plan K=%lu n_chain=%lu root_t=%lu start=%lu n_index=%lu bad=%lu slow=%lu st=%u nroot=%u troot=%u idxov=%u log2nbk=%u capK=%lu\n",
               (unsigned long)hp.K, (unsigned long)hp.n_chain, (unsigned long)hp.root_t, (unsigned long)hp.start,
               (unsigned long)hp.n_index, (unsigned long)hp.n_bad, (unsigned long)hp.n_slow, hp.status, hp.nroot,
@@ -713,7 +755,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_file, uint64_t flen, uint32_
       c->capK = hp.cap_need + hp.cap_need / 4 + 4096;
       continue;
     }
-    if (hp.status) return 0;  // not provable here -> full pass
+    if (hp.status) return 0;  // not provable here -> full pass (whole file) / unproven (span)
     out->final_len = flen;
     out->n_chain = hp.n_chain;
     out->n_crc_bad = hp.n_bad;
@@ -746,6 +788,101 @@ extern "C" int srd_validate_index_device(srd_ctx* c, const uint8_t* d_file, uint
   return r;
 }
 
+extern "C" int srd_validate_span_device(srd_ctx* c, const uint8_t* d_span, uint64_t span_off, uint64_t lo,
+                                        uint64_t hi, uint32_t flags, srd_device_result* out) {
+  if (!c || !out || !d_span) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (lo == 0) {
+    if (span_off) { set_err("bad argument: a span starting at tail 0 is the whole file (span_off must be 0)"); return SRD_ERR_ARG; }
+    return srd_validate_index_device(c, d_span, hi, flags, out);
+  }
+  if (span_off % SPAN_BYTES || span_off > lo || hi < lo + 21 || hi >= (1ull << 40)) {
+    set_err("bad span: need span_off % 16384 == 0, span_off <= lo, lo + 21 <= hi < 2^40");
+    return SRD_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  c->scan_ms = 0;
+  c->scan_launches = 0;
+  memset(out, 0, sizeof *out);
+  out->file_len = hi;
+  HIPCHK(hipEventRecord(c->ev[2], c->stream));
+  bool done = false;
+  int r = optimistic_pass(c, d_span, span_off, lo, hi, flags, out, &done);
+  if (!r && !done) {
+    out->mode = SRD_MODE_SPAN_UNPROVEN;
+    out->final_len = 0;
+    out->n_chain = 0;
+    out->n_index = 0;
+    out->n_crc_bad = 0;
+  }
+  HIPCHK(hipEventRecord(c->ev[3], c->stream));
+  HIPCHK(hipEventSynchronize(c->ev[3]));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+  c->total_ms = ms;
+  return r;
+}
+
+extern "C" int srd_index_partition_device(srd_ctx* c, const uint64_t* d_keys, const uint64_t* d_vals, uint64_t n,
+                                          uint32_t world, uint64_t* d_out_pairs, uint64_t* counts) {
+  if (!c || !counts || world == 0 || world > PART_MAX_WORLD || (n && (!d_keys || !d_vals || !d_out_pairs))) {
+    set_err("bad argument");
+    return SRD_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const uint64_t nc = (uint64_t)world * GLUE_BLOCKS + 1;
+  TRY(ensure(c, B_PCNT, nc * 4));
+  TRY(ensure(c, B_POFF, nc * 4 + 8 * PART_MAX_WORLD));
+  TRY(ensure_cub(c, nc));
+  PartArgs a{};
+  a.keys = d_keys;
+  a.vals = d_vals;
+  a.n = n;
+  a.world = world;
+  a.cnt = P<uint32_t>(c, B_PCNT);
+  a.off = P<uint32_t>(c, B_POFF);
+  a.out = d_out_pairs;
+  a.counts = (uint64_t*)(P<uint32_t>(c, B_POFF) + ((nc + 1) & ~1ull));
+  part_count_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(a);
+  size_t tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, a.cnt, a.off, (int)nc, c->stream));
+  part_scatter_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(a);
+  part_counts_kernel<<<1, 64, 0, c->stream>>>(a);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(counts, a.counts, world * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+__global__ void set_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
+
+extern "C" int srd_index_build_device(srd_ctx* c, const uint64_t* d_pairs, uint64_t n, uint64_t* d_out_keys,
+                                      uint64_t* d_out_packed, uint64_t* n_index) {
+  if (!c || !n_index || (n && (!d_pairs || !d_out_keys || !d_out_packed))) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (n >= (1ull << 32) - 2) { set_err("too many pairs"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
+  *n_index = 0;
+  if (!n) return 0;
+  TRY(ensure(c, B_MKEY, n * 8));
+  TRY(ensure(c, B_MVAL, n * 8));
+  TRY(ensure(c, B_MPLAN, sizeof(Plan)));
+  const uint32_t log2_nbk = index_log2_buckets(n);
+  TRY(alloc_index(c, n, log2_nbk));
+  Plan* pl = P<Plan>(c, B_MPLAN);
+  HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
+  set_u64_kernel<<<1, 1, 0, c->stream>>>(&pl->n_chain, n);
+  deinterleave_kernel<<<blocks(std::min<uint64_t>(n, 1 << 20), 256), 256, 0, c->stream>>>(
+      d_pairs, n, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL));
+  HIPCHK(hipGetLastError());
+  TRY(launch_index_bucketed(c, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL), &pl->n_chain, &pl->status, log2_nbk,
+                            d_out_keys, d_out_packed, pl));
+  HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->h_plan->idx_overflow)
+    return index_global(c, n, n_index, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL), d_out_keys, d_out_packed);
+  *n_index = c->h_plan->n_index;
+  return 0;
+}
+
 extern "C" int srd_ctx_timings(srd_ctx* c, double* scan_ms, int* scan_launches, double* total_ms) {
   if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
   if (scan_ms) *scan_ms = c->scan_ms;
@@ -772,7 +909,7 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
   //      file_len is proven through recorded nodes ----
   if (!full) {
     bool done = false;
-    TRY(optimistic_pass(c, d_file, flen, flags, out, &done));
+    TRY(optimistic_pass(c, d_file, 0, 0, flen, flags, out, &done));
     if (done) return 0;
   }
   // ---- full pass ----
@@ -996,34 +1133,72 @@ extern "C" int srd_xxh3_64_batch(srd_ctx* c, const uint8_t* keys, uint64_t klen,
   });
 }
 
-extern "C" int srd_synth_store_device(srd_ctx* c, uint8_t* d_out, uint64_t n, uint64_t fixed_len,
-                                      const uint64_t* lens, uint64_t seed, uint64_t* len_out) {
-  if (!len_out) { set_err("bad argument"); return SRD_ERR_ARG; }
-  std::vector<uint64_t> off(n);
+// entry tails: lens (if given) holds the lengths of entries 0 .. first+n-1
+static int synth_offsets(uint64_t first, uint64_t n, uint64_t fixed_len, const uint64_t* lens, uint64_t span_off,
+                         std::vector<uint64_t>* off, uint64_t* e0, uint64_t* lo, uint64_t* hi) {
   uint64_t tail = 0;
-  for (uint64_t i = 0; i < n; i++) {
-    uint64_t L = lens ? lens[i] : fixed_len;
+  *lo = 0;
+  *e0 = first;
+  bool have_e0 = false;
+  if (off) off->clear();
+  for (uint64_t i = 0; i < first + n; i++) {
+    const uint64_t L = lens ? lens[i] : fixed_len;
     if (L == 0) { set_err("empty payload"); return SRD_ERR_ARG; }
-    off[i] = tail;
-    tail += ((64 - tail % 64) & 63) + L + 20;
+    if (i == first) *lo = tail;
+    const uint64_t end = tail + ((64 - tail % 64) & 63) + L + 20;
+    if (!have_e0 && (end > span_off || i == first)) { *e0 = i; have_e0 = true; }
+    if (have_e0 && off) off->push_back(tail);
+    tail = end;
   }
-  *len_out = tail;
-  if (!d_out || !n) return 0;
+  *hi = tail;
+  return 0;
+}
+
+static int synth_launch(Ctx* c, uint8_t* d_abs, const std::vector<uint64_t>& off, uint64_t e0, uint64_t fixed_len,
+                        const uint64_t* lens, uint64_t seed, uint64_t clip_lo) {
+  const uint64_t n = off.size();
+  if (!n) return 0;
   HIPCHK(hipSetDevice(c->device));
   void *doff = nullptr, *dl = nullptr;
   HIPCHK(hipMalloc(&doff, n * 8));
   HIPCHK(hipMemcpyAsync(doff, off.data(), n * 8, hipMemcpyHostToDevice, c->stream));
   if (lens) {
     HIPCHK(hipMalloc(&dl, n * 8));
-    HIPCHK(hipMemcpyAsync(dl, lens, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(dl, lens + e0, n * 8, hipMemcpyHostToDevice, c->stream));
   }
   synth_kernel<<<(unsigned)std::min<uint64_t>(n, 65536), 64, 0, c->stream>>>(
-      d_out, (const uint64_t*)doff, (const uint64_t*)dl, fixed_len, n, seed);
+      d_abs, (const uint64_t*)doff, (const uint64_t*)dl, fixed_len, n, seed, e0, clip_lo);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   hipFree(doff);
   if (dl) hipFree(dl);
   return 0;
+}
+
+extern "C" int srd_synth_store_device(srd_ctx* c, uint8_t* d_out, uint64_t n, uint64_t fixed_len,
+                                      const uint64_t* lens, uint64_t seed, uint64_t* len_out) {
+  if (!len_out) { set_err("bad argument"); return SRD_ERR_ARG; }
+  std::vector<uint64_t> off;
+  uint64_t e0, lo, hi;
+  TRY(synth_offsets(0, n, fixed_len, lens, 0, d_out ? &off : nullptr, &e0, &lo, &hi));
+  *len_out = hi;
+  if (!d_out || !n) return 0;
+  if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  return synth_launch(c, d_out, off, 0, fixed_len, lens, seed, 0);
+}
+
+extern "C" int srd_synth_span_device(srd_ctx* c, uint8_t* d_span, uint64_t span_off, uint64_t first,
+                                     uint64_t n, uint64_t fixed_len, const uint64_t* lens, uint64_t seed,
+                                     uint64_t* lo_out, uint64_t* hi_out) {
+  if (!lo_out || !hi_out || (span_off % SPAN_BYTES)) { set_err("bad argument"); return SRD_ERR_ARG; }
+  std::vector<uint64_t> off;
+  uint64_t e0, lo, hi;
+  TRY(synth_offsets(first, n, fixed_len, lens, span_off, d_span ? &off : nullptr, &e0, &lo, &hi));
+  *lo_out = lo;
+  *hi_out = hi;
+  if (!d_span || !n) return 0;
+  if (!c || span_off > lo) { set_err("bad argument: span_off must be <= the shard's lower tail"); return SRD_ERR_ARG; }
+  return synth_launch(c, d_span - span_off, off, e0, fixed_len, lens, seed, span_off);
 }
 
 // host self-test of the CRC algebra (no GPU): checks the tables against a

@@ -121,10 +121,12 @@ struct Link2Args {
   int64_t* d_par;
   uint64_t* d_slot;
   uint32_t* has_child;
+  uint64_t s_lo;     // first resident span (span mode)
+  uint64_t span_lo;  // span mode: the shard's lower tail (a node with p == span_lo is the shard's first entry); 0 = whole file
 };
 
 __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
-  const uint64_t sp = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  const uint64_t sp = a.s_lo + (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
   if (sp >= a.n_spans) return;
   const uint32_t n = min(a.span_count[sp], a.cap);
   const uint64_t gb = a.span_base[sp];
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     const uint64_t mp = p - 20;  // p >= 20 by construction
     const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
     int64_t par = PAR_MISS;
-    if (sp2 < a.n_spans) {
+    if (sp2 >= a.s_lo && sp2 < a.n_spans) {
       const uint32_t n2 = min(a.span_count[sp2], a.cap);
       uint32_t lo = 0, hi = n2;
       const uint64_t* cm = a.c_m + sp2 * a.cap;
@@ -146,7 +148,13 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
       }
       if (lo < n2 && cm[lo] == mp) par = (int64_t)(a.span_base[sp2] + lo);
     }
-    if (par == PAR_MISS && p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) par = PAR_ROOT;
+    if (par == PAR_MISS) {
+      if (a.span_lo) {
+        if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
+      } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {
+        par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
+      }
+    }
     a.d_m[g] = m;
     a.d_par[g] = par;
     a.d_slot[g] = gi;
@@ -171,6 +179,7 @@ struct ShapeArgs {
   uint64_t* chain_g;
   const unsigned long long* counters;
   Plan* plan;
+  uint32_t coff;     // chain entries before the first candidate (1 whole file, 0 span mode)
 };
 
 __device__ __forceinline__ uint64_t start_node(const ShapeArgs& a, uint64_t K) {
@@ -232,7 +241,8 @@ __global__ __launch_bounds__(1024) void plan_kernel(ShapeArgs a) {
   pl->max_root = a.counters[0];
   pl->n_weak = a.counters[1];
   pl->overflow = a.counters[2];
-  const bool troot = ld_u64_unaligned(a.file, a.flen - 12) == 0;  // flen >= 21 here
+  // whole file only: file_len is itself a root tail (prev 0); flen >= 21 here
+  const bool troot = a.coff && ld_u64_unaligned(a.file, a.flen - 12) == 0;
   pl->troot = troot;
   if (troot) {  // file_len is itself a root tail: chain = that one entry
     pl->status = 0;
@@ -249,7 +259,7 @@ __global__ __launch_bounds__(1024) void plan_kernel(ShapeArgs a) {
   if (pl->nroot != 1) st |= ST_ROOTS;
   pl->status = st;
   pl->chain_core = total;
-  pl->n_chain = st ? 0 : 1 + total;
+  pl->n_chain = st ? 0 : a.coff + total;
 }
 
 __global__ __launch_bounds__(256) void scatter2_kernel(ShapeArgs a) {
@@ -258,7 +268,7 @@ __global__ __launch_bounds__(256) void scatter2_kernel(ShapeArgs a) {
   const uint64_t K = *a.Kp;
   uint64_t lo, hi;
   chunk_of(K, &lo, &hi);
-  uint64_t run = 1 + (uint64_t)a.part_ex[blockIdx.x];
+  uint64_t run = a.coff + (uint64_t)a.part_ex[blockIdx.x];
   for (uint64_t base = lo; base < hi; base += blockDim.x) {
     const uint64_t g = base + threadIdx.x;
     const bool f = g < hi && a.flag[g];
@@ -403,6 +413,75 @@ __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
       a.opacked[run + r] = ((key >> 48) << 48) | (a.mo[c] & 0xFFFFFFFFFFFFull);  // key_indexer.rs:79-85
     }
     run += tot;
+  }
+}
+
+// --------------------------------------------------------------------------
+// Index exchange between entry-range shards: partition (key_hash, value)
+// pairs by owner rank, stable (chain order kept inside every owner's run),
+// so that after an all-to-all each owner's received runs are in shard order
+// = file order and the bucketed build's latest-wins-by-position is exact.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t world) {
+  return (uint32_t)(((key >> 32) * (uint64_t)world) >> 32);  // key hashes are XXH3 outputs: uniform
+}
+constexpr uint32_t PART_MAX_WORLD = 64;
+struct PartArgs {
+  const uint64_t* keys;
+  const uint64_t* vals;
+  uint64_t n;
+  uint32_t world;
+  uint32_t* cnt;  // [world * GLUE_BLOCKS + 1], owner-major
+  uint32_t* off;  // exclusive scan of cnt
+  uint64_t* out;  // [2n] interleaved (key, value), grouped by owner
+  uint64_t* counts;  // [world]
+};
+__global__ __launch_bounds__(256) void part_count_kernel(PartArgs a) {
+  __shared__ uint32_t h[PART_MAX_WORLD];
+  for (uint32_t o = threadIdx.x; o < a.world; o += blockDim.x) h[o] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[(uint64_t)a.world * GLUE_BLOCKS] = 0;
+  __syncthreads();
+  uint64_t lo, hi;
+  chunk_of(a.n, &lo, &hi);
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&h[owner_of(a.keys[i], a.world)], 1u);
+  __syncthreads();
+  for (uint32_t o = threadIdx.x; o < a.world; o += blockDim.x) a.cnt[(uint64_t)o * GLUE_BLOCKS + blockIdx.x] = h[o];
+}
+__global__ __launch_bounds__(256) void part_scatter_kernel(PartArgs a) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t run[PART_MAX_WORLD];
+  for (uint32_t o = threadIdx.x; o < a.world; o += blockDim.x) run[o] = a.off[(uint64_t)o * GLUE_BLOCKS + blockIdx.x];
+  __syncthreads();
+  uint64_t lo, hi;
+  chunk_of(a.n, &lo, &hi);
+  for (uint64_t base = lo; base < hi; base += blockDim.x) {
+    const uint64_t i = base + threadIdx.x;
+    const bool in = i < hi;
+    const uint64_t k = in ? a.keys[i] : 0;
+    const uint32_t own = in ? owner_of(k, a.world) : ~0u;
+    for (uint32_t o = 0; o < a.world; o++) {
+      uint32_t tot;
+      const uint32_t r = block_rank256(own == o, wsum, &tot);
+      if (own == o) {
+        const uint64_t pos = (uint64_t)run[o] + r;
+        a.out[2 * pos] = k;
+        a.out[2 * pos + 1] = a.vals[i];
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) run[o] += tot;
+      __syncthreads();
+    }
+  }
+}
+__global__ void part_counts_kernel(PartArgs a) {
+  const uint32_t o = threadIdx.x;
+  if (o < a.world) a.counts[o] = a.off[(uint64_t)(o + 1) * GLUE_BLOCKS] - a.off[(uint64_t)o * GLUE_BLOCKS];
+}
+// interleaved pairs -> key / value arrays (the bucketed build's input)
+__global__ void deinterleave_kernel(const uint64_t* pairs, uint64_t n, uint64_t* k, uint64_t* v) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    k[i] = pairs[2 * i];
+    v[i] = pairs[2 * i + 1];
   }
 }
 

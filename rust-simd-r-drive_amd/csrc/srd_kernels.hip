@@ -86,6 +86,11 @@ struct ScanArgs {
   unsigned long long* counters;    // [0] max root tail, [1] weak, [2] overflow
   uint32_t ablate;                 // timing experiments only (SRD_SCAN_ABLATE): 1 no CRC, 2 no slow path, 4 slow path stops after the exact test
   uint32_t filt_hb;                // (file_len-1) >> 32: bound of a node's p-byte 4 (p < file_len < 2^40)
+  // span mode (entry-range shard): tiles [k_lo, n_tiles) are resident, k_lo a
+  // multiple of SPAN_TILES; only nodes with m > m_lo are recorded (m_lo = the
+  // shard's lower tail; 0 = whole file, where m >= 1)
+  uint64_t k_lo;
+  uint64_t m_lo;
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -287,8 +292,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // balanced contiguous tile range per wave (whole spans)
   const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES_V2;
   const uint64_t w = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
-  const uint64_t spw = (a.n_spans + total_waves - 1) / total_waves;
-  const uint64_t s0 = w * spw;
+  const uint64_t s_lo = a.k_lo / SPAN_TILES;
+  const uint64_t spw = (a.n_spans - s_lo + total_waves - 1) / total_waves;
+  const uint64_t s0 = s_lo + w * spw;
   const uint64_t k0 = s0 * SPAN_TILES;
   const uint64_t k1 = min((s0 + spw) * SPAN_TILES, a.n_tiles);
   if (k0 >= k1) return;
@@ -323,7 +329,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     // the line just before this wave's first tile: its tail bytes and its raw
     // CRC (= SX_63 of tile k0-1) seed the window; all lanes load it
     uint32_t pl[16];
-    const u32x4* q = (const u32x4*)(file + (k0 ? k0 * (uint64_t)TILE - 64 : 0));
+    const bool has_prev = k0 > a.k_lo;  // the line before the resident range reads as zeros
+    const u32x4* q = (const u32x4*)(file + (has_prev ? k0 * (uint64_t)TILE - 64 : k0 * (uint64_t)TILE));
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const u32x4 v = q[j];
@@ -332,8 +339,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     const uint32_t cp = SRD_CRC_LINE(pl, lds, R);
     if (lane == 0) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) win[j] = k0 ? pl[12 + j] : 0u;
-      win[22] = k0 ? cp : 0u;
+      for (int j = 0; j < 4; j++) win[j] = has_prev ? pl[12 + j] : 0u;
+      win[22] = has_prev ? cp : 0u;
     }
   }
 
@@ -412,7 +419,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint32_t f4 = alignb(W[5], W[4], sh);
       // recover_valid_chain's node test (data_store.rs:404-470) at m = B + r
       const uint32_t u = (uint32_t)(r + 20);  // t - B >= 6
-      const bool inrange = (u <= remu) && (B != 0 || r >= 1);
+      const bool inrange = (u <= remu) && ((int64_t)B + r > (int64_t)a.m_lo);
       const uint64_t roots = __ballot(inrange && (f2 | f3) == 0);
       if (roots) rootmax = B + (uint64_t)(64 * f - 14 + 20) + (63 - __builtin_clzll(roots));  // increasing in (k, f)
       const uint64_t m = B + (int64_t)r;
@@ -677,6 +684,10 @@ struct FinArgs {
   const uint64_t* d_n_chain;
   const uint64_t* d_root_t;
   const uint32_t* d_status;
+  // chain entries before the first candidate: 1 (entry 0 is the root entry
+  // with prev 0, not a candidate) or 0 (span mode: the shard's first entry,
+  // prev == the shard's lower tail, is a candidate record)
+  uint32_t coff;
   // outputs
   uint64_t *o_mo, *o_kh, *o_prev, *o_start, *o_len;
   uint32_t *o_crc_st, *o_crc, *o_pieces;  // o_pieces: bit0 suf ok, bit1 sxm ok (slow path input)
@@ -752,7 +763,7 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
   uint64_t mo, kh, p, start, len;
   uint32_t crc_st, suf = 0, sxm = 0, tail = 0, pieces = 0;
   bool tomb;
-  if (c == 0) {
+  if (c < a.coff) {
     const uint64_t t = root_t;
     mo = t - 20;
     kh = ld_u64_unaligned(a.file, mo);
@@ -778,7 +789,7 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
       pieces |= 2;
     }
     if (fl & F_TAIL) { tail = 0; pieces |= 4; }
-    const int64_t pg = a.d_status ? (c >= 2 ? 0 : PAR_ROOT) : a.par[g];
+    const int64_t pg = a.d_status ? (c >= a.coff + 1 ? 0 : PAR_ROOT) : a.par[g];
     if (pg >= 0) {
       const uint64_t pgi = a.d_status ? a.chain_g[c - 1] : a.slot[pg];
       const u32x4 pr1 = a.c_rec[2 * pgi + 1];
@@ -981,16 +992,20 @@ __device__ __forceinline__ uint64_t synth_word(uint64_t seed, uint64_t entry, ui
 }
 
 // one wave per entry; entry_off[i] = prev tail (where the prepad starts)
+// `out` is indexed by absolute file offset; bytes below clip_lo (a multiple
+// of 64) are not written (span mode: they precede the shard's resident range).
+// Entry i of this launch is global entry id0 + i (its key and payload seed).
 __global__ __launch_bounds__(64) void synth_kernel(uint8_t* out, const uint64_t* entry_off,
                                                    const uint64_t* lens, uint64_t fixed_len, uint64_t n,
-                                                   uint64_t seed) {
+                                                   uint64_t seed, uint64_t id0, uint64_t clip_lo) {
   const int lane = threadIdx.x & 63;
   for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint64_t tail = entry_off[i];
     const uint64_t len = lens ? lens[i] : fixed_len;
     const uint64_t pad = prepad64(tail);
     const uint64_t st = tail + pad;  // 64-aligned
-    if (lane < (int)pad) out[tail + lane] = 0;
+    const uint64_t id = id0 + i;
+    if (lane < (int)pad && tail + lane >= clip_lo) out[tail + lane] = 0;
     // payload: 8-byte words
     uint32_t acc = 0;
     for (uint64_t blk = 0; blk < len; blk += TILE) {
@@ -999,10 +1014,12 @@ __global__ __launch_bounds__(64) void synth_kernel(uint8_t* out, const uint64_t*
       uint64_t le = ls + 64 < len ? ls + 64 : len;
       if (ls < len) {
         for (uint64_t w = ls / 8; w * 8 < le; w++) {
-          const uint64_t v = synth_word(seed, i, w);
+          const uint64_t v = synth_word(seed, id, w);
           const uint64_t nb = le - w * 8 < 8 ? le - w * 8 : 8;
-          if (nb == 8) *(uint64_t*)(out + st + w * 8) = v;  // st is 64-aligned
-          else for (uint64_t b = 0; b < nb; b++) out[st + w * 8 + b] = (uint8_t)(v >> (8 * b));
+          if (st + w * 8 >= clip_lo) {
+            if (nb == 8) *(uint64_t*)(out + st + w * 8) = v;  // st is 64-aligned
+            else for (uint64_t b = 0; b < nb; b++) out[st + w * 8 + b] = (uint8_t)(v >> (8 * b));
+          }
           for (uint64_t b = 0; b < nb; b++) s = g_tabs.tab[0][(s ^ (uint32_t)(v >> (8 * b))) & 0xff] ^ (s >> 8);
         }
       }
@@ -1017,14 +1034,16 @@ __global__ __launch_bounds__(64) void synth_kernel(uint8_t* out, const uint64_t*
       uint8_t key[32] = {'b', 'e', 'n', 'c', 'h', '-', 'k', 'e', 'y', '-'};
       uint8_t dig[24];
       int nd = 0;
-      uint64_t v = i;
+      uint64_t v = id;
       do { dig[nd++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
       for (int q = 0; q < nd; q++) key[10 + q] = dig[nd - 1 - q];
       const uint64_t kh = xxh3_64(key, 10 + nd);
-      uint8_t* mb = out + st + len;
-      for (int b = 0; b < 8; b++) mb[b] = (uint8_t)(kh >> (8 * b));
-      for (int b = 0; b < 8; b++) mb[8 + b] = (uint8_t)(tail >> (8 * b));
-      for (int b = 0; b < 4; b++) mb[16 + b] = (uint8_t)(crc >> (8 * b));
+      uint8_t mbuf[20];
+      for (int b = 0; b < 8; b++) mbuf[b] = (uint8_t)(kh >> (8 * b));
+      for (int b = 0; b < 8; b++) mbuf[8 + b] = (uint8_t)(tail >> (8 * b));
+      for (int b = 0; b < 4; b++) mbuf[16 + b] = (uint8_t)(crc >> (8 * b));
+      for (int b = 0; b < 20; b++)
+        if (st + len + b >= clip_lo) out[st + len + b] = mbuf[b];
     }
   }
 }

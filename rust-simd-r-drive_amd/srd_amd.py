@@ -30,6 +30,10 @@ LIB_PATH = os.path.join(HERE, "build", "libsrd_amd.so")
 
 SRD_FLAG_FORCE_FULL = 1
 SRD_FLAG_NO_CRC = 2
+SRD_MODE_OPTIMISTIC = 0
+SRD_MODE_FULL = 1
+SRD_MODE_SPAN_UNPROVEN = 3
+SPAN_ALIGN = 16384  # span_off granularity of srd_validate_span_device
 METADATA_SIZE = 20
 NULL_BYTE = b"\x00"
 TAG_BITS = 16
@@ -42,6 +46,8 @@ EXPORTS = [
     "srd_recover_valid_chain", "srd_key_indexer_build", "srd_crc32_batch",
     "srd_crc32_batch_device", "srd_xxh3_64_batch", "srd_xxh3_64_batch_device",
     "srd_synth_store_device", "srd_selftest_host", "srd_padded_size",
+    "srd_validate_span_device", "srd_index_partition_device", "srd_index_build_device",
+    "srd_synth_span_device",
 ]
 
 
@@ -99,6 +105,10 @@ def lib():
         L.srd_padded_size.argtypes = [u64]
         L.srd_padded_size.restype = u64
         L.srd_synth_store_device.argtypes = [vp, vp, u64, u64, vp, u64, C.POINTER(u64)]
+        L.srd_validate_span_device.argtypes = [vp, vp, u64, u64, u64, u32, C.POINTER(DeviceResult)]
+        L.srd_index_partition_device.argtypes = [vp, vp, vp, u64, u32, vp, vp]
+        L.srd_index_build_device.argtypes = [vp, vp, u64, vp, vp, C.POINTER(u64)]
+        L.srd_synth_span_device.argtypes = [vp, vp, u64, u64, u64, u64, vp, u64, C.POINTER(u64), C.POINTER(u64)]
         for f in EXPORTS:
             if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
                          "srd_padded_size"):
@@ -224,6 +234,76 @@ def validate_index_device(d_ptr: int, file_len: int, flags: int = 0, ctx: Contex
     r = DeviceResult()
     _check(lib().srd_validate_index_device(ctx.h, C.c_void_p(d_ptr), file_len, flags, C.byref(r)))
     return r
+
+
+class _DevView:
+    def __init__(self, ptr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 3}
+
+
+_TYPESTR = {np.uint64: "<i8", np.uint32: "<i4", np.uint8: "|u1"}
+
+
+def device_view(ptr: int, n: int, dtype=np.uint64, device: int = 0):
+    """Zero-copy torch view of n elements of a library-owned device array
+    (result arrays of the *_device calls; int64/int32/uint8 bit patterns)."""
+    import torch
+    if n == 0 or not ptr:
+        return torch.empty(0, dtype={np.uint64: torch.int64, np.uint32: torch.int32, np.uint8: torch.uint8}[dtype],
+                           device=f"cuda:{device}")
+    return torch.as_tensor(_DevView(ptr, n, _TYPESTR[dtype]), device=f"cuda:{device}")
+
+
+def device_to_numpy(ptr: int, n: int, dtype=np.uint64) -> np.ndarray:
+    return device_view(ptr, n, dtype).cpu().numpy().view(dtype).copy()
+
+
+def validate_span_device(d_ptr: int, span_off: int, lo: int, hi: int, flags: int = 0,
+                         ctx: Context | None = None) -> DeviceResult:
+    """Entry-range shard [lo, hi) of a store, resident at d_ptr = file byte
+    span_off (srd_validate_span_device).  mode == SRD_MODE_SPAN_UNPROVEN means
+    the caller must use the whole-file path."""
+    ctx = ctx or default_ctx()
+    r = DeviceResult()
+    _check(lib().srd_validate_span_device(ctx.h, C.c_void_p(d_ptr), span_off, lo, hi, flags, C.byref(r)))
+    return r
+
+
+def index_partition_device(d_keys: int, d_vals: int, n: int, world: int, d_out_pairs: int,
+                           ctx: Context | None = None) -> list[int]:
+    """Group n device (key_hash, value) pairs by owner rank into interleaved
+    pairs at d_out_pairs; returns the per-owner counts."""
+    ctx = ctx or default_ctx()
+    counts = np.zeros(max(world, 1), np.uint64)
+    _check(lib().srd_index_partition_device(ctx.h, C.c_void_p(d_keys), C.c_void_p(d_vals), n, world,
+                                            C.c_void_p(d_out_pairs), _ptr(counts)))
+    return [int(x) for x in counts[:world]]
+
+
+def index_build_device(d_pairs: int, n: int, d_out_keys: int, d_out_packed: int,
+                       ctx: Context | None = None) -> int:
+    """KeyIndexer::build over n interleaved device (key_hash, offset) pairs in
+    file order; returns the index size."""
+    ctx = ctx or default_ctx()
+    out = C.c_uint64()
+    _check(lib().srd_index_build_device(ctx.h, C.c_void_p(d_pairs), n, C.c_void_p(d_out_keys),
+                                        C.c_void_p(d_out_packed), C.byref(out)))
+    return out.value
+
+
+def synth_span(d_ptr: int | None, span_off: int, first: int, n: int, payload_len: int = 4096, lens=None,
+               seed: int = 0x5EED0001, ctx: Context | None = None) -> tuple[int, int]:
+    """Shard of the synthetic store holding entries [first, first+n): returns
+    (lo, hi); writes file bytes [span_off, hi) at d_ptr when given."""
+    lo, hi = C.c_uint64(), C.c_uint64()
+    lp = None
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, np.uint64)
+        lp = _ptr(lens)
+    h = (ctx or default_ctx()).h if d_ptr else C.c_void_p(0)
+    _check(lib().srd_synth_span_device(h, C.c_void_p(d_ptr or 0), span_off, first, n, payload_len, lp, seed,
+                                       C.byref(lo), C.byref(hi)))
+    return lo.value, hi.value
 
 
 def recover_valid_chain(file, ctx: Context | None = None) -> int:

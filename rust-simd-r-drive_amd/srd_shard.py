@@ -1,0 +1,135 @@
+"""Multi-GPU open of one store sharded by entry range.
+
+One process per GPU.  Rank r holds the file bytes of entries
+[first_r, first_r + n_r) in its HBM (plus < 16 KiB of the previous shard as a
+halo, so the span starts on a 16 KiB boundary) and proves, with
+srd_validate_span_device, that the backward chain from its upper tail hi_r
+reaches an entry whose prev_offset is its lower tail lo_r.  No data-path
+collective is needed for that: shards are independent.
+
+The exchange step is small and real:
+  1. boundaries: all_gather of (proven, lo, hi, n_chain, n_crc_bad) -- the
+     shard chains compose into the whole file's chain iff every shard is
+     proven, lo_0 == 0, hi_r == lo_{r+1} and hi_{W-1} == file_len.  That is
+     recover_valid_chain's answer (data_store.rs:383-482) for a clean store:
+     final_len = file_len.  Anything else (a torn tail, a corrupt shard) is
+     decided by the whole-file path, whose byte-wise outer loop is global.
+  2. index: KeyIndexer::build (key_indexer.rs:98-124) is latest-wins over the
+     whole chain, so keys that live in several shards must meet.  Each rank
+     partitions its shard-local index by owner = ((key_hash >> 32) * W) >> 32,
+     an all_to_all moves the pairs to their owners (16 B per key), and each
+     owner runs the bucketed build over the runs it received, which arrive in
+     shard order = file order, so latest-wins-by-position stays exact.  The
+     global index is the disjoint union of the owners' indexes; its size is
+     an all_reduce(SUM).
+
+The device work goes through a backend object so that the protocol can be
+exercised on CPU with the gloo backend in the tests (tests/test_shard_gloo.py
+plugs in the oracle there, as the checker); `HipBackend` is the product and
+has no fallback.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+import srd_amd as S
+
+
+def plan_entry_shards(n_entries: int, world: int) -> list[tuple[int, int]]:
+    """Equal entry-count ranges (first, count), one per rank."""
+    base, extra = divmod(n_entries, world)
+    out, first = [], 0
+    for r in range(world):
+        n = base + (1 if r < extra else 0)
+        out.append((first, n))
+        first += n
+    return out
+
+
+@dataclass
+class ShardStatus:
+    proven: bool
+    lo: int
+    hi: int
+    n_chain: int
+    n_crc_bad: int
+
+
+@dataclass
+class ShardedResult:
+    final_len: int          # whole-file recover_valid_chain result (file_len when all shards compose)
+    composed: bool          # False -> the caller must run the whole-file path
+    n_chain: int            # chain entries over all shards
+    n_crc_bad: int
+    n_index: int            # global KeyIndexer size (disjoint union of owner indexes)
+    owner_keys: torch.Tensor    # this rank's part of the global index (key_hash as int64 bits)
+    owner_packed: torch.Tensor  # pack(tag16, offset48) as int64 bits
+    local: object = None        # backend's shard-local result (chain arrays)
+
+
+class HipBackend:
+    """Device work on this rank's GPU through the C ABI (libsrd_amd.so)."""
+
+    def __init__(self, ctx: S.Context, device: int):
+        self.ctx, self.device = ctx, device
+
+    def validate_span(self, buf: torch.Tensor, span_off: int, lo: int, hi: int, flags: int = 0):
+        r = S.validate_span_device(buf.data_ptr(), span_off, lo, hi, flags, self.ctx)
+        proven = r.mode == S.SRD_MODE_OPTIMISTIC or (lo == 0 and r.final_len == hi)
+        st = ShardStatus(bool(proven), lo, hi, int(r.n_chain), int(r.n_crc_bad))
+        keys = S.device_view(r.index_key_hash, r.n_index, np.uint64, self.device)
+        packed = S.device_view(r.index_packed, r.n_index, np.uint64, self.device)
+        return st, keys, packed, r
+
+    def partition(self, keys: torch.Tensor, packed: torch.Tensor, world: int):
+        n = keys.numel()
+        pairs = torch.empty(2 * max(n, 1), dtype=torch.int64, device=keys.device)
+        counts = S.index_partition_device(keys.data_ptr(), packed.data_ptr(), n, world, pairs.data_ptr(), self.ctx)
+        return pairs[: 2 * n], counts
+
+    def build(self, pairs: torch.Tensor):
+        n = pairs.numel() // 2
+        ok = torch.empty(max(n, 1), dtype=torch.int64, device=pairs.device)
+        op = torch.empty(max(n, 1), dtype=torch.int64, device=pairs.device)
+        ni = S.index_build_device(pairs.data_ptr(), n, ok.data_ptr(), op.data_ptr(), self.ctx)
+        return ok[:ni], op[:ni]
+
+
+def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, hi: int, file_len: int,
+                           group=None) -> ShardedResult:
+    """One rank's part of the sharded open: validate its shard, check the
+    composition, exchange the index.  Collective over `group`."""
+    world = dist.get_world_size(group)
+    dev = buf.device
+    # collectives run where the backend lives: device memory for nccl (RCCL
+    # over xGMI), host memory for gloo (CPU tests, several ranks on one GPU)
+    cd = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
+    st, keys, packed, local = backend.validate_span(buf, span_off, lo, hi)
+    # 1. boundaries
+    mine = torch.tensor([int(st.proven), st.lo, st.hi, st.n_chain, st.n_crc_bad], dtype=torch.int64, device=cd)
+    allst = torch.empty(world * 5, dtype=torch.int64, device=cd)
+    dist.all_gather_into_tensor(allst, mine, group=group)
+    rows = allst.view(world, 5).cpu().tolist()
+    composed = all(r[0] for r in rows) and rows[0][1] == 0 and rows[-1][2] == file_len and all(
+        rows[i][2] == rows[i + 1][1] for i in range(world - 1))
+    n_chain = sum(r[3] for r in rows)
+    n_bad = sum(r[4] for r in rows)
+    if not composed:
+        empty = torch.empty(0, dtype=torch.int64, device=dev)
+        return ShardedResult(0, False, 0, 0, 0, empty, empty, local)
+    # 2. index exchange
+    pairs, counts = backend.partition(keys, packed, world)
+    send = torch.tensor(counts, dtype=torch.int64, device=cd)
+    recv = torch.empty(world, dtype=torch.int64, device=cd)
+    dist.all_to_all_single(recv, send, group=group)
+    rc = recv.cpu().tolist()
+    got = torch.empty(2 * sum(rc), dtype=torch.int64, device=cd)
+    dist.all_to_all_single(got, pairs.to(cd), [2 * c for c in rc], [2 * c for c in counts], group=group)
+    okeys, opacked = backend.build(got.to(dev))
+    ni = torch.tensor([okeys.numel()], dtype=torch.int64, device=cd)
+    dist.all_reduce(ni, group=group)
+    return ShardedResult(file_len, True, n_chain, n_bad, int(ni.item()), okeys, opacked, local)

@@ -1,0 +1,67 @@
+"""The product multi-GPU path (srd_shard.sharded_validate_index + HipBackend)
+with 2 and 3 ranks in separate processes sharing this box's one GPU (gloo for
+the exchange; the driver's 8-GPU run uses RCCL): the merged global index
+equals the oracle's KeyIndexer::build of the same whole store."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _worker(rank, world, port, n_total, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import srd_amd as S
+    import srd_shard as SH
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        ctx = S.Context(0)
+        first, cnt = SH.plan_entry_shards(n_total, world)[rank]
+        lo, hi = S.synth_span(None, 0, first, cnt, 1000)
+        span_off = lo - lo % S.SPAN_ALIGN
+        buf = torch.zeros(S.padded_size(hi - span_off), dtype=torch.uint8, device="cuda:0")
+        S.synth_span(buf.data_ptr(), span_off, first, cnt, 1000, ctx=ctx)
+        res = SH.sharded_validate_index(SH.HipBackend(ctx, 0), buf, span_off, lo, hi, S.synth_store_len(n_total, 1000))
+        q.put((rank, res.composed, res.final_len, res.n_chain, res.n_crc_bad, res.n_index,
+               dict(zip(res.owner_keys.cpu().numpy().view(np.uint64).tolist(),
+                        res.owner_packed.cpu().numpy().view(np.uint64).tolist()))))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_open_two_processes(world):
+    import torch.multiprocessing as mp
+    import oracle as O
+    n = 3001
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    store = O.synth_store(n, 1000)
+    want = O.key_indexer_build(store, store.size)
+    merged = {}
+    for rank, composed, final_len, n_chain, n_bad, n_index, idx in out:
+        assert (composed, final_len, n_chain, n_bad, n_index) == (True, store.size, n, 0, len(want))
+        assert not (merged.keys() & idx.keys())
+        merged.update(idx)
+    assert merged == want

@@ -1,0 +1,140 @@
+"""The multi-GPU exchange protocol of srd_shard (boundary composition +
+owner-partitioned index all_to_all) on CPU: world_size 2 and 3 over gloo.
+The per-shard device work is replaced by the CPU oracle (test checker only);
+the product HipBackend is covered by tests/test_gpu_shards.py on the GPU."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class OracleBackend:
+    """Stand-in for HipBackend: same outputs, computed by the oracle."""
+
+    def __init__(self, store):
+        import oracle as O
+        self.O, self.store = O, store
+        self.flen = O.recover_valid_chain(store)
+        self.chain = O.chain(store, self.flen)
+        self.tails = {e["meta_off"] + 20: i for i, e in enumerate(self.chain)}
+
+    def validate_span(self, buf, span_off, lo, hi, flags=0):
+        ch = self.chain
+        a = 0 if lo == 0 else self.tails.get(lo, -1) + 1
+        b = self.tails.get(hi, -2) + 1
+        proven = a >= 0 and b > a and (lo == 0 or ch[a]["prev_offset"] == lo)
+        seg = ch[a:b] if proven else []
+        latest = {}
+        for e in seg:
+            latest[e["key_hash"]] = ((e["key_hash"] >> 48) << 48) | e["meta_off"]
+        from srd_shard import ShardStatus
+        st = ShardStatus(bool(proven), lo, hi, len(seg), sum(1 - e["crc_ok"] for e in seg))
+        k = torch.tensor(np.array(list(latest.keys()), np.uint64).view(np.int64))
+        v = torch.tensor(np.array(list(latest.values()), np.uint64).view(np.int64))
+        return st, k, v, seg
+
+    def partition(self, keys, packed, world):
+        ku = keys.numpy().view(np.uint64)
+        own = ((ku >> np.uint64(32)) * np.uint64(world)) >> np.uint64(32)
+        order = np.argsort(own, kind="stable")
+        pairs = np.stack([keys.numpy()[order], packed.numpy()[order]], 1).reshape(-1)
+        return torch.from_numpy(pairs.copy()), [int((own == w).sum()) for w in range(world)]
+
+    def build(self, pairs):
+        p = pairs.numpy().reshape(-1, 2)
+        latest = {}
+        for k, v in p:
+            latest.pop(int(k), None)  # latest position wins; order = file order of the latest entry
+            latest[int(k)] = int(v)
+        return torch.tensor(list(latest.keys()), dtype=torch.int64), torch.tensor(list(latest.values()), dtype=torch.int64)
+
+
+def _worker(rank, world, port, store_bytes, cuts, torn, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import srd_shard as SH
+        store = np.frombuffer(store_bytes, np.uint8)
+        be = OracleBackend(np.frombuffer(store_bytes[:len(store_bytes) - torn], np.uint8) if torn else store)
+        full = OracleBackend(store)
+        tails = [0] + [e["meta_off"] + 20 for e in full.chain]
+        a, b = cuts[rank], cuts[rank + 1]
+        lo, hi = tails[a], tails[b]
+        file_len = store.size - torn
+        if rank == world - 1:
+            hi = file_len
+        span_off = lo - lo % 16384
+        buf = torch.from_numpy(store[span_off:hi].copy())
+        res = SH.sharded_validate_index(be, buf, span_off, lo, hi, file_len)
+        q.put((rank, res.composed, res.final_len, res.n_chain, res.n_index,
+               dict(zip(res.owner_keys.numpy().view(np.uint64).tolist(), res.owner_packed.numpy().view(np.uint64).tolist()))))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(world, store, cuts, torn=0):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, store.tobytes(), cuts, torn, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return sorted(out)
+
+
+def _store():
+    import random
+    import xxhash
+    import oracle as O
+    rnd = random.Random(41)
+    buf = bytearray()
+    t = 0
+    for _ in range(300):
+        kh = xxhash.xxh3_64_intdigest(b"k%d" % rnd.randrange(70))
+        if rnd.random() < 0.1:
+            t = O.write_entries(buf, t, [(kh, b"\x00")], allow_null=True)
+        else:
+            t = O.write_entries(buf, t, [(kh, rnd.randbytes(rnd.choice([1, 9, 64, 500, 4096])))])
+    return np.frombuffer(bytes(buf), np.uint8)
+
+
+@pytest.mark.parametrize("world,cuts", [(2, [0, 150, 300]), (3, [0, 1, 200, 300])])
+def test_sharded_exchange_matches_whole_file(world, cuts):
+    import oracle as O
+    store = _store()
+    out = _run(world, store, cuts)
+    want = O.key_indexer_build(store, store.size)
+    merged = {}
+    for rank, composed, final_len, n_chain, n_index, idx in out:
+        assert composed and final_len == store.size and n_chain == 300 and n_index == len(want)
+        for k, v in idx.items():
+            assert k not in merged
+            assert ((k >> 32) * world) >> 32 == rank  # owner partition
+            merged[k] = v
+    assert merged == want
+
+
+def test_sharded_torn_tail_is_not_composed():
+    store = _store()
+    out = _run(2, store, [0, 150, 300], torn=9)
+    assert all(not composed for _, composed, *_ in out)

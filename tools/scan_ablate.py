@@ -1,6 +1,6 @@
 # timing-only helper: scan-kernel time on the C2 store under SRD_SCAN_ABLATE variants
 import os, sys, json
-sys.path.insert(0, "rust-simd-r-drive_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rust-simd-r-drive_amd"))
 import torch, srd_amd as S
 ctx = S.Context(0)
 n = 1 << 20
