@@ -84,7 +84,7 @@ typedef struct {
   uint64_t n_index;        /* KeyIndexer entries */
   uint64_t n_crc_bad;      /* chain entries whose CRC does not match */
   uint64_t n_candidates;   /* chain-node candidates recorded by the scan */
-  uint64_t n_weak;         /* candidates skipped by the optimistic pass */
+  uint64_t n_weak;         /* reserved (0) */
   uint32_t mode;           /* 0 = optimistic pass sufficed, 1 = full pass */
   uint32_t reserved;
   /* chain, file order; device pointers */

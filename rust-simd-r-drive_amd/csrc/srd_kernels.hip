@@ -83,7 +83,7 @@ struct ScanArgs {
   uint32_t* span_count;
   uint64_t* c_m;                   // [n_spans*cap] candidate metadata offsets
   u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
-  unsigned long long* counters;    // [0] max root tail, [1] weak, [2] overflow
+  unsigned long long* counters;    // [0] max root tail, [1] unused, [2] overflow
   uint32_t ablate;                 // timing experiments only (SRD_SCAN_ABLATE): 1 no CRC, 2 no slow path, 4 slow path stops after the exact test
   uint32_t filt_hb;                // (file_len-1) >> 32: bound of a node's p-byte 4 (p < file_len < 2^40)
   // span mode (entry-range shard): tiles [k_lo, n_tiles) are resident, k_lo a
@@ -324,7 +324,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // tile's SX partial of line 63 (= its true SX_63).
   const uint32_t hb = a.filt_hb;
   uint64_t rootmax = 0;
-  uint32_t weak = 0;
   {
     // the line just before this wave's first tile: its tail bytes and its raw
     // CRC (= SX_63 of tile k0-1) seed the window; all lanes load it
@@ -364,12 +363,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     if (lane < 2 || lane == 32) a.tile[4 * k + (lane == 32 ? 2 : lane)] = hx;
 
     // ---- filter, level 1: any aligned zero halfword in the lane's line
-    //      (16-bit has-zero, 2 VALU per dword); level 2 (exact, per
-    //      position) in the slow path: p >> 32 <= hb = (file_len-1) >> 32 ----
-    uint32_t acc = 0;
+    //      (packed 16-bit min over the 16 dwords: 1 VALU per dword); level 2
+    //      (exact, per position) in the slow path ----
+    u16x2 zmin = __builtin_bit_cast(u16x2, d[0]);
 #pragma unroll
-    for (int i = 0; i < 16; i++) acc |= (d[i] + 0xFFFEFFFFu) & ~d[i];
-    uint64_t slow = __ballot((acc & 0x80008000u) != 0);
+    for (int i = 1; i < 16; i++) zmin = __builtin_elementwise_min(zmin, __builtin_bit_cast(u16x2, d[i]));
+    uint64_t slow = __ballot(zmin.x == 0 || zmin.y == 0);
     if (a.ablate & 2) slow = 0;
 
     while (slow) {
@@ -412,15 +411,62 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // level 2, exact: p >> 32 <= (file_len-1) >> 32 (roots: p == 0 pass too)
       const uint32_t f3 = alignb(W[4], W[3], sh);
-      if (!__ballot(f3 <= hb) || (a.ablate & 4)) continue;
-      const uint32_t tbyte = (tdw >> (((o - 1) & 3) * 8)) & 0xffu;
-      const uint32_t f0 = alignb(W[1], W[0], sh), f1 = alignb(W[2], W[1], sh);
       const uint32_t f2 = alignb(W[3], W[2], sh);
       const uint32_t f4 = alignb(W[5], W[4], sh);
-      // recover_valid_chain's node test (data_store.rs:404-470) at m = B + r
       const uint32_t u = (uint32_t)(r + 20);  // t - B >= 6
       const bool inrange = (u <= remu) && ((int64_t)B + r > (int64_t)a.m_lo);
-      const uint64_t roots = __ballot(inrange && (f2 | f3) == 0);
+      if (!FULL) {
+        // optimistic pass: only strong nodes (p >= 20 so p != 0, crc field
+        // != 0) are recorded; a chain through any other node fails the shape
+        // check and goes to the full pass, so nothing else is needed here
+        const uint64_t pm = __ballot(inrange && f3 <= hb && (f2 | f3) != 0 && f4 != 0);
+        if (!pm || (a.ablate & 4)) continue;
+        if ((pm & (pm - 1)) == 0) {
+          // one possible node (the common case: one metadata record per
+          // line): the node test and the record run on the scalar unit
+          const int bl = __builtin_ctzll(pm);
+          const uint32_t s2 = __builtin_amdgcn_readlane(f2, bl), s3 = __builtin_amdgcn_readlane(f3, bl);
+          const int rs = 64 * f + bl - 14;
+          const uint32_t os = (uint32_t)bl + 2;
+          const uint32_t stb = (__builtin_amdgcn_readlane(tdw, bl) >> (((os - 1) & 3) * 8)) & 0xffu;
+          const uint64_t m = B + (int64_t)rs;
+          const uint64_t p = (uint64_t)s2 | ((uint64_t)s3 << 32);
+          const uint64_t dp = m - p;
+          const bool tomb = dp == 1 && stb == 0;
+          const uint32_t pp = (0u - s2) & 63u;
+          if (!(p >= 20 && p < m && (tomb || dp > pp))) continue;  // data_store.rs:404-470
+          const uint32_t us = (uint32_t)(rs + 20);
+          const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
+          const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
+          const int lm = rs >> 6;
+          const uint32_t hm = lm < 0 ? __builtin_amdgcn_readfirstlane(hxp) : __builtin_amdgcn_readlane(hx, lm & 63);
+          const uint32_t s0 = __builtin_amdgcn_readlane(alignb(W[1], W[0], sh), bl);
+          const uint32_t s1 = __builtin_amdgcn_readlane(alignb(W[2], W[1], sh), bl);
+          const uint32_t s4 = __builtin_amdgcn_readlane(f4, bl);
+          if (count < a.cap) {
+            if (lane == 0) {
+              const uint64_t gi = span * a.cap + count;
+              const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
+              const uint32_t fl = (tomb ? F_TOMB : 0u) | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
+                                  (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
+                                  ((js & 63) < 32 ? F_SUF_LO : 0u);
+              a.c_m[gi] = m;
+              a.c_rec[2 * gi] = u32x4{s2, s3, s0, s1};
+              a.c_rec[2 * gi + 1] = u32x4{s4, hm, hs, fl};
+            }
+          } else if (lane == 0) {
+            atomicOr((unsigned int*)(a.counters + 2), 1u);
+          }
+          count++;
+          continue;
+        }
+      } else if (!__ballot(f3 <= hb)) {
+        continue;
+      }
+      const uint32_t tbyte = (tdw >> (((o - 1) & 3) * 8)) & 0xffu;
+      const uint32_t f0 = alignb(W[1], W[0], sh), f1 = alignb(W[2], W[1], sh);
+      // recover_valid_chain's node test (data_store.rs:404-470) at m = B + r
+      const uint64_t roots = FULL ? __ballot(inrange && (f2 | f3) == 0) : 0ull;
       if (roots) rootmax = B + (uint64_t)(64 * f - 14 + 20) + (63 - __builtin_clzll(roots));  // increasing in (k, f)
       const uint64_t m = B + (int64_t)r;
       const uint64_t p = (uint64_t)f2 | ((uint64_t)f3 << 32);
@@ -429,7 +475,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint32_t pp = (0u - f2) & 63u;  // prepad(p)
       const bool isnode = inrange && p >= 20 && p < m && (tomb || dp > pp);
       const bool strong = isnode && (FULL || f4 != 0);
-      weak += (uint32_t)__popcll(__ballot(isnode && !strong));
       const uint64_t cm = __ballot(strong);
       if (!cm) continue;
       const uint32_t js = (u + ((0u - u) & 63u)) >> 6;  // line of the next entry's start
@@ -482,11 +527,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     process(k0 + j + 2, Cv, A);
   }
 
-  // rootmax / weak are wave-uniform already
-  if (lane == 0) {
-    if (rootmax) atomicMax(a.counters + 0, (unsigned long long)rootmax);
-    if (weak) atomicAdd(a.counters + 1, (unsigned long long)weak);
-  }
+  // rootmax is wave-uniform already
+  if (lane == 0 && rootmax) atomicMax(a.counters + 0, (unsigned long long)rootmax);
 }
 
 // --------------------------------------------------------------------------
