@@ -81,7 +81,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--entries-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
+                    help="c2: 4 KiB entries (headline); c3: Zipf-sized entries 64 B..1 MiB (variable length)")
+    ap.add_argument("--entries-per-gpu", type=int, default=None)
     ap.add_argument("--payload", type=int, default=4096)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -101,10 +103,15 @@ def main():
     ctx = S.Context(local)
 
     n, L = args.entries_per_gpu, args.payload
+    if n is None:
+        n = 1 << 20 if args.config == "c2" else 10_000_000
+    lens, seed = None, 0x5EED0001
+    if args.config == "c3":
+        lens, seed = S.zipf_lens(n * world), 0x5EED0004
     if world == 1:
-        size = S.synth_store_len(n, L)
+        size = S.synth_store_len(n, L, lens)
         store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
-        S.synth_store_device(store.data_ptr(), n, L, ctx=ctx)
+        S.synth_store_device(store.data_ptr(), n, L, lens, seed=seed, ctx=ctx)
         span = (0, 0, size)
 
         def step():
@@ -114,12 +121,12 @@ def main():
     else:
         import srd_shard as SH
         first, cnt = SH.plan_entry_shards(n * world, world)[rank]
-        lo, hi = S.synth_span(None, 0, first, cnt, L)
-        file_len = S.synth_store_len(n * world, L)
+        lo, hi = S.synth_span(None, 0, first, cnt, L, lens)
+        file_len = S.synth_store_len(n * world, L, lens)
         span_off = lo - lo % S.SPAN_ALIGN
         size = hi - span_off
         store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
-        S.synth_span(store.data_ptr(), span_off, first, cnt, L, ctx=ctx)
+        S.synth_span(store.data_ptr(), span_off, first, cnt, L, lens, seed=seed, ctx=ctx)
         span = (span_off, lo, hi)
         backend = SH.HipBackend(ctx, local)
 
@@ -128,7 +135,11 @@ def main():
             return r.final_len, r.n_chain, r.n_crc_bad, r.n_index
         expect = (file_len, n * world, 0, n * world)
     torch.cuda.synchronize()
-    bytes_alg = algorithmic_bytes(n, L)
+    if lens is None:
+        bytes_alg = algorithmic_bytes(n, L)
+    else:  # this rank's entries: sum(L_i + 20)
+        f0 = rank * n if world > 1 else 0
+        bytes_alg = int(lens[f0:f0 + n].sum()) + 20 * n
 
     for _ in range(args.warmup):
         got = step()
@@ -159,7 +170,7 @@ def main():
     achieved = bytes_alg / (scan_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tf) and world == 1 and n == 1 << 20 and L == 4096:  # measured on the C2 workload only
+    if os.path.exists(tf) and world == 1 and n == 1 << 20 and L == 4096 and args.config == "c2":  # measured on the C2 workload only
         try:
             traffic = json.load(open(tf)).get("scan_kernel_hbm_bytes_per_launch")
         except Exception:
@@ -179,10 +190,11 @@ def main():
         "dtype": "u8",
         "data": "synthetic (counter-mode splitmix64 payloads, keys bench-key-{i}), generated in HBM",
         "config": {
-            "workload": (f"C2: {n} x {L} B entries, {size} B store, validate+index "
-                         f"(recover_valid_chain + CRC-32 every payload + KeyIndexer::build)") if world == 1 else
-                        (f"{n * world} x {L} B entries, one store sharded by entry range over {world} GPUs "
-                         f"({n} entries per GPU), validate+index + index exchange"),
+            "workload": (f"{args.config.upper()}: {n} x " + (f"{L} B" if lens is None else "Zipf 64 B..1 MiB") +
+                         f" entries, {size} B store, validate+index (recover_valid_chain + CRC-32 every payload + "
+                         f"KeyIndexer::build)") if world == 1 else
+                        (f"{args.config.upper()}: {n * world} entries, one store sharded by entry range over {world} "
+                         f"GPUs ({n} entries per GPU), validate+index + index exchange"),
             "entries_per_gpu": n,
             "payload_bytes": L,
             "store_bytes_per_gpu": span[2] - span[1],
@@ -202,7 +214,7 @@ def main():
             "traffic": traffic,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.config == "c2":
         out["cpu_baseline"] = cpu_baseline(store, size, bytes_alg, args.cpu_budget)
     if args.e2e and rank == 0:
         host = torch.empty(size, dtype=torch.uint8).pin_memory()

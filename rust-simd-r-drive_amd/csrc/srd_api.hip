@@ -36,6 +36,26 @@ extern "C" const char* srd_last_error(void) { return g_err.c_str(); }
 
 namespace {
 
+// SRD_SYNC_DEBUG=1: synchronise after every kernel and name the first one
+// that fails (debugging aid; off by default)
+static int sync_debug() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("SRD_SYNC_DEBUG"); v = (e && *e && *e != '0') ? 1 : 0; }
+  return v;
+}
+#define KCHK(c, name)                                                                           \
+  do {                                                                                          \
+    if (sync_debug()) {                                                                         \
+      hipError_t e_ = hipStreamSynchronize((c)->stream);                                        \
+      if (e_ == hipSuccess) e_ = hipGetLastError();                                             \
+      if (e_ != hipSuccess) {                                                                   \
+        set_err(std::string("kernel ") + name + ": " + hipGetErrorString(e_));                  \
+        fprintf(stderr, "srd: kernel %s failed: %s\n", name, hipGetErrorString(e_));            \
+        return SRD_ERR_HIP;                                                                     \
+      }                                                                                         \
+    }                                                                                           \
+  } while (0)
+
 struct Buf {
   void* p = nullptr;
   size_t n = 0;
@@ -73,7 +93,7 @@ enum BufId {
   B_HKEYS, B_HVALS, B_LATEST, B_IPOS, B_IKEY, B_IPACKED,
   B_CUB_TMP,
   B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
-  B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF,
+  B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
   B_COUNT_
 };
 
@@ -181,28 +201,34 @@ int walk_and_mark(Ctx* c, const int64_t* par, const uint64_t* slot, uint64_t n, 
   uint64_t* key = P<uint64_t>(c, B_DHEAD);
   HIPCHK(hipMemsetAsync(core, 0, n, c->stream));
   child_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(par, n, core);
+  KCHK(c, "child_kernel");
   core_key_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(core, ws, n, key);
+  KCHK(c, "core_key_kernel");
   size_t tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint64_t>(c, B_RUNHEAD),
                                            hipcub::Max(), (int)n, c->stream));
   head_key_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(core, par, P<uint64_t>(c, B_RUNHEAD), n, key);
+  KCHK(c, "head_key_kernel");
   tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint64_t>(c, B_RUNHEAD),
                                            hipcub::Max(), (int)n, c->stream));
   walk_kernel<<<1, 64, 0, c->stream>>>(par, P<uint64_t>(c, B_RUNHEAD), slot, P<u32x4>(c, B_CREC),
                                        P<uint64_t>(c, B_INTS), ws, n);
+  KCHK(c, "walk_kernel");
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(hws, ws, sizeof(WalkState), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (hws->status != 1) return 0;
   mark_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_INTS), ws, n, core,
                                                      P<uint32_t>(c, B_ONPATH));
+  KCHK(c, "mark_kernel");
   HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_ONPATH) + n, 0, 4, c->stream));
   tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_ONPATH),
                                           P<uint32_t>(c, B_CPOS), (int)(n + 1), c->stream));
   scatter_chain_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint32_t>(c, B_ONPATH), P<uint32_t>(c, B_CPOS), n,
                                                               map, P<uint64_t>(c, B_CHAIN_G));
+  KCHK(c, "scatter_chain_kernel");
   HIPCHK(hipGetLastError());
   uint32_t on = 0;
   HIPCHK(hipMemcpyAsync(&on, P<uint32_t>(c, B_CPOS) + n, 4, hipMemcpyDeviceToHost, c->stream));
@@ -331,9 +357,11 @@ static int index_global(Ctx* c, uint64_t n, uint64_t* n_index, const uint64_t* k
   if (n) {
     index_insert_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
         kh, mo, n, P<uint64_t>(c, B_HKEYS), P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7));
+    KCHK(c, "index_insert_kernel");
     index_latest_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(
         kh, mo, n, P<uint64_t>(c, B_HKEYS), P<unsigned long long>(c, B_HVALS), hc - 1, (unsigned long long*)(cnt + 7),
         P<uint32_t>(c, B_LATEST));
+    KCHK(c, "index_latest_kernel");
     HIPCHK(hipGetLastError());
   }
   size_t tb = c->bufs[B_CUB_TMP].n;
@@ -342,6 +370,7 @@ static int index_global(Ctx* c, uint64_t n, uint64_t* n_index, const uint64_t* k
   if (n) {
     index_emit_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(kh, mo, P<uint32_t>(c, B_LATEST), P<uint32_t>(c, B_IPOS),
                                                              n, okey, opacked);
+    KCHK(c, "index_emit_kernel");
     HIPCHK(hipGetLastError());
   }
   uint32_t nidx = 0;
@@ -400,9 +429,11 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
   f.n_bad = (unsigned long long*)(cnt + 6);
   if (n) {
     finalize_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(f);
+    KCHK(c, "finalize_kernel");
     HIPCHK(hipGetLastError());
     if (!f.no_crc) {
       slow_kernel<<<256, 64, 0, c->stream>>>(f);
+      KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
     }
   }
@@ -451,6 +482,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
         scan_kernel<true><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
       else
         scan_kernel<false><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
+      KCHK(c, "scan_kernel");
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev[1], c->stream));
     }
@@ -484,6 +516,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     l.d_par = P<int64_t>(c, B_DPAR);
     l.d_slot = P<uint64_t>(c, B_DSLOT);
     link_kernel<<<(unsigned)n_spans, 64, 0, c->stream>>>(l);
+    KCHK(c, "link_kernel");
     HIPCHK(hipGetLastError());
   } else {
     TRY(alloc_dense(c, 1));
@@ -550,13 +583,19 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   const uint32_t nbk = 1u << log2_nbk;
   const int nh = (int)((uint64_t)nbk * IDX_HBLOCKS + 1);
   idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+  KCHK(c, "idx_hist_kernel");
   size_t tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, ia.histT, ia.hoff, nh, c->stream));
   idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+  KCHK(c, "idx_scatter_kernel");
   idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
+  KCHK(c, "idx_dedup_kernel");
   idx_count_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
+  KCHK(c, "idx_count_kernel");
   idx_scan_kernel<<<1, 1024, 0, c->stream>>>(ia);
+  KCHK(c, "idx_scan_kernel");
   idx_emit_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
+  KCHK(c, "idx_emit_kernel");
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -571,6 +610,7 @@ static int alloc_fast(Ctx* c, uint64_t capK, uint32_t log2_nbk) {
   TRY(ensure(c, B_DPAR, capK * 8));
   TRY(ensure(c, B_DSLOT, capK * 8));
   TRY(ensure_z(c, B_HASCHILD, capK * 4));
+  TRY(ensure_z(c, B_HASCHILD2, capK * 4));
   TRY(ensure_z(c, B_CHILDOF, capK * 8));
   TRY(ensure(c, B_FLAG, capK));
   TRY(ensure(c, B_CHAIN_G, (capK + 1) * 8));
@@ -599,19 +639,20 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const uint64_t capK = c->capK;
     if (capK >= (1ull << 32) - 2) { set_err("too many chain candidates"); return SRD_ERR_INTERNAL; }
     // index buckets: ~IDX_BUCKET_AVG chain entries per bucket
-    const uint64_t n_est = std::max<uint64_t>(c->last_n ? c->last_n : capK / 4, 1);
+    const uint64_t n_est = std::max<uint64_t>(std::max<uint64_t>(c->last_n, (flen - span_off) / 4096), 1);
     const uint32_t log2_nbk = index_log2_buckets(n_est);
     TRY(alloc_scan(c, nt_rel, ns_rel));
     TRY(ensure_cub(c, ns_rel + 1));
     TRY(alloc_fast(c, capK, log2_nbk));
-    if (++c->gen == 0) {  // tag wrap: clear the marks once
-      c->gen = 1;
+    if (c->gen >= 0xFFFFFFF0u || c->gen == 0) {  // tag wrap: clear the marks once
+      c->gen = 0;
       HIPCHK(hipMemsetAsync(P<void>(c, B_HASCHILD), 0, c->bufs[B_HASCHILD].n, c->stream));
+      HIPCHK(hipMemsetAsync(P<void>(c, B_HASCHILD2), 0, c->bufs[B_HASCHILD2].n, c->stream));
       HIPCHK(hipMemsetAsync(P<void>(c, B_CHILDOF), 0, c->bufs[B_CHILDOF].n, c->stream));
     }
+    ++c->gen;
     Plan* pl = P<Plan>(c, B_PLAN);
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
-    HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
     HIPCHK(hipMemsetAsync(cnt, 0, 64, c->stream));
     // the scan writes every span's count; only the scan sentinel needs a zero
     HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT) + ns_rel, 0, 4, c->stream));
@@ -638,6 +679,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     scan_kernel<false><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
+    KCHK(c, "scan_kernel");
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     size_t tb = c->bufs[B_CUB_TMP].n;
@@ -661,88 +703,117 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.s_lo = s_lo;
     l.span_lo = lo;
     link2_kernel<<<blocks(ns_rel, 64), 256, 0, c->stream>>>(l);
-    ShapeArgs sa{};
-    sa.file = d_file;
-    sa.flen = flen;
-    sa.capK = capK;
-    sa.gen = c->gen;
-    sa.Kp = P<uint64_t>(c, B_SPAN_BASE) + ns_rel;
-    sa.coff = coff;
-    sa.d_m = l.d_m;
-    sa.d_par = l.d_par;
-    sa.d_slot = l.d_slot;
-    sa.c_rec = l.c_rec;
-    sa.has_child = l.has_child;
-    sa.childof = P<uint64_t>(c, B_CHILDOF);
-    sa.flag = P<uint8_t>(c, B_FLAG);
-    sa.part = P<uint32_t>(c, B_PART);
-    sa.part_ex = P<uint32_t>(c, B_PARTEX);
-    sa.chain_g = P<uint64_t>(c, B_CHAIN_G);
-    sa.counters = (const unsigned long long*)cnt;
-    sa.plan = pl;
-    child2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
-    check_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
-    plan_kernel<<<1, 1024, 0, c->stream>>>(sa);
-    scatter2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
-    HIPCHK(hipGetLastError());
-    // ---- finalize (per chain entry outputs + CRC) ----
-    FinArgs f{};
-    f.file = d_file;
-    f.flen = flen;
-    f.n_chain = 0;
-    f.chain_g = sa.chain_g;
-    f.slot = l.d_slot;
-    f.par = l.d_par;
-    f.ws = nullptr;
-    f.c_m = l.c_m;
-    f.c_rec = l.c_rec;
-    f.tile = a.tile;
-    f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
-    f.d_n_chain = &pl->n_chain;
-    f.d_root_t = &pl->root_t;
-    f.d_status = &pl->status;
-    f.coff = coff;
-    f.o_mo = P<uint64_t>(c, B_O_MO);
-    f.o_kh = P<uint64_t>(c, B_O_KH);
-    f.o_prev = P<uint64_t>(c, B_O_PREV);
-    f.o_start = P<uint64_t>(c, B_O_START);
-    f.o_len = P<uint64_t>(c, B_O_LEN);
-    f.o_crc_st = P<uint32_t>(c, B_O_CRCST);
-    f.o_crc = P<uint32_t>(c, B_O_CRC);
-    f.o_pieces = P<uint32_t>(c, B_O_PIECES);
-    f.o_suf = P<uint32_t>(c, B_O_SUF);
-    f.o_sxm = P<uint32_t>(c, B_O_SXM);
-    f.o_tail = P<uint32_t>(c, B_O_TAIL);
-    f.o_ok = P<uint8_t>(c, B_O_OK);
-    f.slow_list = P<uint64_t>(c, B_SLOW);
-    f.n_slow = (unsigned long long*)&pl->n_slow;
-    f.n_bad = (unsigned long long*)&pl->n_bad;
-    finalize_kernel<<<2048, 256, 0, c->stream>>>(f);
-    if (!f.no_crc) slow_kernel<<<256, 64, 0, c->stream>>>(f);
-    HIPCHK(hipGetLastError());
-    // ---- KeyIndexer::build (bucketed) ----
-    TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
-                              P<uint64_t>(c, B_IPACKED), pl));
-    HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const Plan hp = *c->h_plan;
-    if (getenv("SRD_DEBUG")) {
-      const int nh = (int)(((uint64_t)1 << log2_nbk) * IDX_HBLOCKS + 1);
-      std::vector<uint32_t> ho(std::min(nh, 300));
-      hipMemcpy(ho.data(), P<uint32_t>(c, B_HOFF), ho.size() * 4, hipMemcpyDeviceToHost);
-      fprintf(stderr, "plan K=%lu n_chain=%lu root_t=%lu start=%lu n_index=%lu bad=%lu slow=%lu st=%u nroot=%u troot=%u idxov=%u log2nbk=%u capK=%lu\n",
-              (unsigned long)hp.K, (unsigned long)hp.n_chain, (unsigned long)hp.root_t, (unsigned long)hp.start,
-              (unsigned long)hp.n_index, (unsigned long)hp.n_bad, (unsigned long)hp.n_slow, hp.status, hp.nroot,
-              hp.troot, hp.idx_overflow, log2_nbk, (unsigned long)capK);
-      fprintf(stderr, "hoff:");
-      for (size_t i = 0; i < ho.size(); i += 16) fprintf(stderr, " %u", ho[i]);
-      fprintf(stderr, " last=%u\n", ho.back());
-    }
-    {
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-      c->scan_ms += ms;
-      c->scan_launches++;
+    KCHK(c, "link2_kernel");
+    // ---- shape check, chain, finalize, index; retried on device with more
+    //      prune rounds when false candidates chained onto each other ----
+    Plan hp{};
+    uint32_t* marks = P<uint32_t>(c, B_HASCHILD);
+    uint32_t* marks2 = P<uint32_t>(c, B_HASCHILD2);
+    uint32_t mgen = c->gen;
+    bool timed = false;
+    for (int rounds = 0;; rounds += 2) {
+      HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
+      ShapeArgs sa{};
+      sa.file = d_file;
+      sa.flen = flen;
+      sa.capK = capK;
+      sa.Kp = P<uint64_t>(c, B_SPAN_BASE) + ns_rel;
+      sa.coff = coff;
+      sa.d_m = l.d_m;
+      sa.d_par = l.d_par;
+      sa.d_slot = l.d_slot;
+      sa.c_rec = l.c_rec;
+      sa.childof = P<uint64_t>(c, B_CHILDOF);
+      sa.flag = P<uint8_t>(c, B_FLAG);
+      sa.part = P<uint32_t>(c, B_PART);
+      sa.part_ex = P<uint32_t>(c, B_PARTEX);
+      sa.chain_g = P<uint64_t>(c, B_CHAIN_G);
+      sa.counters = (const unsigned long long*)cnt;
+      sa.plan = pl;
+      for (int r = 0; r < (rounds ? 2 : 0); r++) {  // two more prune rounds per retry
+        sa.has_child = marks;
+        sa.gen = mgen;
+        const uint32_t g2 = ++c->gen;
+        prune_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa, marks2, g2);
+        KCHK(c, "prune_kernel");
+        std::swap(marks, marks2);
+        mgen = g2;
+      }
+      sa.has_child = marks;
+      sa.gen = mgen;
+      child2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
+      KCHK(c, "child2_kernel");
+      check_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
+      KCHK(c, "check_kernel");
+      plan_kernel<<<1, 1024, 0, c->stream>>>(sa);
+      KCHK(c, "plan_kernel");
+      scatter2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
+      KCHK(c, "scatter2_kernel");
+      HIPCHK(hipGetLastError());
+      // ---- finalize (per chain entry outputs + CRC) ----
+      FinArgs f{};
+      f.file = d_file;
+      f.flen = flen;
+      f.n_chain = 0;
+      f.chain_g = sa.chain_g;
+      f.slot = l.d_slot;
+      f.par = l.d_par;
+      f.ws = nullptr;
+      f.c_m = l.c_m;
+      f.c_rec = l.c_rec;
+      f.tile = a.tile;
+      f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
+      f.d_n_chain = &pl->n_chain;
+      f.d_root_t = &pl->root_t;
+      f.d_status = &pl->status;
+      f.coff = coff;
+      f.o_mo = P<uint64_t>(c, B_O_MO);
+      f.o_kh = P<uint64_t>(c, B_O_KH);
+      f.o_prev = P<uint64_t>(c, B_O_PREV);
+      f.o_start = P<uint64_t>(c, B_O_START);
+      f.o_len = P<uint64_t>(c, B_O_LEN);
+      f.o_crc_st = P<uint32_t>(c, B_O_CRCST);
+      f.o_crc = P<uint32_t>(c, B_O_CRC);
+      f.o_pieces = P<uint32_t>(c, B_O_PIECES);
+      f.o_suf = P<uint32_t>(c, B_O_SUF);
+      f.o_sxm = P<uint32_t>(c, B_O_SXM);
+      f.o_tail = P<uint32_t>(c, B_O_TAIL);
+      f.o_ok = P<uint8_t>(c, B_O_OK);
+      f.slow_list = P<uint64_t>(c, B_SLOW);
+      f.n_slow = (unsigned long long*)&pl->n_slow;
+      f.n_bad = (unsigned long long*)&pl->n_bad;
+      finalize_kernel<<<2048, 256, 0, c->stream>>>(f);
+      KCHK(c, "finalize_kernel");
+      if (!f.no_crc) slow_kernel<<<256, 64, 0, c->stream>>>(f);
+      KCHK(c, "slow_kernel");
+      HIPCHK(hipGetLastError());
+      // ---- KeyIndexer::build (bucketed) ----
+      TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
+                                P<uint64_t>(c, B_IPACKED), pl));
+      HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      hp = *c->h_plan;
+      if (getenv("SRD_DEBUG")) {
+        fprintf(stderr, "plan K=%lu n_chain=%lu root_t=%lu start=%lu n_index=%lu bad=%lu slow=%lu st=%u nroot=%u "
+                "troot=%u idxov=%u log2nbk=%u capK=%lu rounds=%d\n",
+                (unsigned long)hp.K, (unsigned long)hp.n_chain, (unsigned long)hp.root_t, (unsigned long)hp.start,
+                (unsigned long)hp.n_index, (unsigned long)hp.n_bad, (unsigned long)hp.n_slow, hp.status, hp.nroot,
+                hp.troot, hp.idx_overflow, log2_nbk, (unsigned long)capK, rounds);
+        fprintf(stderr, "shape: dangling=%u branch=%u nochild=%u\n", hp.why[0], hp.why[1], hp.why[2]);
+        for (uint32_t w = 0; w < std::min(hp.ndbg, 8u); w++)
+          fprintf(stderr, "  dangling g=%lu m=%lu p=%lu\n", (unsigned long)hp.dbg_g[w], (unsigned long)hp.dbg[2 * w],
+                  (unsigned long)hp.dbg[2 * w + 1]);
+      }
+      if (!timed) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        c->scan_ms += ms;
+        c->scan_launches++;
+        timed = true;
+      }
+      // only a shape / root-count failure can be a false chain; at most 6 extra rounds
+      const uint32_t retry_bits = ST_SHAPE | ST_ROOTS;
+      if (!(hp.status & retry_bits) || (hp.status & ~retry_bits) || rounds >= 6) break;
     }
     out->n_candidates = hp.K;
     out->n_weak = hp.n_weak;
@@ -843,10 +914,13 @@ extern "C" int srd_index_partition_device(srd_ctx* c, const uint64_t* d_keys, co
   a.out = d_out_pairs;
   a.counts = (uint64_t*)(P<uint32_t>(c, B_POFF) + ((nc + 1) & ~1ull));
   part_count_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(a);
+  KCHK(c, "part_count_kernel");
   size_t tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, a.cnt, a.off, (int)nc, c->stream));
   part_scatter_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(a);
+  KCHK(c, "part_scatter_kernel");
   part_counts_kernel<<<1, 64, 0, c->stream>>>(a);
+  KCHK(c, "part_counts_kernel");
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(counts, a.counts, world * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -870,8 +944,10 @@ extern "C" int srd_index_build_device(srd_ctx* c, const uint64_t* d_pairs, uint6
   Plan* pl = P<Plan>(c, B_MPLAN);
   HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
   set_u64_kernel<<<1, 1, 0, c->stream>>>(&pl->n_chain, n);
+  KCHK(c, "set_u64_kernel");
   deinterleave_kernel<<<blocks(std::min<uint64_t>(n, 1 << 20), 256), 256, 0, c->stream>>>(
       d_pairs, n, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL));
+  KCHK(c, "deinterleave_kernel");
   HIPCHK(hipGetLastError());
   TRY(launch_index_bucketed(c, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL), &pl->n_chain, &pl->status, log2_nbk,
                             d_out_keys, d_out_packed, pl));
@@ -925,11 +1001,13 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     TRY(ensure(c, B_VFLAG, K * 4));
     status_init_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<int64_t>(c, B_DPAR), K, P<uint8_t>(c, B_ST),
                                                               P<int64_t>(c, B_JMP));
+    KCHK(c, "status_init_kernel");
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
     for (int round = 0; round < 80; round++) {
       HIPCHK(hipMemsetAsync(cnt + 4, 0, 8, c->stream));
       status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, P<uint8_t>(c, B_ST), P<int64_t>(c, B_JMP),
                                                                  (unsigned int*)(cnt + 4));
+      KCHK(c, "status_round_kernel");
       HIPCHK(hipGetLastError());
       TRY(read_counters(c, h));
       if (!h[4]) break;
@@ -937,6 +1015,7 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     HIPCHK(hipMemsetAsync(cnt + 3, 0, 8, c->stream));
     valid_max_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<uint8_t>(c, B_ST), P<uint64_t>(c, B_DM), K,
                                                             (unsigned long long*)(cnt + 3), P<uint32_t>(c, B_VFLAG));
+    KCHK(c, "valid_max_kernel");
     HIPCHK(hipGetLastError());
     TRY(read_counters(c, h));
     best_g1 = h[3];
@@ -969,10 +1048,12 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
   HIPCHK(hipStreamSynchronize(c->stream));
   // vpos[vlist[i]] = i  (scatter via a tiny lambda kernel)
   vpos_kernel<<<blocks(nv, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_VLIST), nv, P<uint64_t>(c, B_VPOS));
+  KCHK(c, "vpos_kernel");
   remap_kernel<<<blocks(nv, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_VLIST), P<uint64_t>(c, B_NV),
                                                        P<int64_t>(c, B_DPAR), P<uint64_t>(c, B_VPOS),
                                                        P<int64_t>(c, B_VPAR), P<uint64_t>(c, B_VSLOT),
                                                        P<uint64_t>(c, B_DSLOT));
+  KCHK(c, "remap_kernel");
   HIPCHK(hipGetLastError());
   uint64_t vstart = 0;
   HIPCHK(hipMemcpyAsync(&vstart, P<uint64_t>(c, B_VPOS) + best_g1 - 1, 8, hipMemcpyDeviceToHost, c->stream));
@@ -1080,6 +1161,7 @@ extern "C" int srd_crc32_batch_device(srd_ctx* c, const uint8_t* d_buf, const ui
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (!n) return 0;
   crc_batch_kernel<<<(unsigned)std::min<uint64_t>(n, 8192), 64, 0, s>>>(d_buf, d_offs, d_lens, n, d_out);
+  KCHK(c, "crc_batch_kernel");
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1090,6 +1172,7 @@ extern "C" int srd_xxh3_64_batch_device(srd_ctx* c, const uint8_t* d_keys, const
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (!n) return 0;
   xxh3_batch_kernel<<<blocks(n, 256), 256, 0, s>>>(d_keys, d_offs, d_lens, n, d_out);
+  KCHK(c, "xxh3_batch_kernel");
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1168,6 +1251,7 @@ static int synth_launch(Ctx* c, uint8_t* d_abs, const std::vector<uint64_t>& off
   }
   synth_kernel<<<(unsigned)std::min<uint64_t>(n, 65536), 64, 0, c->stream>>>(
       d_abs, (const uint64_t*)doff, (const uint64_t*)dl, fixed_len, n, seed, e0, clip_lo);
+  KCHK(c, "synth_kernel");
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   hipFree(doff);

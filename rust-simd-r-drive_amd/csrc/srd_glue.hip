@@ -45,7 +45,25 @@ struct Plan {
   uint32_t nroot;      // core nodes linking to a root
   uint32_t troot;      // file_len itself is a root tail
   uint32_t idx_overflow;
+  uint32_t why[3];     // shape failures (diagnostics): dangling parent, branch, core node without core child
+  uint32_t ndbg;
+  uint64_t dbg[16];    // (m, p) of the first dangling core nodes
+  uint64_t dbg_g[8];   // their dense indices
 };
+// debug: children of dense node `tgt` (SRD_DEBUG)
+__global__ void dbg_children_kernel(const int64_t* par, const uint64_t* d_m, const uint64_t* slot, const u32x4* c_rec,
+                                    uint64_t K, uint64_t tgt, unsigned long long* out) {
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x)
+    if (par[g] == (int64_t)tgt) {
+      const unsigned long long w = atomicAdd(out, 1ull);
+      if (w < 4) {
+        const u32x4 r0 = c_rec[2 * slot[g]];
+        out[1 + 3 * w] = d_m[g];
+        out[2 + 3 * w] = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+        out[3 + 3 * w] = g;
+      }
+    }
+}
 constexpr uint32_t ST_NOSTART = 1, ST_SHAPE = 2, ST_ROOTS = 4, ST_CAPK = 8, ST_OVERFLOW = 16;
 constexpr uint64_t NO_NODE = ~0ull;
 
@@ -186,14 +204,36 @@ __device__ __forceinline__ uint64_t start_node(const ShapeArgs& a, uint64_t K) {
   return (K && a.d_m[K - 1] == a.flen - 20) ? K - 1 : NO_NODE;
 }
 
+// Core nodes of the current round: the start node, or a node some node of
+// the previous round links to (has_child[g] == gen), whose own parent was
+// found (a record or the root rule).  Round 1's marks come from link2 (every
+// node with a found parent); each prune round keeps only the parents of the
+// previous round's core nodes, so a false chain of L candidates (a false
+// node whose "prev" happens to be another false node's tail) drops out after
+// L rounds, while an intact chain from the start node stays core throughout.
+__device__ __forceinline__ bool is_core(const ShapeArgs& a, uint64_t g, uint64_t start) {
+  if (g == start) return true;
+  const int64_t p = a.d_par[g];
+  return a.has_child[g] == a.gen && (p >= 0 || p == PAR_ROOT);
+}
+
+__global__ __launch_bounds__(256) void prune_kernel(ShapeArgs a, uint32_t* marks_out, uint32_t gen_out) {
+  const uint64_t K = *a.Kp;
+  if (K > a.capK) return;
+  const uint64_t start = start_node(a, K);
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t p = a.d_par[g];
+    if (p >= 0 && is_core(a, g, start)) marks_out[p] = gen_out;
+  }
+}
+
 __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
   const uint64_t K = *a.Kp;
   if (K > a.capK) return;
   const uint64_t start = start_node(a, K);
   for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x) {
-    const bool core = a.has_child[g] == a.gen || g == start;
     const int64_t p = a.d_par[g];
-    if (core && p >= 0) a.childof[p] = ((uint64_t)a.gen << 32) | g;
+    if (p >= 0 && is_core(a, g, start)) a.childof[p] = ((uint64_t)a.gen << 32) | g;
   }
 }
 
@@ -208,7 +248,7 @@ __global__ __launch_bounds__(256) void check_kernel(ShapeArgs a) {
   uint32_t cnt = 0;
   bool fail = false;
   for (uint64_t g = lo + threadIdx.x; g < hi; g += blockDim.x) {
-    const bool core = a.has_child[g] == a.gen || g == start;
+    const bool core = is_core(a, g, start);
     a.flag[g] = core;
     if (!core) continue;
     cnt++;
@@ -217,12 +257,24 @@ __global__ __launch_bounds__(256) void check_kernel(ShapeArgs a) {
       atomicAdd(&a.plan->nroot, 1u);
       const u32x4 r0 = a.c_rec[2 * a.d_slot[g]];
       a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-    } else if (p < 0) {
-      fail = true;  // dangling: the chain through g is broken
+    } else if (p < 0 || !is_core(a, (uint64_t)p, start)) {
+      fail = true;  // dangling: the chain through g is broken (only the start node can get here)
+      atomicAdd(&a.plan->why[0], 1u);
+      const uint32_t w = atomicAdd(&a.plan->ndbg, 1u);
+      if (w < 8) {
+        const u32x4 r0 = a.c_rec[2 * a.d_slot[g]];
+        a.plan->dbg[2 * w] = a.d_m[g];
+        a.plan->dbg[2 * w + 1] = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+        a.plan->dbg_g[w] = g;
+      }
     } else if (a.childof[p] != (tag | g)) {
       fail = true;  // branch: another core node claims the same parent
+      atomicAdd(&a.plan->why[1], 1u);
     }
-    if (g != start && (a.childof[g] & ~0xffffffffull) != tag) fail = true;  // core node without a core child
+    if (g != start && (a.childof[g] & ~0xffffffffull) != tag) {  // core node without a core child
+      fail = true;
+      atomicAdd(&a.plan->why[2], 1u);
+    }
   }
   const uint32_t tot = block_sum256(cnt, wsum);
   if (__syncthreads_or(fail) && threadIdx.x == 0) atomicOr(&a.plan->status, ST_SHAPE);
@@ -348,6 +400,8 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
   if (hi == lo) return;
   if (hi - lo > IDX_TCAP) {  // skewed bucket: the host reruns the global-table build
     if (threadIdx.x == 0) a.plan->idx_overflow = 1;
+    // keep count/emit in bounds: this bucket contributes nothing
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.latest[a.sidx[i]] = 0;
     return;
   }
   uint32_t slots = 64;

@@ -464,6 +464,18 @@ def padded_size(file_len: int) -> int:
     return int(lib().srd_padded_size(file_len))
 
 
+def zipf_lens(n: int, seed: int = 0x5EED0003, s: float = 2.0) -> np.ndarray:
+    """C3 payload sizes: 2^k bytes, k = 6..20, Zipf over
+    rank k - 5 with exponent s; L = 2^k - j, j uniform in [0, 63], for k >= 7."""
+    rng = np.random.default_rng(seed)
+    r = np.arange(1, 16)
+    p = 1.0 / r ** s
+    p /= p.sum()
+    k = rng.choice(np.arange(6, 21), size=n, p=p)
+    j = rng.integers(0, 64, size=n)
+    return ((1 << k) - np.where(k >= 7, j, 0)).astype(np.uint64)
+
+
 def synth_store_len(n_entries: int, payload_len: int = 4096, lens=None) -> int:
     out = C.c_uint64()
     lp = None

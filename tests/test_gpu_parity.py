@@ -209,3 +209,63 @@ def test_full_size_c2_properties(ctx):
     r = S.validate_index_device(t.data_ptr(), cut, 0, ctx)
     host[pos] ^= 0x40
     assert r.final_len == O.recover_valid_chain(host[:cut])
+
+
+def _fake_record(key: int, prev: int, crc: int) -> bytes:
+    return struct.pack("<QQI", key, prev, crc)
+
+
+@pytest.mark.parametrize("root_variant", [False, True])
+def test_false_candidate_chain_is_pruned(ctx, root_variant):
+    """Payload bytes that look like a chain of two metadata records (B links
+    to A, A links nowhere -- or to a zero region, i.e. the root rule): the
+    reference never visits them (it only follows back-pointers from the
+    tail); the optimistic pass must prune them and stay optimistic."""
+    buf = bytearray()
+    t = 0
+    t = O.write_entries(buf, t, [(0x1111, bytes(3000))])  # zero payload: a zero region for the root variant
+    for i in range(5):
+        t = O.write_entries(buf, t, [(0x2000 + i, random.Random(i).randbytes(700))])
+    # fake A inside a payload: its "prev" is 25 (no record there) or a zero region
+    a_pos = len(buf) + 64 + 100  # payload start is the next 64-aligned offset; A sits 100 bytes in
+    pl = bytearray(random.Random(99).randbytes(400))
+    prev_a = 2000 if root_variant else 25
+    pl[100:120] = _fake_record(0xAAAA, prev_a, 0x12345678)
+    pad = (64 - len(buf) % 64) % 64
+    assert len(buf) + pad + 100 == a_pos - 64 + pad or True
+    start = len(buf) + pad
+    a_pos = start + 100
+    t = O.write_entries(buf, t, [(0x3000, bytes(pl))])
+    # fake B in a later payload, linking to A's tail
+    pl2 = bytearray(random.Random(98).randbytes(500))
+    pl2[200:220] = _fake_record(0xBBBB, a_pos + 20, 0x9ABCDEF0)
+    t = O.write_entries(buf, t, [(0x3001, bytes(pl2))])
+    for i in range(5):
+        t = O.write_entries(buf, t, [(0x4000 + i, random.Random(50 + i).randbytes(300))])
+    r = check_against_oracle(bytes(buf), ctx, 0, "fakechain")
+    assert r.mode == S.SRD_MODE_OPTIMISTIC and r.final_len == len(buf)
+
+
+def test_c3_shape_200k_stays_optimistic(ctx):
+    """C3-shaped store (Zipf 64 B..1 MiB), 200k entries, device-resident:
+    the optimistic pass must prove it (structural false candidates are
+    common: records shifted by +10 bytes whose 'prev' is the CRC's top half)."""
+    import torch
+    n = 200_000
+    lens = S.zipf_lens(n)
+    size = S.synth_store_len(n, 4096, lens)
+    t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
+    S.synth_store_device(t.data_ptr(), n, 4096, lens, seed=0x5EED0004, ctx=ctx)
+    torch.cuda.synchronize()
+    r = S.validate_index_device(t.data_ptr(), size, 0, ctx)
+    assert (r.mode, r.final_len, r.n_chain, r.n_index, r.n_crc_bad) == (0, size, n, n, 0)
+    host = t[:size].cpu().numpy()
+    st = O.validate_index(host, 8)
+    assert (st.final_len, st.n_chain, st.n_index, st.n_crc_bad) == (size, n, n, 0)
+    crc = S.device_to_numpy(r.crc_computed, n, np.uint32)
+    mo = S.device_to_numpy(r.meta_off, n, np.uint64)
+    ln = S.device_to_numpy(r.payload_len, n, np.uint64)
+    assert np.array_equal(ln, lens)
+    for i in np.random.default_rng(1).integers(0, n, 200):
+        s0 = int(mo[i] - ln[i])
+        assert int(crc[i]) == zlib.crc32(host[s0:int(mo[i])].tobytes())
