@@ -144,6 +144,8 @@ int upload_tables() {
   memcpy(t.winit, g_host_tabs.winit, sizeof t.winit);
   memcpy(t.zero_crc, g_host_tabs.zero_crc, sizeof t.zero_crc);
   t.x32768 = g_host_tabs.x32768;
+  t.xtile[0] = kX0;
+  for (int e = 1; e <= 64; e++) t.xtile[e] = mulp(g_host_tabs.x32768, t.xtile[e - 1]);
   memcpy(t.pow8, g_host_tabs.pow8, sizeof t.pow8);
   memcpy(t.invpow, g_host_tabs.invpow, sizeof t.invpow);
   for (int pos = 0; pos < 8; pos++)
@@ -432,7 +434,7 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
     KCHK(c, "finalize_kernel");
     HIPCHK(hipGetLastError());
     if (!f.no_crc) {
-      slow_kernel<<<256, 64, 0, c->stream>>>(f);
+      slow_kernel<<<4096, 64, 0, c->stream>>>(f);
       KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
     }
@@ -784,7 +786,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.n_bad = (unsigned long long*)&pl->n_bad;
       finalize_kernel<<<2048, 256, 0, c->stream>>>(f);
       KCHK(c, "finalize_kernel");
-      if (!f.no_crc) slow_kernel<<<256, 64, 0, c->stream>>>(f);
+      if (!f.no_crc) slow_kernel<<<4096, 64, 0, c->stream>>>(f);
       KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
       // ---- KeyIndexer::build (bucketed) ----

@@ -71,6 +71,7 @@ struct DevTables {
   uint32_t m16k[4][256];           // v -> v * x^16384 byte tables
   uint32_t m128[4][256];
   uint32_t m256[4][256];
+  uint32_t xtile[65];              // X^e, X = x^32768 (one tile), e = 0..64
 };
 __device__ DevTables g_tabs;
 
@@ -788,6 +789,7 @@ __device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint
   return ~(mulp(g_tabs.invpow[dd], y) ^ tail);
 }
 
+constexpr uint64_t LONG_TILES = 4;  // whole tiles a finalize thread combines serially
 __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t);
 __global__ void finalize_kernel(FinArgs a) {
   uint64_t n = a.n_chain, root_t = 0;
@@ -862,7 +864,9 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
   }
   if (!(pieces & 4)) tail = tail_crc(a.file, mo);  // re-read the partial last line
   const bool need_long = len >= 64;
-  if (!need_long || ((pieces & 1) && (pieces & 2))) {
+  // entries spanning many whole tiles combine them with one wave (slow_kernel)
+  const bool many_tiles = need_long && mo / TILE > start / TILE + 1 + LONG_TILES;
+  if (!need_long || ((pieces & 1) && (pieces & 2) && !many_tiles)) {
     const uint32_t crc = crc_from_pieces(start, mo, suf, sxm, tail, a.tile);
     a.o_crc[c] = crc;
     a.o_ok[c] = crc == crc_st;
@@ -904,7 +908,53 @@ __device__ uint32_t tile_probe_sx(const uint8_t* file, uint64_t flen, uint64_t k
   return __shfl(sx, (int)j);
 }
 
-// one wave per slow entry (a piece of the combine was not recorded)
+// x^(8n) for any n (binary exponentiation over pow8[k] = x^(8*2^k))
+__device__ __forceinline__ uint32_t xpow8_dev(uint64_t n) {
+  uint32_t r = kX0;
+  for (int k = 0; n; k++, n >>= 1)
+    if (n & 1) r = mulp(g_tabs.pow8[k], r);
+  return r;
+}
+__device__ __forceinline__ uint32_t xpow8_any(uint64_t n) { return xpow8_dev(n); }
+
+// crc_from_pieces with the whole tiles between the start tile k0 and the
+// metadata tile k1 combined by the 64 lanes of the calling wave: lane l
+// Horner-combines tiles k0+1+l, +65+l, ... with X^64 steps, weights its sum by
+// X^(distance of its last tile to tile k1-1), and the wave XOR-reduces.
+__device__ uint32_t crc_from_pieces_wave(uint64_t s, uint64_t m, uint32_t suf, uint32_t sxm, uint32_t tail,
+                                         const uint32_t* tile) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t len = m - s;
+  if (len < 64) return tail ^ g_tabs.zero_crc[len];
+  const uint64_t k0 = s / TILE, k1 = m / TILE;
+  const uint32_t j0 = (uint32_t)((s % TILE) / 64);
+  uint32_t acc = suf ^ g_tabs.winit[j0];
+  uint32_t y;
+  if (k0 == k1) {
+    y = acc ^ sxm;
+  } else {
+    const uint64_t n = k1 - k0 - 1;  // whole tiles between
+    uint32_t h = 0;
+    uint64_t jl = 0;
+    bool any = false;
+    for (uint64_t j = lane; j < n; j += 64) {
+      h = mulp(g_tabs.xtile[64], h) ^ tile_T(tile, k0 + 1 + j);
+      jl = j;
+      any = true;
+    }
+    uint32_t v = any ? mulp(g_tabs.xtile[n - 1 - jl], h) : 0u;  // n-1-jl < 64
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+    // acc * X^n ^ mid, then one more tile step into k1
+    const uint32_t xn = xpow8_any(n * (uint64_t)TILE);
+    acc = mulp(xn, acc) ^ v;
+    y = mulp(g_tabs.x32768, acc) ^ tile_T(tile, k1) ^ sxm;
+  }
+  const uint64_t dd = (k1 + 1) * TILE - m;
+  return ~(mulp(g_tabs.invpow[dd], y) ^ tail);
+}
+
+// one wave per slow entry (a piece of the combine was not recorded, or the
+// entry spans more than LONG_TILES whole tiles)
 __global__ __launch_bounds__(64) void slow_kernel(FinArgs a) {
   __shared__ uint32_t tab[1024];
   const unsigned long long ns = *a.n_slow;
@@ -917,8 +967,8 @@ __global__ __launch_bounds__(64) void slow_kernel(FinArgs a) {
     uint32_t pieces = a.o_pieces[c], suf = a.o_suf[c], sxm = a.o_sxm[c], tail = a.o_tail[c];
     if (!(pieces & 1)) suf = tile_probe_sx(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64), tab);
     if (!(pieces & 2)) sxm = tile_probe_sx(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64), tab);
+    const uint32_t crc = crc_from_pieces_wave(s, m, suf, sxm, tail, a.tile);
     if ((threadIdx.x & 63) == 0) {
-      const uint32_t crc = crc_from_pieces(s, m, suf, sxm, tail, a.tile);
       a.o_crc[c] = crc;
       a.o_ok[c] = crc == a.o_crc_st[c];
       if (crc != a.o_crc_st[c]) atomicAdd(a.n_bad, 1ull);
@@ -974,12 +1024,6 @@ __global__ void index_emit_kernel(const uint64_t* kh, const uint64_t* mo, const 
 // --------------------------------------------------------------------------
 // batch digests (compute_checksum / compute_hash_batch)
 // --------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t xpow8_dev(uint64_t n) {
-  uint32_t r = kX0;
-  for (int k = 0; n; k++, n >>= 1)
-    if (n & 1) r = mulp(g_tabs.pow8[k], r);
-  return r;
-}
 
 // one wave per range; range bytes may have any alignment
 __global__ __launch_bounds__(64) void crc_batch_kernel(const uint8_t* buf, const uint64_t* offs,
