@@ -341,6 +341,12 @@ static int alloc_hash(Ctx* c, uint64_t n) {
   return 0;
 }
 
+static bool index_global_env() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("SRD_INDEX_GLOBAL"); v = (e && *e && *e != '0') ? 1 : 0; }
+  return v;
+}
+
 // KeyIndexer::build over n (key_hash, meta_off) pairs in file order with one
 // global open-addressing table (device-wide atomics); syncs for the count.
 // Default pairs: the chain in B_O_KH / B_O_MO -> B_IKEY / B_IPACKED.
@@ -434,7 +440,7 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
     KCHK(c, "finalize_kernel");
     HIPCHK(hipGetLastError());
     if (!f.no_crc) {
-      slow_kernel<<<4096, 64, 0, c->stream>>>(f);
+      slow_kernel<<<1024, 64, 0, c->stream>>>(f);
       KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
     }
@@ -594,8 +600,6 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   KCHK(c, "idx_dedup_kernel");
   idx_count_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
   KCHK(c, "idx_count_kernel");
-  idx_scan_kernel<<<1, 1024, 0, c->stream>>>(ia);
-  KCHK(c, "idx_scan_kernel");
   idx_emit_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
   KCHK(c, "idx_emit_kernel");
   HIPCHK(hipGetLastError());
@@ -747,10 +751,8 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       KCHK(c, "child2_kernel");
       check_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
       KCHK(c, "check_kernel");
-      plan_kernel<<<1, 1024, 0, c->stream>>>(sa);
-      KCHK(c, "plan_kernel");
-      scatter2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
-      KCHK(c, "scatter2_kernel");
+      scatter_plan_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
+      KCHK(c, "scatter_plan_kernel");
       HIPCHK(hipGetLastError());
       // ---- finalize (per chain entry outputs + CRC) ----
       FinArgs f{};
@@ -786,12 +788,13 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.n_bad = (unsigned long long*)&pl->n_bad;
       finalize_kernel<<<2048, 256, 0, c->stream>>>(f);
       KCHK(c, "finalize_kernel");
-      if (!f.no_crc) slow_kernel<<<4096, 64, 0, c->stream>>>(f);
+      if (!f.no_crc) slow_kernel<<<1024, 64, 0, c->stream>>>(f);
       KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
-      // ---- KeyIndexer::build (bucketed) ----
-      TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
-                                P<uint64_t>(c, B_IPACKED), pl));
+      // ---- KeyIndexer::build (bucketed; SRD_INDEX_GLOBAL=1: one global table, timing experiments) ----
+      if (!index_global_env())
+        TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
+                                  P<uint64_t>(c, B_IPACKED), pl));
       HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       hp = *c->h_plan;
@@ -834,7 +837,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     out->n_crc_bad = hp.n_bad;
     out->n_index = hp.n_index;
     c->last_n = hp.n_chain;
-    if (hp.idx_overflow) TRY(index_global(c, hp.n_chain, &out->n_index));
+    if (hp.idx_overflow || index_global_env()) TRY(index_global(c, hp.n_chain, &out->n_index));
     set_out_ptrs(c, out);
     *done = true;
     return 0;

@@ -107,6 +107,20 @@ __device__ __forceinline__ void chunk_of(uint64_t n, uint64_t* lo, uint64_t* hi)
   *hi = min(n, *lo + ch);
 }
 
+// sum of part[0 .. blockIdx.x) (exclusive prefix of this block) and of all
+// np partials, by every block itself (np <= 1024; replaces a one-block scan launch)
+__device__ __forceinline__ void block_prefix(const uint32_t* part, uint32_t np, uint32_t* wsum, uint64_t* before,
+                                             uint64_t* total) {
+  uint32_t b = 0, t = 0;
+  for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+    const uint32_t v = part[i];
+    t += v;
+    b += i < blockIdx.x ? v : 0u;
+  }
+  *before = block_sum256(b, wsum);
+  *total = block_sum256(t, wsum);
+}
+
 // exclusive scan of up to 1024 partials with one 1024-thread block
 __device__ uint64_t block_scan_partials(const uint32_t* part, uint32_t np, uint32_t* part_ex) {
   __shared__ uint64_t s[1024];
@@ -281,46 +295,48 @@ __global__ __launch_bounds__(256) void check_kernel(ShapeArgs a) {
   if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
 }
 
-// one block of 1024 threads
-__global__ __launch_bounds__(1024) void plan_kernel(ShapeArgs a) {
+// The plan (every block decides it from the same inputs; block 0 publishes
+// it) fused with the chain scatter: chain_g[coff + rank] = record slot of
+// core node g, in file order.
+__global__ __launch_bounds__(256) void scatter_plan_kernel(ShapeArgs a) {
+  __shared__ uint32_t wsum[4];
   const uint64_t K = *a.Kp;
   const bool capk = K > a.capK;
-  const uint64_t total = block_scan_partials(a.part, capk ? 0u : (uint32_t)GLUE_BLOCKS, a.part_ex);
-  if (threadIdx.x) return;
+  uint64_t before = 0, total = 0;
+  block_prefix(a.part, capk ? 0u : (uint32_t)GLUE_BLOCKS, wsum, &before, &total);
   Plan* pl = a.plan;
-  uint32_t st = pl->status;
-  pl->K = K;
-  pl->max_root = a.counters[0];
-  pl->n_weak = a.counters[1];
-  pl->overflow = a.counters[2];
+  uint32_t st = pl->status;  // check_kernel's shape bits
   // whole file only: file_len is itself a root tail (prev 0); flen >= 21 here
   const bool troot = a.coff && ld_u64_unaligned(a.file, a.flen - 12) == 0;
-  pl->troot = troot;
-  if (troot) {  // file_len is itself a root tail: chain = that one entry
-    pl->status = 0;
-    pl->n_chain = 1;
-    pl->root_t = a.flen;
-    pl->chain_core = 0;
-    return;
-  }
-  if (capk) { st |= ST_CAPK; pl->cap_need = K; }
+  if (capk) st |= ST_CAPK;
   if (a.counters[2]) st |= ST_OVERFLOW;
   const uint64_t start = capk ? NO_NODE : start_node(a, K);
-  pl->start = start;
   if (start == NO_NODE) st |= ST_NOSTART;
   if (pl->nroot != 1) st |= ST_ROOTS;
-  pl->status = st;
-  pl->chain_core = total;
-  pl->n_chain = st ? 0 : a.coff + total;
-}
-
-__global__ __launch_bounds__(256) void scatter2_kernel(ShapeArgs a) {
-  __shared__ uint32_t wsum[4];
-  if (a.plan->status || a.plan->troot) return;
-  const uint64_t K = *a.Kp;
+  __syncthreads();  // every block has read pl->status / nroot before block 0 rewrites them
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    pl->K = K;
+    pl->max_root = a.counters[0];
+    pl->n_weak = a.counters[1];
+    pl->overflow = a.counters[2];
+    pl->troot = troot;
+    if (troot) {  // file_len is itself a root tail: chain = that one entry
+      pl->status = 0;
+      pl->n_chain = 1;
+      pl->root_t = a.flen;
+      pl->chain_core = 0;
+    } else {
+      if (capk) pl->cap_need = K;
+      pl->start = start;
+      pl->status = st;
+      pl->chain_core = total;
+      pl->n_chain = st ? 0 : a.coff + total;
+    }
+  }
+  if (st || troot) return;
   uint64_t lo, hi;
   chunk_of(K, &lo, &hi);
-  uint64_t run = a.coff + (uint64_t)a.part_ex[blockIdx.x];
+  uint64_t run = a.coff + before;
   for (uint64_t base = lo; base < hi; base += blockDim.x) {
     const uint64_t g = base + threadIdx.x;
     const bool f = g < hi && a.flag[g];
@@ -446,16 +462,15 @@ __global__ __launch_bounds__(256) void idx_count_kernel(IdxArgs a) {
   if (threadIdx.x == 0) a.part[blockIdx.x] = t;
 }
 
-__global__ __launch_bounds__(1024) void idx_scan_kernel(IdxArgs a) {
-  const uint64_t total = block_scan_partials(a.part, GLUE_BLOCKS, a.part_ex);
-  if (threadIdx.x == 0) a.plan->n_index = total;
-}
 
 __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
   __shared__ uint32_t wsum[4];
+  uint64_t before = 0, total = 0;
+  block_prefix(a.part, GLUE_BLOCKS, wsum, &before, &total);
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.plan->n_index = total;
   uint64_t lo, hi;
   chunk_of(idx_n(a), &lo, &hi);
-  uint64_t run = a.part_ex[blockIdx.x];
+  uint64_t run = before;
   for (uint64_t base = lo; base < hi; base += blockDim.x) {
     const uint64_t c = base + threadIdx.x;
     const bool f = c < hi && a.latest[c];
