@@ -688,6 +688,17 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     KCHK(c, "scan_kernel");
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
+#ifdef SRD_ABLATE_NOLOAD
+    if (a.ablate & (16 | 256)) {  // timing experiment only (16: no HBM loads, 256: stop after the scan)
+      HIPCHK(hipEventSynchronize(c->ev[1]));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+      c->scan_ms += ms;
+      c->scan_launches++;
+      set_err("ablate 16: scan only");
+      return SRD_ERR_INTERNAL;
+    }
+#endif
     size_t tb = c->bufs[B_CUB_TMP].n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_SPAN_COUNT),
                                             P<uint64_t>(c, B_SPAN_BASE), (int)(ns_rel + 1), c->stream));

@@ -301,11 +301,21 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   if (k0 >= k1) return;
 
   uint32_t count = 0;
+  // store batching (registers, flushed with few wide stores): per-tile values
+  // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
+  uint32_t tacc = 0, scnt = 0;
+  uint32_t rq[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) rq[i] = 0;
+  uint64_t rvalid = 0;  // wave-uniform: record slots buffered in rq
 
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
   // (no loads under divergent/uniform branches, so the compiler's vmcnt
   // waits never have to drain the prefetch ring).
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
+#ifdef SRD_ABLATE_NOLOAD
+    if (a.ablate & 16) k = k0;  // timing experiment: compute-only (re-reads one L2-resident tile)
+#endif
     const u32x4* q = (const u32x4*)(file + k * (uint64_t)TILE + 64ull * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -344,24 +354,64 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
   }
 
-  auto process = [&](uint64_t k, uint32_t (&d)[16], const uint32_t (&nx)[16]) {
+  // first 8 bytes of tile k+1 (line 63's window) by a SCALAR load: the slow
+  // loop must not touch a register of the vector prefetch ring, or the
+  // compiler drains the whole ring (vmcnt(0)) in front of it
+  auto next_head = [&](uint64_t k, uint32_t* n0, uint32_t* n1) {
+    const __attribute__((address_space(4))) uint32_t* q =
+        (const __attribute__((address_space(4))) uint32_t*)(file + (k + 1) * (uint64_t)TILE);
+    *n0 = q[0];
+    *n1 = q[1];
+  };
+
+  // TAIL (compile-time): tile k lies within TILE + 64 bytes of file_len, so
+  // bytes >= flen must read as 0.  Only the last <= 2 tiles of the file are
+  // tail tiles; they run after the ring loop, because masking ring registers
+  // under a branch inside the loop makes the compiler drain the whole
+  // prefetch ring (vmcnt(0)) at the loop header.
+  auto process = [&](uint64_t k, uint32_t (&d)[16], auto tail_c) {
+    constexpr bool tail_tile = decltype(tail_c)::value;
     const uint64_t B = k * (uint64_t)TILE;
     const uint64_t span = k / SPAN_TILES;
     // bytes left in the file from B (uniform, 32-bit: every in-tile test below
     // is relative to B, so the uniform bookkeeping stays on the scalar unit)
     const uint64_t rem64 = flen - B;
     const uint32_t remu = (rem64 >> 32) ? 0xFFFFFFFFu : (uint32_t)rem64;
-    const bool tail_tile = TILE + 64 > remu;  // uniform; bytes >= flen read as 0
     if (tail_tile) {
 #pragma unroll
       for (int j = 0; j < 16; j++) d[j] = mask_past_end32(d[j], 64u * lane + 4 * j, remu);
     }
 
+#if SRD_EXP == 1  // timing experiment: consume the tile only
+    {
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < 16; j++) x ^= d[j];
+      if (x == 0x9E3779B9u && lane == 63 && k == 0) a.tile[0] = x;
+      return;
+    }
+#endif
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
     const uint32_t c = (a.ablate & 1) ? (d[0] ^ d[5] ^ d[15]) : SRD_CRC_LINE(d, lds, R);
     const uint32_t hx = (a.ablate & 1) ? c : half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
-    // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32
-    if (lane < 2 || lane == 32) a.tile[4 * k + (lane == 32 ? 2 : lane)] = hx;
+    // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
+    // Buffered in lanes 4(k%16) + {0,1,2} of tacc and written with ONE
+    // coalesced 256-B store per 16 tiles (a 12-byte store per tile cost ~10 %
+    // of the kernel's time).
+    {
+      const int t = (int)(k & 15);
+      const uint32_t v0 = __builtin_amdgcn_readlane(hx, 0), v1 = __builtin_amdgcn_readlane(hx, 1),
+                     v2 = __builtin_amdgcn_readlane(hx, 32);
+      tacc = lane == 4 * t ? v0 : lane == 4 * t + 1 ? v1 : lane == 4 * t + 2 ? v2 : tacc;
+      if (t == 15 || k + 1 == k1) {
+        const uint64_t g = k & ~15ull;
+        const uint32_t lo = (uint32_t)(max(g, k0) - g) * 4;
+        if ((uint32_t)lane >= lo && lane < 4 * t + 4) a.tile[4 * g + lane] = tacc;
+      }
+    }
+#if SRD_EXP == 2  // timing experiment: + CRC / tile values
+    return;
+#endif
 
     // ---- filter, level 1: any aligned zero halfword in the lane's line
     //      (packed 16-bit min over the 16 dwords: 1 VALU per dword); level 2
@@ -371,6 +421,16 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     for (int i = 1; i < 16; i++) zmin = __builtin_elementwise_min(zmin, __builtin_bit_cast(u16x2, d[i]));
     uint64_t slow = __ballot(zmin.x == 0 || zmin.y == 0);
     if (a.ablate & 2) slow = 0;
+#if SRD_EXP == 3  // timing experiment: + the level-1 filter
+    if (slow == 0x123456789ull && k == 0 && lane == 0) a.tile[1] = 1;
+    return;
+#endif
+    // Re-define d by an empty asm once its loads have been consumed: a loop
+    // that stores and uses a register last written by a pending VMEM load
+    // makes the compiler flush vmcnt to 0 in the loop preheader, draining the
+    // prefetch ring on every flagged tile.
+#pragma unroll
+    for (int j = 0; j < 16; j++) asm volatile("" : "+v"(d[j]));
 
     while (slow) {
       const int f = __builtin_ctzll(slow);
@@ -385,14 +445,22 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 #pragma unroll
         for (int j = 0; j < 16; j++) win[4 + j] = d[j];
       }
-      if (f < 63 ? lane == f + 1 : lane == 0) {
-        uint32_t n0 = f < 63 ? d[0] : nx[0], n1 = f < 63 ? d[1] : nx[1];
-        if (f == 63 && tail_tile) {
+      if (f < 63) {
+        if (lane == f + 1) {
+          win[20] = d[0];
+          win[21] = d[1];
+        }
+      } else {
+        uint32_t n0, n1;
+        next_head(k, &n0, &n1);
+        if (tail_tile) {
           n0 = mask_past_end32(n0, TILE, remu);
           n1 = mask_past_end32(n1, TILE + 4, remu);
         }
-        win[20] = n0;
-        win[21] = n1;
+        if (lane == 0) {
+          win[20] = n0;
+          win[21] = n1;
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -445,12 +513,28 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const uint32_t s1 = __builtin_amdgcn_readlane(alignb(W[2], W[1], sh), bl);
           const uint32_t s4 = __builtin_amdgcn_readlane(f4, bl);
           if (count < a.cap) {
-            if (lane == 0) {
+            const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
+            const uint32_t fl = (tomb ? F_TOMB : 0u) | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
+                                (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
+                                ((js & 63) < 32 ? F_SUF_LO : 0u);
+            if (count < 64) {
+              // slot `count` of the span -> lane `count` of the record registers
+              // (flushed with three stores per span, see flush_span)
+              const int cl = (int)count;
+              const bool mine = lane == cl;
+              rq[0] = mine ? (uint32_t)m : rq[0];
+              rq[1] = mine ? (uint32_t)(m >> 32) : rq[1];
+              rq[2] = mine ? s2 : rq[2];
+              rq[3] = mine ? s3 : rq[3];
+              rq[4] = mine ? s0 : rq[4];
+              rq[5] = mine ? s1 : rq[5];
+              rq[6] = mine ? s4 : rq[6];
+              rq[7] = mine ? hm : rq[7];
+              rq[8] = mine ? hs : rq[8];
+              rq[9] = mine ? fl : rq[9];
+              rvalid |= 1ull << cl;
+            } else if (lane == 0) {
               const uint64_t gi = span * a.cap + count;
-              const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
-              const uint32_t fl = (tomb ? F_TOMB : 0u) | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
-                                  (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
-                                  ((js & 63) < 32 ? F_SUF_LO : 0u);
               a.c_m[gi] = m;
               a.c_rec[2 * gi] = u32x4{s2, s3, s0, s1};
               a.c_rec[2 * gi + 1] = u32x4{s4, hm, hs, fl};
@@ -506,26 +590,71 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       win[22] = hx;
     }
     if ((k + 1) % SPAN_TILES == 0 || k + 1 == k1) {
-      if (lane == 0) a.span_count[span] = count;
+      // the span's buffered records: slot = lane
+      if (rvalid) {
+        if ((rvalid >> lane) & 1) {
+          const uint64_t gi = span * a.cap + lane;
+          a.c_m[gi] = ((uint64_t)rq[1] << 32) | rq[0];
+          a.c_rec[2 * gi] = u32x4{rq[2], rq[3], rq[4], rq[5]};
+          a.c_rec[2 * gi + 1] = u32x4{rq[6], rq[7], rq[8], rq[9]};
+        }
+        rvalid = 0;
+      }
+      // span counts: lane span%64 of scnt, one store per 64 spans
+      const uint32_t sp = (uint32_t)(span & 63);
+      scnt = (uint32_t)lane == sp ? count : scnt;
+      if (sp == 63 || k + 1 == k1) {
+        const uint64_t sg = span & ~63ull;
+        const uint32_t slo = (uint32_t)(max(sg, k0 / SPAN_TILES) - sg);
+        if ((uint32_t)lane >= slo && (uint32_t)lane <= sp) a.span_count[sg + lane] = scnt;
+      }
       count = 0;
     }
   };
 
   // 3-buffer register ring: two tiles in flight while one is processed.
   // Loads are clamped, never skipped (tiles up to n_tiles+1 are readable).
-  const uint32_t nk = (uint32_t)(k1 - k0);
+  // kt = the first tail tile (flen - kt*TILE < TILE + 64)
+  const uint64_t kt = flen >= (uint64_t)TILE + 64 ? (flen - TILE - 64) / TILE + 1 : 0;
+  const uint64_t km = min(k1, max(k0, kt));  // ring part: [k0, km)
+  const uint32_t nk = (uint32_t)(km - k0);
+  const std::false_type body{};
   uint32_t A[16], Bv[16], Cv[16];
+#if SRD_RING == 4
+  uint32_t Dv[16];
+  load_tile(k0, A);
+  load_tile(k0 + 1, Bv);
+  load_tile(k0 + 2, Cv);
+  for (uint32_t j = 0; j < nk; j += 4) {
+    load_tile(k0 + min(j + 3, nk), Dv);
+    process(k0 + j, A, body);
+    if (j + 1 >= nk) break;
+    load_tile(k0 + min(j + 4, nk), A);
+    process(k0 + j + 1, Bv, body);
+    if (j + 2 >= nk) break;
+    load_tile(k0 + min(j + 5, nk), Bv);
+    process(k0 + j + 2, Cv, body);
+    if (j + 3 >= nk) break;
+    load_tile(k0 + min(j + 6, nk), Cv);
+    process(k0 + j + 3, Dv, body);
+  }
+#else
   load_tile(k0, A);
   load_tile(k0 + 1, Bv);
   for (uint32_t j = 0; j < nk; j += 3) {
     load_tile(k0 + min(j + 2, nk), Cv);
-    process(k0 + j, A, Bv);
+    process(k0 + j, A, body);
     if (j + 1 >= nk) break;
     load_tile(k0 + min(j + 3, nk), A);
-    process(k0 + j + 1, Bv, Cv);
+    process(k0 + j + 1, Bv, body);
     if (j + 2 >= nk) break;
     load_tile(k0 + min(j + 4, nk), Bv);
-    process(k0 + j + 2, Cv, A);
+    process(k0 + j + 2, Cv, body);
+  }
+#endif
+  for (uint64_t k = km; k < k1; k++) {  // the file's last <= 2 tiles
+    load_tile(k, A);
+    process(k, A, std::true_type{});
   }
 
   // rootmax is wave-uniform already

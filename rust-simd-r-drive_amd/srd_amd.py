@@ -26,7 +26,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libsrd_amd.so")
+LIB_PATH = os.environ.get("SRD_LIB_PATH") or os.path.join(HERE, "build", "libsrd_amd.so")  # override: timing tools only
 
 SRD_FLAG_FORCE_FULL = 1
 SRD_FLAG_NO_CRC = 2
