@@ -41,7 +41,7 @@ constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
 #define SRD_CRC_LINE crc_line1
 #endif
 #ifndef SRD_RING
-#define SRD_RING 3
+#define SRD_RING 4
 #endif
 #ifndef SRD_REPL
 #define SRD_REPL 32
@@ -58,6 +58,10 @@ constexpr int F_SUF_SHIFT = 3;        // 2 bits: 0 value, 1 next-tile T, 2 next-
 // the recorded sxm / suf value is a lower-half partial (line < 32): true value =
 // mul16k(v) ^ SX_32 of the tile holding m (sxm) or the entry start (suf kind 0) -- see lo_fix()
 constexpr uint32_t F_SXM_LO = 32u, F_SUF_LO = 64u;
+// lean record (optimistic scan, one candidate in the line): only c_m and
+// {-, sxm, suf, flags} are written; link2_kernel reads p / key_hash / crc from
+// the file, applies the node test and completes the record (clearing F_LEAN)
+constexpr uint32_t F_LEAN = 128u;
 
 struct DevTables {
   uint32_t tab[4][256];
@@ -112,6 +116,20 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* f, uint64_t 
   return v;
 }
 __device__ __forceinline__ uint64_t prepad64(uint64_t o) { return (64 - (o & 63)) & 63; }
+// the 20-byte metadata record at m (entry_metadata.rs:75-112), any alignment;
+// reads the dwords covering [m, m + 20) (the buffer is padded past file_len)
+__device__ __forceinline__ void ld_meta(const uint8_t* f, uint64_t m, uint64_t* kh, uint64_t* p, uint32_t* crc) {
+  const uint32_t* q = (const uint32_t*)(f + (m & ~3ull));
+  const uint32_t sh = (uint32_t)(m & 3) * 8;
+  uint32_t w[6], v[5];
+#pragma unroll
+  for (int i = 0; i < 6; i++) w[i] = q[i];
+#pragma unroll
+  for (int i = 0; i < 5; i++) v[i] = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+  *kh = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+  *p = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+  *crc = v[4];
+}
 // zero the bytes of dword v (file offset o) at or past n
 __device__ __forceinline__ uint32_t mask_past_end(uint32_t v, uint64_t o, uint64_t n) {
   if (o + 4 <= n) return v;
@@ -122,6 +140,14 @@ __device__ __forceinline__ uint32_t mask_past_end32(uint32_t v, uint32_t o, uint
   if (o + 4 <= n) return v;
   if (o >= n) return 0u;
   return v & ((1u << (8 * (n - o))) - 1u);
+}
+
+// raw buffer resource over [base, base + bytes) for stores whose unused lanes
+// pass OOB_OFF (out of range: the hardware drops them)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t OOB_OFF = 0xFFFFFFFFu;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);  // gfx9 raw dword format
 }
 
 __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t sh) {
@@ -304,9 +330,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
   uint32_t tacc = 0, scnt = 0;
-  uint32_t rq[10];
+  uint32_t rq[5];
 #pragma unroll
-  for (int i = 0; i < 10; i++) rq[i] = 0;
+  for (int i = 0; i < 5; i++) rq[i] = 0;
   uint64_t rvalid = 0;  // wave-uniform: record slots buffered in rq
 
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
@@ -395,19 +421,22 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     const uint32_t c = (a.ablate & 1) ? (d[0] ^ d[5] ^ d[15]) : SRD_CRC_LINE(d, lds, R);
     const uint32_t hx = (a.ablate & 1) ? c : half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
-    // Buffered in lanes 4(k%16) + {0,1,2} of tacc and written with ONE
-    // coalesced 256-B store per 16 tiles (a 12-byte store per tile cost ~10 %
-    // of the kernel's time).
+    // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
+    // tiles.  Every store of this loop is an UNCONDITIONAL buffer store whose
+    // unused lanes carry an out-of-range offset (dropped by the hardware): a
+    // store under a branch makes the count of memory ops between a prefetch
+    // load and its wait path-dependent, and the compiler then waits for the
+    // store's completion too (measured: ~10 % of the kernel).
     {
       const int t = (int)(k & 15);
       const uint32_t v0 = __builtin_amdgcn_readlane(hx, 0), v1 = __builtin_amdgcn_readlane(hx, 1),
                      v2 = __builtin_amdgcn_readlane(hx, 32);
       tacc = lane == 4 * t ? v0 : lane == 4 * t + 1 ? v1 : lane == 4 * t + 2 ? v2 : tacc;
-      if (t == 15 || k + 1 == k1) {
-        const uint64_t g = k & ~15ull;
-        const uint32_t lo = (uint32_t)(max(g, k0) - g) * 4;
-        if ((uint32_t)lane >= lo && lane < 4 * t + 4) a.tile[4 * g + lane] = tacc;
-      }
+      const bool flush = t == 15 || k + 1 == k1;  // uniform
+      const uint64_t g = k & ~15ull;
+      const uint32_t lo = (uint32_t)(max(g, k0) - g) * 4;
+      const uint32_t off = (flush && (uint32_t)lane >= lo && lane < 4 * t + 4) ? 4u * lane : OOB_OFF;
+      __builtin_amdgcn_raw_buffer_store_b32(tacc, out_rsrc(a.tile + 4 * g, 256), off, 0, 0);
     }
 #if SRD_EXP == 2  // timing experiment: + CRC / tile values
     return;
@@ -492,52 +521,35 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
         if (!pm || (a.ablate & 4)) continue;
         if ((pm & (pm - 1)) == 0) {
           // one possible node (the common case: one metadata record per
-          // line): the node test and the record run on the scalar unit
+          // line): a LEAN record -- m, the two suffix values only the scan
+          // has, and the position flags.  link2_kernel reads p / key_hash /
+          // crc from the file and applies the node test (data_store.rs:404-470).
           const int bl = __builtin_ctzll(pm);
-          const uint32_t s2 = __builtin_amdgcn_readlane(f2, bl), s3 = __builtin_amdgcn_readlane(f3, bl);
           const int rs = 64 * f + bl - 14;
-          const uint32_t os = (uint32_t)bl + 2;
-          const uint32_t stb = (__builtin_amdgcn_readlane(tdw, bl) >> (((os - 1) & 3) * 8)) & 0xffu;
           const uint64_t m = B + (int64_t)rs;
-          const uint64_t p = (uint64_t)s2 | ((uint64_t)s3 << 32);
-          const uint64_t dp = m - p;
-          const bool tomb = dp == 1 && stb == 0;
-          const uint32_t pp = (0u - s2) & 63u;
-          if (!(p >= 20 && p < m && (tomb || dp > pp))) continue;  // data_store.rs:404-470
           const uint32_t us = (uint32_t)(rs + 20);
           const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
           const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
           const int lm = rs >> 6;
           const uint32_t hm = lm < 0 ? __builtin_amdgcn_readfirstlane(hxp) : __builtin_amdgcn_readlane(hx, lm & 63);
-          const uint32_t s0 = __builtin_amdgcn_readlane(alignb(W[1], W[0], sh), bl);
-          const uint32_t s1 = __builtin_amdgcn_readlane(alignb(W[2], W[1], sh), bl);
-          const uint32_t s4 = __builtin_amdgcn_readlane(f4, bl);
           if (count < a.cap) {
             const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
-            const uint32_t fl = (tomb ? F_TOMB : 0u) | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
-                                (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
-                                ((js & 63) < 32 ? F_SUF_LO : 0u);
+            const uint32_t fl = F_LEAN | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT) |
+                                (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) | ((js & 63) < 32 ? F_SUF_LO : 0u);
             if (count < 64) {
-              // slot `count` of the span -> lane `count` of the record registers
-              // (flushed with three stores per span, see flush_span)
-              const int cl = (int)count;
-              const bool mine = lane == cl;
+              // slot `count` of the span -> lane `count` of the record
+              // registers (flushed with two stores at the span's end)
+              const bool mine = lane == (int)count;
               rq[0] = mine ? (uint32_t)m : rq[0];
               rq[1] = mine ? (uint32_t)(m >> 32) : rq[1];
-              rq[2] = mine ? s2 : rq[2];
-              rq[3] = mine ? s3 : rq[3];
-              rq[4] = mine ? s0 : rq[4];
-              rq[5] = mine ? s1 : rq[5];
-              rq[6] = mine ? s4 : rq[6];
-              rq[7] = mine ? hm : rq[7];
-              rq[8] = mine ? hs : rq[8];
-              rq[9] = mine ? fl : rq[9];
-              rvalid |= 1ull << cl;
+              rq[2] = mine ? hm : rq[2];
+              rq[3] = mine ? hs : rq[3];
+              rq[4] = mine ? fl : rq[4];
+              rvalid |= 1ull << count;
             } else if (lane == 0) {
               const uint64_t gi = span * a.cap + count;
               a.c_m[gi] = m;
-              a.c_rec[2 * gi] = u32x4{s2, s3, s0, s1};
-              a.c_rec[2 * gi + 1] = u32x4{s4, hm, hs, fl};
+              a.c_rec[2 * gi + 1] = u32x4{0u, hm, hs, fl};
             }
           } else if (lane == 0) {
             atomicOr((unsigned int*)(a.counters + 2), 1u);
@@ -589,30 +601,32 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       for (int j = 0; j < 4; j++) win[j] = d[12 + j];
       win[22] = hx;
     }
-    if ((k + 1) % SPAN_TILES == 0 || k + 1 == k1) {
-      // the span's buffered records: slot = lane
-      if (rvalid) {
-        if ((rvalid >> lane) & 1) {
-          const uint64_t gi = span * a.cap + lane;
-          a.c_m[gi] = ((uint64_t)rq[1] << 32) | rq[0];
-          a.c_rec[2 * gi] = u32x4{rq[2], rq[3], rq[4], rq[5]};
-          a.c_rec[2 * gi + 1] = u32x4{rq[6], rq[7], rq[8], rq[9]};
-        }
-        rvalid = 0;
-      }
-      // span counts: lane span%64 of scnt, one store per 64 spans
+    // span end: the span's buffered records (slot = lane) and its count
+    // (lane span%64 of scnt, one store per 64 spans) -- unconditional stores
+    const bool span_end = (k + 1) % SPAN_TILES == 0 || k + 1 == k1;  // uniform
+    {
+      const bool w = span_end && ((rvalid >> lane) & 1);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + span * a.cap, 64 * 8),
+                                            w ? 8u * lane : OOB_OFF, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, rq[2], rq[3], rq[4]},  // lean: link2_kernel completes it
+                                             out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
+                                             w ? 32u * lane + 16u : OOB_OFF, 0, 0);
       const uint32_t sp = (uint32_t)(span & 63);
-      scnt = (uint32_t)lane == sp ? count : scnt;
-      if (sp == 63 || k + 1 == k1) {
-        const uint64_t sg = span & ~63ull;
-        const uint32_t slo = (uint32_t)(max(sg, k0 / SPAN_TILES) - sg);
-        if ((uint32_t)lane >= slo && (uint32_t)lane <= sp) a.span_count[sg + lane] = scnt;
+      scnt = (span_end && (uint32_t)lane == sp) ? count : scnt;
+      const bool sfl = span_end && (sp == 63 || k + 1 == k1);
+      const uint64_t sg = span & ~63ull;
+      const uint32_t slo = (uint32_t)(max(sg, k0 / SPAN_TILES) - sg);
+      __builtin_amdgcn_raw_buffer_store_b32(scnt, out_rsrc(a.span_count + sg, 256),
+                                            (sfl && (uint32_t)lane >= slo && (uint32_t)lane <= sp) ? 4u * lane : OOB_OFF,
+                                            0, 0);
+      if (span_end) {
+        rvalid = 0;
+        count = 0;
       }
-      count = 0;
     }
   };
 
-  // 3-buffer register ring: two tiles in flight while one is processed.
+  // register ring (SRD_RING = 4 buffers: three tiles in flight while one is processed).
   // Loads are clamped, never skipped (tiles up to n_tiles+1 are readable).
   // kt = the first tail tile (flen - kt*TILE < TILE + 64)
   const uint64_t kt = flen >= (uint64_t)TILE + 64 ? (flen - TILE - 64) / TILE + 1 : 0;
