@@ -178,6 +178,64 @@ int srd_xxh3_64_batch_device(srd_ctx *ctx, const uint8_t *d_keys,
                              const uint64_t *d_offs, const uint64_t *d_lens,
                              uint64_t n, uint64_t *d_out, void *stream);
 
+/* ---- checksum-on-append batch writer (BASELINE config C5) ----
+ *   srd_batch_write           <- DataStoreWriter::batch_write
+ *                                src/storage_engine/data_store.rs:838-843
+ *                                (compute_hash_batch + batch_write_with_key_hashes
+ *                                 data_store.rs:847-939, allow_null_bytes = false)
+ *   SRD_WRITE_ALLOW_NULL      <- batch_write_with_key_hashes(.., true), the
+ *                                tombstone path used by deletes (:864-897)
+ * The serialized bytes are exactly what the reference appends to the file:
+ * per entry a zero prepad to the next 64-byte boundary (none for a
+ * tombstone), the payload, and EntryMetadata{key_hash, prev_offset = the
+ * previous tail, crc32(payload)} (entry_metadata.rs:75-93).  The returned
+ * (key_hash, metadata offset) pairs are the reference's key_hash_offsets, in
+ * entry order, for the caller's index (reindex, data_store.rs:936). */
+#define SRD_WRITE_ALLOW_NULL 1u
+
+typedef struct {
+  uint64_t src;      /* payload offset in the payload buffer */
+  uint64_t len;      /* payload length (1 for a tombstone) */
+  uint64_t key_src;  /* key offset in the key buffer */
+  uint64_t tail;     /* file tail before this entry (its prev_offset) */
+  uint32_t key_len;
+  uint32_t tomb;     /* 1: NULL-byte payload written as a tombstone */
+} srd_write_entry;
+
+/* Host-side layout of a batch appended at file offset `tail`: fills out[n]
+ * and *new_tail.  `payloads` (host) is read only to recognise NULL-byte
+ * payloads.  Errors (SRD_ERR_ARG, message as the reference's InvalidInput):
+ * "Payload cannot be empty.", "NULL-byte payloads cannot be written
+ * directly." (without SRD_WRITE_ALLOW_NULL). */
+int srd_batch_layout(uint64_t tail, const uint8_t *payloads,
+                     const uint64_t *key_offs, const uint64_t *key_lens,
+                     const uint64_t *pay_offs, const uint64_t *pay_lens,
+                     uint64_t n, uint32_t flags, srd_write_entry *out,
+                     uint64_t *new_tail);
+
+/* batch_write from HOST buffers (pin them for full PCIe rate): payload and
+ * key bytes are copied to HBM in chunks on a side stream while the writer
+ * kernel serializes the previous chunk on the context stream.  The output
+ * goes to d_out (device), d_out[j] = file byte (tail & ~63) + j, capacity
+ * out_cap bytes; d_out == NULL only computes *new_tail.  kh_out / mo_out
+ * (host, nullable) receive the key hashes and metadata offsets. */
+int srd_batch_write(srd_ctx *ctx, uint64_t tail, const uint8_t *keys,
+                    const uint64_t *key_offs, const uint64_t *key_lens,
+                    const uint8_t *payloads, const uint64_t *pay_offs,
+                    const uint64_t *pay_lens, uint64_t n, uint32_t flags,
+                    uint8_t *d_out, uint64_t out_cap, uint64_t *new_tail,
+                    uint64_t *kh_out, uint64_t *mo_out);
+
+/* The writer kernel alone on device-resident inputs (entries from
+ * srd_batch_layout, copied to the device by the caller); out[j] = file byte
+ * out_base + j (out_base 64-aligned).  Asynchronous on `stream`. */
+int srd_batch_write_device(srd_ctx *ctx, const uint8_t *d_keys,
+                           const uint8_t *d_payloads,
+                           const srd_write_entry *d_entries, uint64_t n,
+                           uint8_t *d_out, uint64_t out_base,
+                           uint64_t *d_kh_out, uint64_t *d_mo_out,
+                           void *stream);
+
 /* Synthetic store of the BASELINE configs written on the device (the
  * checksum-on-append writer of data_store.rs:847-939 for keys
  * "bench-key-{i}" and counter-mode splitmix64 payloads).  lens==NULL ->

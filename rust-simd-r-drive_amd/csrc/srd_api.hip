@@ -18,6 +18,7 @@
 #include "srd_amd.h"
 #include "srd_kernels.hip"
 #include "srd_glue.hip"
+#include "srd_writer.hip"
 
 using namespace srd;
 
@@ -79,6 +80,11 @@ struct Ctx {
   uint32_t gen = 0;     // generation tag of has_child / childof
   uint64_t last_n = 0;  // chain length of the previous call (index bucket sizing)
   Plan* h_plan = nullptr;  // pinned host copy
+  // batch writer (srd_batch_write): side copy stream, double-buffer events,
+  // pinned entry tables and pinned bounce buffers (non-contiguous inputs)
+  hipStream_t cstream = nullptr;
+  hipEvent_t wev_copied[2] = {nullptr, nullptr}, wev_done[2] = {nullptr, nullptr};
+  void* pin_ent[2] = {nullptr, nullptr};
 };
 
 enum BufId {
@@ -94,6 +100,7 @@ enum BufId {
   B_CUB_TMP,
   B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
   B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
+  B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
   B_COUNT_
 };
 
@@ -277,6 +284,12 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->h_plan) hipHostFree(c->h_plan);
+  for (int i = 0; i < 2; i++) {
+    if (c->pin_ent[i]) hipHostFree(c->pin_ent[i]);
+    if (c->wev_copied[i]) hipEventDestroy(c->wev_copied[i]);
+    if (c->wev_done[i]) hipEventDestroy(c->wev_done[i]);
+  }
+  if (c->cstream) hipStreamDestroy(c->cstream);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1299,6 +1312,136 @@ extern "C" int srd_synth_span_device(srd_ctx* c, uint8_t* d_span, uint64_t span_
   if (!d_span || !n) return 0;
   if (!c || span_off > lo) { set_err("bad argument: span_off must be <= the shard's lower tail"); return SRD_ERR_ARG; }
   return synth_launch(c, d_span - span_off, off, e0, fixed_len, lens, seed, span_off);
+}
+
+// ---------------------------------------------------------------------------
+// Checksum-on-append batch writer (C5): layout on the host (prepad_len chains
+// every start to all earlier lengths), serialization + CRC + key hash on the
+// device (write_kernel), chunked H2D of the inputs on a side stream.
+extern "C" int srd_batch_layout(uint64_t tail, const uint8_t* payloads, const uint64_t* key_offs,
+                                const uint64_t* key_lens, const uint64_t* pay_offs, const uint64_t* pay_lens,
+                                uint64_t n, uint32_t flags, srd_write_entry* out, uint64_t* new_tail) {
+  if (n && (!key_offs || !key_lens || !pay_offs || !pay_lens)) { set_err("bad argument"); return SRD_ERR_ARG; }
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t len = pay_lens[i];
+    if (key_lens[i] > 0xFFFFFFFFull) { set_err("key too long"); return SRD_ERR_ARG; }
+    srd_write_entry e{pay_offs[i], len, key_offs[i], tail, (uint32_t)key_lens[i], 0u};
+    if (payloads && len == 1 && payloads[pay_offs[i]] == 0) {  // payload == NULL_BYTE (data_store.rs:864)
+      if (!(flags & SRD_WRITE_ALLOW_NULL)) {
+        set_err("NULL-byte payloads cannot be written directly.");
+        return SRD_ERR_ARG;
+      }
+      e.tomb = 1;
+      tail += 1 + 20;  // no prepad for a tombstone (:871-895)
+    } else {
+      if (len == 0) { set_err("Payload cannot be empty."); return SRD_ERR_ARG; }
+      tail += ((64 - (tail & 63)) & 63) + len + 20;  // prepad_len (:670-673), payload, metadata
+    }
+    if (out) out[i] = e;
+  }
+  if (new_tail) *new_tail = tail;
+  return 0;
+}
+
+static int launch_write(Ctx* c, hipStream_t s, const uint8_t* pay, const uint8_t* keys, const srd_write_entry* ent,
+                        uint64_t n, uint8_t* out, uint64_t base, uint64_t* kh, uint64_t* mo) {
+  if (!n) return 0;
+  WriteArgs w{pay, keys, ent, n, out, base, kh, mo};
+  const unsigned g = (unsigned)std::min<uint64_t>((n + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
+  write_kernel<<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
+  HIPCHK(hipGetLastError());
+  if (sync_debug()) {
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+  }
+  return 0;
+}
+
+extern "C" int srd_batch_write_device(srd_ctx* c, const uint8_t* d_keys, const uint8_t* d_payloads,
+                                      const srd_write_entry* d_entries, uint64_t n, uint8_t* d_out,
+                                      uint64_t out_base, uint64_t* d_kh_out, uint64_t* d_mo_out, void* stream) {
+  if (!c || (out_base & 63) ||
+      (n && (!d_keys || !d_payloads || !d_entries || !d_out || !d_kh_out || !d_mo_out))) {
+    set_err("bad argument");
+    return SRD_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  return launch_write(c, stream ? (hipStream_t)stream : c->stream, d_payloads, d_keys, d_entries, n, d_out, out_base,
+                      d_kh_out, d_mo_out);
+}
+
+extern "C" int srd_batch_write(srd_ctx* c, uint64_t tail, const uint8_t* keys, const uint64_t* key_offs,
+                               const uint64_t* key_lens, const uint8_t* payloads, const uint64_t* pay_offs,
+                               const uint64_t* pay_lens, uint64_t n, uint32_t flags, uint8_t* d_out, uint64_t out_cap,
+                               uint64_t* new_tail, uint64_t* kh_out, uint64_t* mo_out) {
+  if (!c || !new_tail || (n && (!payloads || !keys))) { set_err("bad argument"); return SRD_ERR_ARG; }
+  std::vector<srd_write_entry> E(n);
+  uint64_t nt = 0;
+  TRY(srd_batch_layout(tail, payloads, key_offs, key_lens, pay_offs, pay_lens, n, flags, E.data(), &nt));
+  *new_tail = nt;
+  if (!d_out || !n) return 0;
+  const uint64_t base = tail & ~63ull;
+  if (nt - base > out_cap) { set_err("out_cap too small for the batch"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
+  constexpr uint64_t CH = 64ull << 20;  // payload bytes per chunk (double-buffered in HBM)
+  constexpr uint64_t KCH = 8ull << 20;  // key bytes per chunk
+  constexpr uint64_t ENT_MAX = 1u << 16;
+  if (!c->cstream) {
+    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+      HIPCHK(hipEventCreateWithFlags(&c->wev_copied[i], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&c->wev_done[i], hipEventDisableTiming));
+      HIPCHK(hipHostMalloc(&c->pin_ent[i], ENT_MAX * sizeof(srd_write_entry), hipHostMallocDefault));
+    }
+  }
+  TRY(ensure(c, B_WKH, n * 8));
+  TRY(ensure(c, B_WMO, n * 8));
+  uint64_t* kh_dev = P<uint64_t>(c, B_WKH);
+  uint64_t* mo_dev = P<uint64_t>(c, B_WMO);
+  uint64_t e0 = 0;
+  for (int ci = 0; e0 < n; ci++) {
+    // a chunk: consecutive entries whose payload and key source ranges stay
+    // within CH / KCH (one entry at least); the ranges are copied as they lie
+    uint64_t plo = E[e0].src, phi = E[e0].src + E[e0].len;
+    uint64_t klo = E[e0].key_src, khi = klo + E[e0].key_len;
+    uint64_t e1 = e0 + 1;
+    while (e1 < n && e1 - e0 < ENT_MAX) {
+      const uint64_t pl2 = std::min(plo, E[e1].src), ph2 = std::max(phi, E[e1].src + E[e1].len);
+      const uint64_t kl2 = std::min(klo, E[e1].key_src), kh2 = std::max(khi, E[e1].key_src + E[e1].key_len);
+      if (ph2 - (pl2 & ~15ull) > CH || kh2 - kl2 > KCH) break;
+      plo = pl2; phi = ph2; klo = kl2; khi = kh2;
+      e1++;
+    }
+    const uint64_t pa = plo & ~15ull;  // keeps every source's 16-byte alignment in the staging buffer
+    const int slot = ci & 1;
+    if (ci >= 2) HIPCHK(hipEventSynchronize(c->wev_done[slot]));  // chunk ci-2's kernel has released the slot
+    TRY(ensure(c, (BufId)(B_WPAY0 + slot), phi - pa));
+    TRY(ensure(c, (BufId)(B_WKEY0 + slot), std::max<uint64_t>(khi - klo, 1)));
+    TRY(ensure(c, (BufId)(B_WENT0 + slot), ENT_MAX * sizeof(srd_write_entry)));
+    srd_write_entry* pe = (srd_write_entry*)c->pin_ent[slot];
+    for (uint64_t i = e0; i < e1; i++) {
+      pe[i - e0] = E[i];
+      pe[i - e0].src -= pa;
+      pe[i - e0].key_src -= klo;
+    }
+    HIPCHK(hipMemcpyAsync(P<void>(c, (BufId)(B_WPAY0 + slot)), payloads + pa, phi - pa, hipMemcpyHostToDevice,
+                          c->cstream));
+    if (khi > klo)
+      HIPCHK(hipMemcpyAsync(P<void>(c, (BufId)(B_WKEY0 + slot)), keys + klo, khi - klo, hipMemcpyHostToDevice,
+                            c->cstream));
+    HIPCHK(hipMemcpyAsync(P<void>(c, (BufId)(B_WENT0 + slot)), pe, (e1 - e0) * sizeof(srd_write_entry),
+                          hipMemcpyHostToDevice, c->cstream));
+    HIPCHK(hipEventRecord(c->wev_copied[slot], c->cstream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->wev_copied[slot], 0));
+    TRY(launch_write(c, c->stream, P<uint8_t>(c, (BufId)(B_WPAY0 + slot)), P<uint8_t>(c, (BufId)(B_WKEY0 + slot)),
+                     P<srd_write_entry>(c, (BufId)(B_WENT0 + slot)), e1 - e0, d_out, base, kh_dev + e0, mo_dev + e0));
+    HIPCHK(hipEventRecord(c->wev_done[slot], c->stream));
+    e0 = e1;
+  }
+  if (kh_out) HIPCHK(hipMemcpyAsync(kh_out, kh_dev, n * 8, hipMemcpyDeviceToHost, c->stream));
+  if (mo_out) HIPCHK(hipMemcpyAsync(mo_out, mo_dev, n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
 }
 
 // host self-test of the CRC algebra (no GPU): checks the tables against a

@@ -291,9 +291,9 @@ __device__ __forceinline__ uint32_t half_suffix_xor(uint32_t v, int lane) {
   return v ^ (row == 0 ? t1 : row == 2 ? t3 : 0u);
 }
 
-template <bool FULL>
-__global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
-  __shared__ ScanLds lds;
+// the LDS tables of the line-CRC machinery (crc_line*, lane_weight); ends
+// with a block barrier
+__device__ __forceinline__ void load_crc_lds(ScanLds& lds) {
   for (int i = threadIdx.x; i < 4 * 256 * 32; i += blockDim.x) {
     const int hi = i >> 14, b = (i >> 6) & 255, t = hi * 2 + ((i >> 5) & 1);
     lds.tab[i] = g_tabs.tab[t][b];
@@ -304,6 +304,17 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     lds.m256[i] = (&g_tabs.m256[0][0])[i];
   }
   __syncthreads();
+}
+// lane l's slice-by-4 lookup bases (tab_lookup)
+__device__ __forceinline__ void crc_lane_bases(uint32_t (&R)[4], int lane) {
+#pragma unroll
+  for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
+}
+
+template <bool FULL>
+__global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
+  __shared__ ScanLds lds;
+  load_crc_lds(lds);
 
   const int lane = threadIdx.x & 63;
   // wave id via readfirstlane: provably uniform, so all tile bookkeeping

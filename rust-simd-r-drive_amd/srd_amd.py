@@ -47,7 +47,7 @@ EXPORTS = [
     "srd_crc32_batch_device", "srd_xxh3_64_batch", "srd_xxh3_64_batch_device",
     "srd_synth_store_device", "srd_selftest_host", "srd_padded_size",
     "srd_validate_span_device", "srd_index_partition_device", "srd_index_build_device",
-    "srd_synth_span_device",
+    "srd_synth_span_device", "srd_batch_layout", "srd_batch_write", "srd_batch_write_device",
 ]
 
 
@@ -109,12 +109,24 @@ def lib():
         L.srd_index_partition_device.argtypes = [vp, vp, vp, u64, u32, vp, vp]
         L.srd_index_build_device.argtypes = [vp, vp, u64, vp, vp, C.POINTER(u64)]
         L.srd_synth_span_device.argtypes = [vp, vp, u64, u64, u64, u64, vp, u64, C.POINTER(u64), C.POINTER(u64)]
+        L.srd_batch_layout.argtypes = [u64, vp, vp, vp, vp, vp, u64, u32, vp, C.POINTER(u64)]
+        L.srd_batch_write.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, u64, u32, vp, u64, C.POINTER(u64), vp, vp]
+        L.srd_batch_write_device.argtypes = [vp, vp, vp, vp, u64, vp, u64, vp, vp, vp]
         for f in EXPORTS:
             if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
                          "srd_padded_size"):
                 getattr(L, f).restype = i32
         _lib = L
     return _lib
+
+
+class WriteEntry(C.Structure):
+    """srd_write_entry (include/srd_amd.h)"""
+    _fields_ = [("src", C.c_uint64), ("len", C.c_uint64), ("key_src", C.c_uint64), ("tail", C.c_uint64),
+                ("key_len", C.c_uint32), ("tomb", C.c_uint32)]
+
+
+WRITE_ALLOW_NULL = 1
 
 
 class SrdError(RuntimeError):
@@ -130,6 +142,7 @@ class Context:
     """One GPU + stream + reusable HBM workspace (srd_ctx)."""
 
     def __init__(self, device: int = 0):
+        self.device = device
         self.h = C.c_void_p()
         _check(lib().srd_ctx_create(device, C.byref(self.h)))
 
@@ -496,3 +509,77 @@ def synth_store_device(d_ptr: int, n_entries: int, payload_len: int = 4096, lens
         lp = _ptr(lens)
     _check(lib().srd_synth_store_device(ctx.h, C.c_void_p(d_ptr), n_entries, payload_len, lp, seed, C.byref(out)))
     return out.value
+
+
+# ---------------------------------------------------------------------------
+# DataStoreWriter::batch_write (data_store.rs:838-939) -- the checksum-on-append
+# writer (BASELINE config C5)
+
+def _blob(parts):
+    parts = [bytes(p) for p in parts]
+    lens = np.array([len(p) for p in parts], np.uint64)
+    offs = np.zeros(len(parts), np.uint64)
+    if len(parts) > 1:
+        offs[1:] = np.cumsum(lens)[:-1]
+    buf = np.frombuffer(b"".join(parts) or b"\x00", np.uint8)
+    return buf, offs, lens
+
+
+def batch_layout(tail: int, keys, payloads, allow_null: bool = False):
+    """srd_batch_layout: (entries as a structured array, new tail); raises SrdError
+    with the reference's InvalidInput messages (empty / NULL-byte payloads)."""
+    kb, ko, kl = _blob(keys)
+    pb, po, pl = _blob(payloads)
+    n = len(payloads)
+    out = (WriteEntry * max(n, 1))()
+    nt = C.c_uint64()
+    _check(lib().srd_batch_layout(tail, _ptr(pb), _ptr(ko), _ptr(kl), _ptr(po), _ptr(pl), n,
+                                  WRITE_ALLOW_NULL if allow_null else 0, C.cast(out, C.c_void_p), C.byref(nt)))
+    return out, int(nt.value)
+
+
+def batch_write_raw(d_out: int, out_cap: int, tail: int, keys_ptr: int, key_offs: np.ndarray, key_lens: np.ndarray,
+                    pay_ptr: int, pay_offs: np.ndarray, pay_lens: np.ndarray, flags: int = 0,
+                    ctx: Context | None = None, want_index: bool = True):
+    """srd_batch_write on caller buffers (host key / payload bytes at keys_ptr /
+    pay_ptr, pinned for full PCIe rate; output in device memory d_out, which
+    holds file bytes from tail & ~63).  Returns (new_tail, key_hashes, meta_offs)."""
+    ctx = ctx or default_ctx()
+    n = len(pay_lens)
+    key_offs = np.ascontiguousarray(key_offs, np.uint64)
+    key_lens = np.ascontiguousarray(key_lens, np.uint64)
+    pay_offs = np.ascontiguousarray(pay_offs, np.uint64)
+    pay_lens = np.ascontiguousarray(pay_lens, np.uint64)
+    kh = np.zeros(max(n, 1), np.uint64) if want_index else None
+    mo = np.zeros(max(n, 1), np.uint64) if want_index else None
+    nt = C.c_uint64()
+    _check(lib().srd_batch_write(ctx.h, tail, C.c_void_p(keys_ptr), _ptr(key_offs), _ptr(key_lens), C.c_void_p(pay_ptr),
+                                 _ptr(pay_offs), _ptr(pay_lens), n, flags, C.c_void_p(d_out), out_cap, C.byref(nt),
+                                 _ptr(kh) if want_index else None, _ptr(mo) if want_index else None))
+    return int(nt.value), (kh[:n] if want_index else None), (mo[:n] if want_index else None)
+
+
+def batch_write(keys, payloads, tail: int = 0, allow_null: bool = False, ctx: Context | None = None):
+    """DataStoreWriter::batch_write on the GPU: keys hashed (compute_hash_batch),
+    payloads CRC'd and serialized exactly as the reference appends them.
+    Returns (new_tail, appended bytes [tail, new_tail), key_hashes, meta_offsets)."""
+    import torch
+    ctx = ctx or default_ctx()
+    kb, ko, kl = _blob(keys)
+    pb, po, pl = _blob(payloads)
+    flags = WRITE_ALLOW_NULL if allow_null else 0
+    nt = C.c_uint64()
+    _check(lib().srd_batch_write(ctx.h, tail, _ptr(kb), _ptr(ko), _ptr(kl), _ptr(pb), _ptr(po), _ptr(pl),
+                                 len(payloads), flags, None, 0, C.byref(nt), None, None))
+    base = tail & ~63
+    cap = max(int(nt.value) - base, 1)
+    dev = torch.zeros(cap + 64, dtype=torch.uint8, device=f"cuda:{_ctx_device(ctx)}")
+    new_tail, kh, mo = batch_write_raw(dev.data_ptr(), cap, tail, kb.ctypes.data, ko, kl, pb.ctypes.data, po, pl,
+                                       flags, ctx)
+    torch.cuda.synchronize()
+    out = dev[tail - base: new_tail - base].cpu().numpy().tobytes()
+    return new_tail, out, [int(x) for x in kh], [int(x) for x in mo]
+
+
+def _ctx_device(ctx: Context) -> int:
+    return int(os.environ.get("SRD_DEVICE", "0")) if ctx is None else getattr(ctx, "device", 0)
