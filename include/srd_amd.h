@@ -236,6 +236,45 @@ int srd_batch_write_device(srd_ctx *ctx, const uint8_t *d_keys,
                            uint64_t *d_kh_out, uint64_t *d_mo_out,
                            void *stream);
 
+/* ---- device KeyIndexer + batched keyed reads ----
+ *   srd_index_table_build_device <- the KeyIndexer HashMap<u64, u64> that
+ *                                   DataStore::open fills (key_indexer.rs:98-124),
+ *                                   adopted on the GPU from the validate pass's
+ *                                   index arrays instead of re-inserted on the host
+ *   srd_index_get_packed_device  <- KeyIndexer::get_packed (key_indexer.rs:164-167)
+ *   srd_batch_read_hashed_device <- DataStoreReader::batch_read_hashed_keys
+ *                                   (data_store.rs:1117-1158) over
+ *                                   read_entry_with_context (:502-565)
+ *   srd_batch_read               <- DataStoreReader::batch_read (:1111-1115)
+ * The table lives in caller-provided device memory of srd_index_table_bytes(n)
+ * bytes (open addressing, load <= 1/2).  A read returns the entry's payload
+ * range [start, end) in the file, or start == end == 0 for None: key absent,
+ * tag mismatch against the verification hash (the reference's collision
+ * check), metadata out of range, or a tombstone. */
+#define SRD_INDEX_NONE (~(uint64_t)0) /* get_packed: key absent */
+
+uint64_t srd_index_table_bytes(uint64_t n);
+/* n unique (key_hash, packed) device pairs (e.g. srd_device_result's index). */
+int srd_index_table_build_device(srd_ctx *ctx, const uint64_t *d_keys,
+                                 const uint64_t *d_packed, uint64_t n,
+                                 void *d_table, uint64_t table_bytes);
+int srd_index_get_packed_device(srd_ctx *ctx, const void *d_table,
+                                uint64_t table_bytes, const uint64_t *d_hashes,
+                                uint64_t n, uint64_t *d_packed_out, void *stream);
+/* d_verify_hashes (nullable): compute_hash of the non-hashed keys; the read is
+ * None when its tag (hash >> 48) differs from the indexed entry's tag. */
+int srd_batch_read_hashed_device(srd_ctx *ctx, const void *d_table,
+                                 uint64_t table_bytes, const uint8_t *d_file,
+                                 uint64_t file_len, const uint64_t *d_hashes,
+                                 const uint64_t *d_verify_hashes, uint64_t n,
+                                 uint64_t *d_start, uint64_t *d_end, void *stream);
+/* Host keys in, host ranges out: keys hashed on the device (XXH3-64) and
+ * verified by their own tags, as batch_read does.  Synchronises. */
+int srd_batch_read(srd_ctx *ctx, const void *d_table, uint64_t table_bytes,
+                   const uint8_t *d_file, uint64_t file_len, const uint8_t *keys,
+                   const uint64_t *key_offs, const uint64_t *key_lens, uint64_t n,
+                   uint64_t *start_out, uint64_t *end_out);
+
 /* Synthetic store of the BASELINE configs written on the device (the
  * checksum-on-append writer of data_store.rs:847-939 for keys
  * "bench-key-{i}" and counter-mode splitmix64 payloads).  lens==NULL ->

@@ -19,6 +19,7 @@
 #include "srd_kernels.hip"
 #include "srd_glue.hip"
 #include "srd_writer.hip"
+#include "srd_index.hip"
 
 using namespace srd;
 
@@ -1442,6 +1443,112 @@ extern "C" int srd_batch_write(srd_ctx* c, uint64_t tail, const uint8_t* keys, c
   if (mo_out) HIPCHK(hipMemcpyAsync(mo_out, mo_dev, n * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Device KeyIndexer table + batched keyed reads (srd_index.hip)
+static uint32_t table_log2cap(uint64_t table_bytes) {
+  uint32_t l = 0;
+  while (l < 62 && (16ull << (l + 1)) <= table_bytes) l++;
+  return l;
+}
+extern "C" uint64_t srd_index_table_bytes(uint64_t n) {
+  uint64_t cap = 64;
+  while (cap < 2 * n) cap <<= 1;
+  return 16 * cap;
+}
+static unsigned grid_for(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192)); }
+
+extern "C" int srd_index_table_build_device(srd_ctx* c, const uint64_t* d_keys, const uint64_t* d_packed, uint64_t n,
+                                            void* d_table, uint64_t table_bytes) {
+  if (!c || !d_table || (n && (!d_keys || !d_packed)) || table_bytes < srd_index_table_bytes(n)) {
+    set_err("bad argument (table_bytes < srd_index_table_bytes(n)?)");
+    return SRD_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const uint32_t l = table_log2cap(table_bytes);
+  uint64_t* tk = (uint64_t*)d_table;
+  uint64_t* tp = tk + (1ull << l);
+  HIPCHK(hipMemsetAsync(tp, 0xFF, (1ull << l) * 8, c->stream));
+  if (n) {
+    idx_table_insert_kernel<<<grid_for(n), 256, 0, c->stream>>>(d_keys, d_packed, n, tk, (unsigned long long*)tp, l);
+    KCHK(c, "idx_table_insert_kernel");
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+extern "C" int srd_index_get_packed_device(srd_ctx* c, const void* d_table, uint64_t table_bytes,
+                                           const uint64_t* d_hashes, uint64_t n, uint64_t* d_packed_out,
+                                           void* stream) {
+  if (!c || !d_table || table_bytes < 16 * 64 || (n && (!d_hashes || !d_packed_out))) {
+    set_err("bad argument");
+    return SRD_ERR_ARG;
+  }
+  if (!n) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  const uint32_t l = table_log2cap(table_bytes);
+  const uint64_t* tk = (const uint64_t*)d_table;
+  idx_get_packed_kernel<<<grid_for(n), 256, 0, stream ? (hipStream_t)stream : c->stream>>>(tk, tk + (1ull << l), l,
+                                                                                             d_hashes, n, d_packed_out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int srd_batch_read_hashed_device(srd_ctx* c, const void* d_table, uint64_t table_bytes,
+                                            const uint8_t* d_file, uint64_t flen, const uint64_t* d_hashes,
+                                            const uint64_t* d_verify, uint64_t n, uint64_t* d_start, uint64_t* d_end,
+                                            void* stream) {
+  if (!c || !d_table || table_bytes < 16 * 64 || (n && (!d_hashes || !d_start || !d_end || (flen && !d_file)))) {
+    set_err("bad argument");
+    return SRD_ERR_ARG;
+  }
+  if (!n) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  const uint32_t l = table_log2cap(table_bytes);
+  const uint64_t* tk = (const uint64_t*)d_table;
+  batch_read_kernel<<<grid_for(n), 256, 0, stream ? (hipStream_t)stream : c->stream>>>(
+      tk, tk + (1ull << l), l, d_file, flen, d_hashes, d_verify, n, d_start, d_end);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int srd_batch_read(srd_ctx* c, const void* d_table, uint64_t table_bytes, const uint8_t* d_file,
+                              uint64_t flen, const uint8_t* keys, const uint64_t* key_offs, const uint64_t* key_lens,
+                              uint64_t n, uint64_t* start_out, uint64_t* end_out) {
+  if (!c || (n && (!keys || !key_offs || !key_lens || !start_out || !end_out))) {
+    set_err("bad argument");
+    return SRD_ERR_ARG;
+  }
+  if (!n) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  uint64_t klen = 0;
+  for (uint64_t i = 0; i < n; i++) klen = std::max(klen, key_offs[i] + key_lens[i]);
+  void *dk = nullptr, *dof = nullptr, *dl = nullptr, *dh = nullptr, *ds = nullptr, *de = nullptr;
+  int r = 0;
+  auto cleanup = [&] { hipFree(dk); hipFree(dof); hipFree(dl); hipFree(dh); hipFree(ds); hipFree(de); };
+  if (hipMalloc(&dk, klen + 1) || hipMalloc(&dof, n * 8) || hipMalloc(&dl, n * 8) || hipMalloc(&dh, n * 8) ||
+      hipMalloc(&ds, n * 8) || hipMalloc(&de, n * 8)) {
+    cleanup();
+    set_err("hipMalloc failed");
+    return SRD_ERR_ALLOC;
+  }
+  if (klen) HIPCHK(hipMemcpyAsync(dk, keys, klen, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(dof, key_offs, n * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(dl, key_lens, n * 8, hipMemcpyHostToDevice, c->stream));
+  r = srd_xxh3_64_batch_device(c, (const uint8_t*)dk, (const uint64_t*)dof, (const uint64_t*)dl, n, (uint64_t*)dh,
+                               nullptr);  // compute_hash_batch (data_store.rs:1112)
+  // batch_read verifies every key by its own tag (Some(keys), :1113)
+  if (!r) r = srd_batch_read_hashed_device(c, d_table, table_bytes, d_file, flen, (const uint64_t*)dh,
+                                           (const uint64_t*)dh, n, (uint64_t*)ds, (uint64_t*)de, nullptr);
+  if (!r) {
+    HIPCHK(hipMemcpyAsync(start_out, ds, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(end_out, de, n * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  cleanup();
+  return r;
 }
 
 // host self-test of the CRC algebra (no GPU): checks the tables against a

@@ -48,6 +48,8 @@ EXPORTS = [
     "srd_synth_store_device", "srd_selftest_host", "srd_padded_size",
     "srd_validate_span_device", "srd_index_partition_device", "srd_index_build_device",
     "srd_synth_span_device", "srd_batch_layout", "srd_batch_write", "srd_batch_write_device",
+    "srd_index_table_bytes", "srd_index_table_build_device", "srd_index_get_packed_device",
+    "srd_batch_read_hashed_device", "srd_batch_read",
 ]
 
 
@@ -112,9 +114,15 @@ def lib():
         L.srd_batch_layout.argtypes = [u64, vp, vp, vp, vp, vp, u64, u32, vp, C.POINTER(u64)]
         L.srd_batch_write.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, u64, u32, vp, u64, C.POINTER(u64), vp, vp]
         L.srd_batch_write_device.argtypes = [vp, vp, vp, vp, u64, vp, u64, vp, vp, vp]
+        L.srd_index_table_bytes.argtypes = [u64]
+        L.srd_index_table_bytes.restype = u64
+        L.srd_index_table_build_device.argtypes = [vp, vp, vp, u64, vp, u64]
+        L.srd_index_get_packed_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
+        L.srd_batch_read_hashed_device.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, vp, vp, vp]
+        L.srd_batch_read.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, u64, vp, vp]
         for f in EXPORTS:
             if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
-                         "srd_padded_size"):
+                         "srd_padded_size", "srd_index_table_bytes"):
                 getattr(L, f).restype = i32
         _lib = L
     return _lib
@@ -583,3 +591,73 @@ def batch_write(keys, payloads, tail: int = 0, allow_null: bool = False, ctx: Co
 
 def _ctx_device(ctx: Context) -> int:
     return int(os.environ.get("SRD_DEVICE", "0")) if ctx is None else getattr(ctx, "device", 0)
+
+
+# ---------------------------------------------------------------------------
+# Device KeyIndexer + batched keyed reads:
+# KeyIndexer::get_packed (key_indexer.rs:164-167), batch_read /
+# batch_read_hashed_keys (data_store.rs:1111-1158) over read_entry_with_context
+# (:502-565)
+
+INDEX_NONE = (1 << 64) - 1
+
+
+class DeviceIndex:
+    """The KeyIndexer adopted on the GPU: an open-addressing table in HBM built
+    from n unique (key_hash, packed) device pairs -- e.g. the index arrays of a
+    validate pass (DeviceResult.index_key_hash / index_packed)."""
+
+    def __init__(self, d_keys: int, d_packed: int, n: int, ctx: Context | None = None):
+        import torch
+        self.ctx = ctx or default_ctx()
+        self.n = n
+        self.nbytes = int(lib().srd_index_table_bytes(n))
+        self.table = torch.empty(self.nbytes, dtype=torch.uint8, device=f"cuda:{self.ctx.device}")
+        _check(lib().srd_index_table_build_device(self.ctx.h, C.c_void_p(d_keys), C.c_void_p(d_packed), n,
+                                                  C.c_void_p(self.table.data_ptr()), self.nbytes))
+
+    def _dev_u64(self, a):
+        import torch
+        return torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(self.table.device)
+
+    def get_packed(self, hashes) -> np.ndarray:
+        """KeyIndexer::get_packed for each hash (INDEX_NONE when absent)."""
+        import torch
+        q = self._dev_u64(hashes)
+        out = torch.empty_like(q)
+        n = q.numel()
+        _check(lib().srd_index_get_packed_device(self.ctx.h, C.c_void_p(self.table.data_ptr()), self.nbytes,
+                                                 C.c_void_p(q.data_ptr()), n, C.c_void_p(out.data_ptr()),
+                                                 C.c_void_p(self.ctx.stream)))
+        torch.cuda.synchronize()
+        return out.cpu().numpy().view(np.uint64)
+
+    def batch_read_hashed_keys(self, d_file: int, file_len: int, hashes, non_hashed_keys=None):
+        """batch_read_hashed_keys: [(start, end) | None] in query order; with
+        non_hashed_keys, each read is verified by tag_from_key (data_store.rs:513-521)."""
+        import torch
+        if non_hashed_keys is not None and len(non_hashed_keys) != len(hashes):
+            raise ValueError("Mismatched lengths for hashed and non-hashed keys.")
+        q = self._dev_u64(hashes)
+        v = self._dev_u64(compute_hash_batch(non_hashed_keys, self.ctx)) if non_hashed_keys is not None else None
+        n = q.numel()
+        st, en = torch.empty_like(q), torch.empty_like(q)
+        torch.cuda.synchronize()
+        _check(lib().srd_batch_read_hashed_device(self.ctx.h, C.c_void_p(self.table.data_ptr()), self.nbytes,
+                                                  C.c_void_p(d_file), file_len, C.c_void_p(q.data_ptr()),
+                                                  C.c_void_p(v.data_ptr()) if v is not None else None, n,
+                                                  C.c_void_p(st.data_ptr()), C.c_void_p(en.data_ptr()),
+                                                  C.c_void_p(self.ctx.stream)))
+        torch.cuda.synchronize()
+        s, e = st.cpu().numpy().view(np.uint64), en.cpu().numpy().view(np.uint64)
+        return [None if a == b else (int(a), int(b)) for a, b in zip(s, e)]
+
+    def batch_read(self, d_file: int, file_len: int, keys):
+        """batch_read (data_store.rs:1111-1115): host keys, hashed and verified on the device."""
+        kb, ko, kl = _blob(keys)
+        n = len(keys)
+        st = np.zeros(max(n, 1), np.uint64)
+        en = np.zeros(max(n, 1), np.uint64)
+        _check(lib().srd_batch_read(self.ctx.h, C.c_void_p(self.table.data_ptr()), self.nbytes, C.c_void_p(d_file),
+                                    file_len, _ptr(kb), _ptr(ko), _ptr(kl), n, _ptr(st), _ptr(en)))
+        return [None if a == b else (int(a), int(b)) for a, b in zip(st[:n], en[:n])]
