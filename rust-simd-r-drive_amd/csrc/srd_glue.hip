@@ -166,32 +166,30 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     const uint64_t gi = sp * a.cap + i, g = gb + i;
     if (g >= a.capK) return;  // plan_kernel reports ST_CAPK
     const uint64_t m = a.c_m[gi];
-    uint64_t p;
+    const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
+    const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     bool node = true;
-    const u32x4 r1 = a.c_rec[2 * gi + 1];
     if (r1[3] & F_LEAN) {
-      // lean record: the metadata fields from the file, recover_valid_chain's
-      // node test (data_store.rs:404-470), then the full record for the
-      // kernels downstream.  A candidate that fails the test gets no parent:
-      // it can never be core, and a chain through it fails the shape check.
-      uint64_t kh;
+      // lean record: key_hash / crc from the file (these loads issue beside
+      // the parent lookup's first one), recover_valid_chain's node test
+      // (data_store.rs:404-470), then the full record for the kernels
+      // downstream.  A candidate that fails the test gets no parent: it can
+      // never be core, and a chain through it fails the shape check.
+      uint64_t kh, p2;
       uint32_t crc;
-      ld_meta(a.file, m, &kh, &p, &crc);
+      ld_meta(a.file, m, &kh, &p2, &crc);
       const uint64_t dp = m - p;
       const bool tomb = dp == 1 && a.file[p] == 0;  // tombstone byte at prev_tail (p = m - 1 here)
       node = p >= 20 && p < m && (tomb || dp > prepad64(p));
-      a.c_rec[2 * gi] = u32x4{(uint32_t)p, (uint32_t)(p >> 32), (uint32_t)kh, (uint32_t)(kh >> 32)};
+      a.c_rec[2 * gi] = u32x4{r0[0], r0[1], (uint32_t)kh, (uint32_t)(kh >> 32)};
       a.c_rec[2 * gi + 1] = u32x4{crc, r1[1], r1[2], (r1[3] & ~F_LEAN) | (tomb ? F_TOMB : 0u)};
-    } else {
-      const u32x4 r0 = a.c_rec[2 * gi];
-      p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     }
     const uint64_t mp = p - 20;  // p >= 20 for nodes
     const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
     int64_t par = PAR_MISS;
-    if (!node) {
-      // no parent, no root
-    } else if (sp2 >= a.s_lo && sp2 < a.n_spans) {
+    // the lookup does not wait for the node test (its loads overlap the
+    // lean record's file reads); a failed test discards it below
+    if (sp2 >= a.s_lo && sp2 < a.n_spans) {
       const uint32_t n2 = min(a.span_count[sp2], a.cap);
       uint32_t lo = 0, hi = n2;
       const uint64_t* cm = a.c_m + sp2 * a.cap;
@@ -201,7 +199,8 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
       }
       if (lo < n2 && cm[lo] == mp) par = (int64_t)(a.span_base[sp2] + lo);
     }
-    if (node && par == PAR_MISS) {
+    if (!node) par = PAR_MISS;  // no parent, no root
+    else if (par == PAR_MISS) {
       if (a.span_lo) {
         if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
       } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {

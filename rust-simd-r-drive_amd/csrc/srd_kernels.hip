@@ -58,8 +58,8 @@ constexpr int F_SUF_SHIFT = 3;        // 2 bits: 0 value, 1 next-tile T, 2 next-
 // the recorded sxm / suf value is a lower-half partial (line < 32): true value =
 // mul16k(v) ^ SX_32 of the tile holding m (sxm) or the entry start (suf kind 0) -- see lo_fix()
 constexpr uint32_t F_SXM_LO = 32u, F_SUF_LO = 64u;
-// lean record (optimistic scan, one candidate in the line): only c_m and
-// {-, sxm, suf, flags} are written; link2_kernel reads p / key_hash / crc from
+// lean record (optimistic scan, one candidate in the line): only c_m, p and
+// {-, sxm, suf, flags} are written; link2_kernel reads key_hash / crc from
 // the file, applies the node test and completes the record (clearing F_LEAN)
 constexpr uint32_t F_LEAN = 128u;
 
@@ -341,9 +341,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
   uint32_t tacc = 0, scnt = 0;
-  uint32_t rq[5];
+  uint32_t rq[7];
 #pragma unroll
-  for (int i = 0; i < 5; i++) rq[i] = 0;
+  for (int i = 0; i < 7; i++) rq[i] = 0;
   uint64_t rvalid = 0;  // wave-uniform: record slots buffered in rq
 
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
@@ -532,12 +532,14 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
         if (!pm || (a.ablate & 4)) continue;
         if ((pm & (pm - 1)) == 0) {
           // one possible node (the common case: one metadata record per
-          // line): a LEAN record -- m, the two suffix values only the scan
-          // has, and the position flags.  link2_kernel reads p / key_hash /
-          // crc from the file and applies the node test (data_store.rs:404-470).
+          // line): a LEAN record -- m, p, the two suffix values only the
+          // scan has, and the position flags.  link2_kernel reads key_hash /
+          // crc from the file (beside its parent lookup, which needs p) and
+          // applies the node test (data_store.rs:404-470).
           const int bl = __builtin_ctzll(pm);
           const int rs = 64 * f + bl - 14;
           const uint64_t m = B + (int64_t)rs;
+          const uint32_t s2 = __builtin_amdgcn_readlane(f2, bl), s3 = __builtin_amdgcn_readlane(f3, bl);  // p
           const uint32_t us = (uint32_t)(rs + 20);
           const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
           const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
@@ -556,10 +558,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
               rq[2] = mine ? hm : rq[2];
               rq[3] = mine ? hs : rq[3];
               rq[4] = mine ? fl : rq[4];
+              rq[5] = mine ? s2 : rq[5];
+              rq[6] = mine ? s3 : rq[6];
               rvalid |= 1ull << count;
             } else if (lane == 0) {
               const uint64_t gi = span * a.cap + count;
               a.c_m[gi] = m;
+              a.c_rec[2 * gi] = u32x4{s2, s3, 0u, 0u};
               a.c_rec[2 * gi + 1] = u32x4{0u, hm, hs, fl};
             }
           } else if (lane == 0) {
@@ -619,7 +624,10 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const bool w = span_end && ((rvalid >> lane) & 1);
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + span * a.cap, 64 * 8),
                                             w ? 8u * lane : OOB_OFF, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, rq[2], rq[3], rq[4]},  // lean: link2_kernel completes it
+      // lean records: link2_kernel completes key_hash and crc
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[5], rq[6]}, out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
+                                            w ? 32u * lane : OOB_OFF, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, rq[2], rq[3], rq[4]},
                                              out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
                                              w ? 32u * lane + 16u : OOB_OFF, 0, 0);
       const uint32_t sp = (uint32_t)(span & 63);
