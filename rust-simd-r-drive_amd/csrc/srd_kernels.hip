@@ -38,10 +38,10 @@ constexpr int TILE = 4096;
 constexpr int SPAN_TILES = 4;
 constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
 #ifndef SRD_CRC_LINE
-#define SRD_CRC_LINE crc_line1
+#define SRD_CRC_LINE crc_line4
 #endif
 #ifndef SRD_RING
-#define SRD_RING 4
+#define SRD_RING 3
 #endif
 #ifndef SRD_REPL
 #define SRD_REPL 32
@@ -349,6 +349,14 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
   // (no loads under divergent/uniform branches, so the compiler's vmcnt
   // waits never have to drain the prefetch ring).
+  // timing experiments (SRD_ABLATE_NOLOAD builds only): runtime ablation
+  // bits; otherwise a compile-time 0, so no branch splits the tile's
+  // straight-line code (CRC, lane weights, suffix XOR, filter) into blocks
+#ifdef SRD_ABLATE_NOLOAD
+  const uint32_t ABL = a.ablate;
+#else
+  constexpr uint32_t ABL = 0;
+#endif
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
 #ifdef SRD_ABLATE_NOLOAD
     if (a.ablate & 16) k = k0;  // timing experiment: compute-only (re-reads one L2-resident tile)
@@ -429,8 +437,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
 #endif
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
-    const uint32_t c = (a.ablate & 1) ? (d[0] ^ d[5] ^ d[15]) : SRD_CRC_LINE(d, lds, R);
-    const uint32_t hx = (a.ablate & 1) ? c : half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
+    const uint32_t c = (ABL & 1) ? (d[0] ^ d[5] ^ d[15]) : SRD_CRC_LINE(d, lds, R);
+    const uint32_t hx = (ABL & 1) ? c : half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
     // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
     // tiles.  Every store of this loop is an UNCONDITIONAL buffer store whose
@@ -460,7 +468,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 #pragma unroll
     for (int i = 1; i < 16; i++) zmin = __builtin_elementwise_min(zmin, __builtin_bit_cast(u16x2, d[i]));
     uint64_t slow = __ballot(zmin.x == 0 || zmin.y == 0);
-    if (a.ablate & 2) slow = 0;
+    if (ABL & 2) slow = 0;
 #if SRD_EXP == 3  // timing experiment: + the level-1 filter
     if (slow == 0x123456789ull && k == 0 && lane == 0) a.tile[1] = 1;
     return;
@@ -529,7 +537,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
         // != 0) are recorded; a chain through any other node fails the shape
         // check and goes to the full pass, so nothing else is needed here
         const uint64_t pm = __ballot(inrange && f3 <= hb && (f2 | f3) != 0 && f4 != 0);
-        if (!pm || (a.ablate & 4)) continue;
+        if (!pm || (ABL & 4)) continue;
         if ((pm & (pm - 1)) == 0) {
           // one possible node (the common case: one metadata record per
           // line): a LEAN record -- m, p, the two suffix values only the
@@ -645,7 +653,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
   };
 
-  // register ring (SRD_RING = 4 buffers: three tiles in flight while one is processed).
+  // register ring (SRD_RING buffers: RING-1 tiles in flight while one is
+  // processed; 3 measured best with the 4-chain line CRC, whose registers a
+  // 4th buffer would spill).
   // Loads are clamped, never skipped (tiles up to n_tiles+1 are readable).
   // kt = the first tail tile (flen - kt*TILE < TILE + 64)
   const uint64_t kt = flen >= (uint64_t)TILE + 64 ? (flen - TILE - 64) / TILE + 1 : 0;
