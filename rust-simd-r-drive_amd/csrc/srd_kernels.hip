@@ -40,6 +40,9 @@ constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
 #ifndef SRD_CRC_LINE
 #define SRD_CRC_LINE crc_line4
 #endif
+#ifndef SRD_LEAN
+#define SRD_LEAN 0  // 1: single-candidate records without key_hash / crc (link2_kernel reads them)
+#endif
 #ifndef SRD_RING
 #define SRD_RING 3
 #endif
@@ -341,9 +344,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
   uint32_t tacc = 0, scnt = 0;
-  uint32_t rq[7];
+  uint32_t rq[SRD_LEAN ? 7 : 10];
 #pragma unroll
-  for (int i = 0; i < 7; i++) rq[i] = 0;
+  for (int i = 0; i < (SRD_LEAN ? 7 : 10); i++) rq[i] = 0;
   uint64_t rvalid = 0;  // wave-uniform: record slots buffered in rq
 
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
@@ -548,6 +551,24 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const int rs = 64 * f + bl - 14;
           const uint64_t m = B + (int64_t)rs;
           const uint32_t s2 = __builtin_amdgcn_readlane(f2, bl), s3 = __builtin_amdgcn_readlane(f3, bl);  // p
+#if !SRD_LEAN
+          // full record: the node test here (data_store.rs:404-470) and the
+          // key hash / crc from the window
+          const uint64_t p = (uint64_t)s2 | ((uint64_t)s3 << 32);
+          const uint64_t dp = m - p;
+          const uint32_t os = (uint32_t)bl + 2;
+          const uint32_t stb = (__builtin_amdgcn_readlane(tdw, bl) >> (((os - 1) & 3) * 8)) & 0xffu;
+          const bool tomb = dp == 1 && stb == 0;
+          if (!(p >= 20 && p < m && (tomb || dp > ((0u - s2) & 63u)))) continue;
+          const uint32_t s0 = __builtin_amdgcn_readlane(alignb(W[1], W[0], sh), bl);
+          const uint32_t s1 = __builtin_amdgcn_readlane(alignb(W[2], W[1], sh), bl);
+          const uint32_t s4 = __builtin_amdgcn_readlane(f4, bl);
+          constexpr uint32_t REC_KIND = 0u;
+#else
+          constexpr uint32_t s0 = 0u, s1 = 0u, s4 = 0u;
+          constexpr bool tomb = false;
+          constexpr uint32_t REC_KIND = F_LEAN;
+#endif
           const uint32_t us = (uint32_t)(rs + 20);
           const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
           const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
@@ -555,11 +576,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const uint32_t hm = lm < 0 ? __builtin_amdgcn_readfirstlane(hxp) : __builtin_amdgcn_readlane(hx, lm & 63);
           if (count < a.cap) {
             const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
-            const uint32_t fl = F_LEAN | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT) |
-                                (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) | ((js & 63) < 32 ? F_SUF_LO : 0u);
+            const uint32_t fl = REC_KIND | (tomb ? F_TOMB : 0u) | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
+                                (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
+                                ((js & 63) < 32 ? F_SUF_LO : 0u);
             if (count < 64) {
               // slot `count` of the span -> lane `count` of the record
-              // registers (flushed with two stores at the span's end)
+              // registers (flushed at the span's end)
               const bool mine = lane == (int)count;
               rq[0] = mine ? (uint32_t)m : rq[0];
               rq[1] = mine ? (uint32_t)(m >> 32) : rq[1];
@@ -568,12 +590,17 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
               rq[4] = mine ? fl : rq[4];
               rq[5] = mine ? s2 : rq[5];
               rq[6] = mine ? s3 : rq[6];
+#if !SRD_LEAN
+              rq[7] = mine ? s0 : rq[7];
+              rq[8] = mine ? s1 : rq[8];
+              rq[9] = mine ? s4 : rq[9];
+#endif
               rvalid |= 1ull << count;
             } else if (lane == 0) {
               const uint64_t gi = span * a.cap + count;
               a.c_m[gi] = m;
-              a.c_rec[2 * gi] = u32x4{s2, s3, 0u, 0u};
-              a.c_rec[2 * gi + 1] = u32x4{0u, hm, hs, fl};
+              a.c_rec[2 * gi] = u32x4{s2, s3, s0, s1};
+              a.c_rec[2 * gi + 1] = u32x4{s4, hm, hs, fl};
             }
           } else if (lane == 0) {
             atomicOr((unsigned int*)(a.counters + 2), 1u);
@@ -632,12 +659,20 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const bool w = span_end && ((rvalid >> lane) & 1);
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + span * a.cap, 64 * 8),
                                             w ? 8u * lane : OOB_OFF, 0, 0);
-      // lean records: link2_kernel completes key_hash and crc
+#if SRD_LEAN  // lean records: link2_kernel completes key_hash and crc
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[5], rq[6]}, out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
                                             w ? 32u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, rq[2], rq[3], rq[4]},
                                              out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
                                              w ? 32u * lane + 16u : OOB_OFF, 0, 0);
+#else
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]},
+                                             out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
+                                             w ? 32u * lane : OOB_OFF, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]},
+                                             out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
+                                             w ? 32u * lane + 16u : OOB_OFF, 0, 0);
+#endif
       const uint32_t sp = (uint32_t)(span & 63);
       scnt = (span_end && (uint32_t)lane == sp) ? count : scnt;
       const bool sfl = span_end && (sp == 63 || k + 1 == k1);
