@@ -196,11 +196,13 @@ int srd_xxh3_64_batch_device(srd_ctx *ctx, const uint8_t *d_keys,
 typedef struct {
   uint64_t src;      /* payload offset in the payload buffer */
   uint64_t len;      /* payload length (1 for a tombstone) */
-  uint64_t key_src;  /* key offset in the key buffer */
+  uint64_t key_src;  /* key offset in the key buffer (SRD_ENTRY_HASHED: the key hash) */
   uint64_t tail;     /* file tail before this entry (its prev_offset) */
   uint32_t key_len;
-  uint32_t tomb;     /* 1: NULL-byte payload written as a tombstone */
+  uint32_t flags;    /* SRD_ENTRY_TOMB | SRD_ENTRY_HASHED */
 } srd_write_entry;
+#define SRD_ENTRY_TOMB 1u   /* NULL-byte payload written as a tombstone */
+#define SRD_ENTRY_HASHED 2u /* key_src holds the key hash (batch_write_with_key_hashes) */
 
 /* Host-side layout of a batch appended at file offset `tail`: fills out[n]
  * and *new_tail.  `payloads` (host) is read only to recognise NULL-byte
@@ -274,6 +276,35 @@ int srd_batch_read(srd_ctx *ctx, const void *d_table, uint64_t table_bytes,
                    const uint8_t *d_file, uint64_t file_len, const uint8_t *keys,
                    const uint64_t *key_offs, const uint64_t *key_lens, uint64_t n,
                    uint64_t *start_out, uint64_t *end_out);
+
+/* ---- iteration and compaction over the device index ----
+ *   srd_iter_entries_device   <- EntryIterator (entry_iterator.rs:69-126) /
+ *                                par_iter_entries (data_store.rs:297-361):
+ *                                the latest non-tombstone entry per key, in
+ *                                EntryIterator order (newest first)
+ *   srd_estimate_compaction_savings_device
+ *                             <- estimate_compaction_savings (:605-616)
+ *   srd_compact_device        <- compact (:706-749): the latest entries
+ *                                re-serialized by write_stream_with_key_hash
+ *                                in iter_entries order from offset 0 (the
+ *                                write_kernel with prehashed keys), into d_out
+ * d_index_packed = srd_device_result.index_packed (n_index values). */
+int srd_iter_entries_device(srd_ctx *ctx, const uint8_t *d_file,
+                            uint64_t file_len, const uint64_t *d_index_packed,
+                            uint64_t n_index, uint64_t *d_start, uint64_t *d_end,
+                            uint64_t *d_meta_off, uint64_t *d_key_hash,
+                            uint64_t *n_out);
+int srd_estimate_compaction_savings_device(srd_ctx *ctx, const uint8_t *d_file,
+                                           uint64_t file_len,
+                                           const uint64_t *d_index_packed,
+                                           uint64_t n_index, uint64_t *savings);
+/* d_out == NULL only computes *new_len.  Fails (SRD_ERR_ARG) like the
+ * reference when a kept payload is all NULL bytes ("NULL-byte-only streams
+ * cannot be written directly."). */
+int srd_compact_device(srd_ctx *ctx, const uint8_t *d_file, uint64_t file_len,
+                       const uint64_t *d_index_packed, uint64_t n_index,
+                       uint8_t *d_out, uint64_t out_cap, uint64_t *new_len,
+                       uint64_t *d_key_hash_out, uint64_t *d_meta_off_out);
 
 /* Synthetic store of the BASELINE configs written on the device (the
  * checksum-on-append writer of data_store.rs:847-939 for keys

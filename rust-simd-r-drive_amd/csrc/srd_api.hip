@@ -102,6 +102,7 @@ enum BufId {
   B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
   B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
+  B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT,
   B_COUNT_
 };
 
@@ -1332,7 +1333,7 @@ extern "C" int srd_batch_layout(uint64_t tail, const uint8_t* payloads, const ui
         set_err("NULL-byte payloads cannot be written directly.");
         return SRD_ERR_ARG;
       }
-      e.tomb = 1;
+      e.flags = SRD_ENTRY_TOMB;
       tail += 1 + 20;  // no prepad for a tombstone (:871-895)
     } else {
       if (len == 0) { set_err("Payload cannot be empty."); return SRD_ERR_ARG; }
@@ -1345,9 +1346,10 @@ extern "C" int srd_batch_layout(uint64_t tail, const uint8_t* payloads, const ui
 }
 
 static int launch_write(Ctx* c, hipStream_t s, const uint8_t* pay, const uint8_t* keys, const srd_write_entry* ent,
-                        uint64_t n, uint8_t* out, uint64_t base, uint64_t* kh, uint64_t* mo) {
+                        uint64_t n, uint8_t* out, uint64_t base, uint64_t* kh, uint64_t* mo,
+                        unsigned int* null_only = nullptr) {
   if (!n) return 0;
-  WriteArgs w{pay, keys, ent, n, out, base, kh, mo};
+  WriteArgs w{pay, keys, ent, n, out, base, kh, mo, null_only};
   const unsigned g = (unsigned)std::min<uint64_t>((n + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
   write_kernel<<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
   HIPCHK(hipGetLastError());
@@ -1549,6 +1551,120 @@ extern "C" int srd_batch_read(srd_ctx* c, const void* d_table, uint64_t table_by
   HIPCHK(hipStreamSynchronize(c->stream));
   cleanup();
   return r;
+}
+
+// ---------------------------------------------------------------------------
+// par_iter_entries / EntryIterator, estimate_compaction_savings and compact
+// over the device index (srd_index.hip iter_* kernels + the writer)
+static int iter_run(Ctx* c, const uint8_t* d_file, uint64_t flen, const uint64_t* d_packed, uint64_t n,
+                    uint64_t* d_start, uint64_t* d_end, uint64_t* d_meta, uint64_t* d_kh, uint64_t* n_out,
+                    uint64_t* kept_bytes) {
+  *n_out = 0;
+  if (kept_bytes) *kept_bytes = 0;
+  if (!n) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  TRY(ensure(c, B_IT_FLAG, n * 4));
+  TRY(ensure(c, B_IT_POS, n * 4));
+  TRY(ensure(c, B_IT_ST, n * 8));
+  TRY(ensure(c, B_IT_EN, n * 8));
+  TRY(ensure(c, B_IT_KEPT, 64));
+  TRY(ensure_cub(c, n));
+  uint32_t* flag = P<uint32_t>(c, B_IT_FLAG);
+  uint32_t* pos = P<uint32_t>(c, B_IT_POS);
+  unsigned long long* kept = P<unsigned long long>(c, B_IT_KEPT);
+  HIPCHK(hipMemsetAsync(kept, 0, 8, c->stream));
+  iter_flag_kernel<<<grid_for(n), 256, 0, c->stream>>>(d_file, flen, d_packed, n, flag, P<uint64_t>(c, B_IT_ST),
+                                                       P<uint64_t>(c, B_IT_EN), kept);
+  KCHK(c, "iter_flag_kernel");
+  size_t tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, flag, pos, (int)n, c->stream));
+  uint32_t last[2] = {0, 0};
+  unsigned long long hk = 0;
+  HIPCHK(hipMemcpyAsync(&last[0], pos + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(&last[1], flag + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(&hk, kept, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const uint64_t nv = (uint64_t)last[0] + last[1];
+  if (d_start && nv) {
+    iter_emit_kernel<<<grid_for(n), 256, 0, c->stream>>>(d_file, d_packed, flag, pos, n, nv, P<uint64_t>(c, B_IT_ST),
+                                                         P<uint64_t>(c, B_IT_EN), d_start, d_end, d_meta, d_kh);
+    KCHK(c, "iter_emit_kernel");
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  *n_out = nv;
+  if (kept_bytes) *kept_bytes = hk;
+  return 0;
+}
+
+extern "C" int srd_iter_entries_device(srd_ctx* c, const uint8_t* d_file, uint64_t flen, const uint64_t* d_packed,
+                                       uint64_t n_index, uint64_t* d_start, uint64_t* d_end, uint64_t* d_meta_off,
+                                       uint64_t* d_key_hash, uint64_t* n_out) {
+  if (!c || !n_out || (n_index && (!d_file || !d_packed || !d_start || !d_end))) {
+    set_err("bad argument");
+    return SRD_ERR_ARG;
+  }
+  return iter_run(c, d_file, flen, d_packed, n_index, d_start, d_end, d_meta_off, d_key_hash, n_out, nullptr);
+}
+
+extern "C" int srd_estimate_compaction_savings_device(srd_ctx* c, const uint8_t* d_file, uint64_t flen,
+                                                      const uint64_t* d_packed, uint64_t n_index, uint64_t* savings) {
+  if (!c || !savings || (n_index && (!d_file || !d_packed))) { set_err("bad argument"); return SRD_ERR_ARG; }
+  uint64_t nv = 0, kept = 0;
+  TRY(iter_run(c, d_file, flen, d_packed, n_index, nullptr, nullptr, nullptr, nullptr, &nv, &kept));
+  *savings = flen > kept ? flen - kept : 0;  // total_size.saturating_sub(unique_entry_size)
+  return 0;
+}
+
+extern "C" int srd_compact_device(srd_ctx* c, const uint8_t* d_file, uint64_t flen, const uint64_t* d_packed,
+                                  uint64_t n_index, uint8_t* d_out, uint64_t out_cap, uint64_t* new_len,
+                                  uint64_t* d_key_hash_out, uint64_t* d_meta_off_out) {
+  if (!c || !new_len || (n_index && (!d_file || !d_packed))) { set_err("bad argument"); return SRD_ERR_ARG; }
+  *new_len = 0;
+  if (!n_index) return 0;
+  TRY(ensure(c, B_IT_OST, n_index * 8));
+  TRY(ensure(c, B_IT_OEN, n_index * 8));
+  TRY(ensure(c, B_IT_OKH, n_index * 8));
+  uint64_t nv = 0;
+  TRY(iter_run(c, d_file, flen, d_packed, n_index, P<uint64_t>(c, B_IT_OST), P<uint64_t>(c, B_IT_OEN), nullptr,
+               P<uint64_t>(c, B_IT_OKH), &nv, nullptr));
+  // layout of the compacted file: write_stream_with_key_hash per entry in
+  // iter_entries order (data_store.rs:706-719, 758-825), tail from 0
+  std::vector<uint64_t> st(nv), en(nv), kh(nv);
+  if (nv) {
+    HIPCHK(hipMemcpyAsync(st.data(), P<uint64_t>(c, B_IT_OST), nv * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(en.data(), P<uint64_t>(c, B_IT_OEN), nv * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(kh.data(), P<uint64_t>(c, B_IT_OKH), nv * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  std::vector<srd_write_entry> E(nv);
+  uint64_t tail = 0;
+  for (uint64_t j = 0; j < nv; j++) {
+    E[j] = srd_write_entry{st[j], en[j] - st[j], kh[j], tail, 0u, SRD_ENTRY_HASHED};
+    tail += ((64 - (tail & 63)) & 63) + (en[j] - st[j]) + 20;
+  }
+  *new_len = tail;
+  if (!d_out || !nv) return 0;
+  if (tail > out_cap) { set_err("out_cap too small for the compacted store"); return SRD_ERR_ARG; }
+  TRY(ensure(c, B_IT_ENT, nv * sizeof(srd_write_entry)));
+  TRY(ensure(c, B_WKH, nv * 8));
+  TRY(ensure(c, B_WMO, nv * 8));
+  TRY(ensure(c, B_IT_KEPT, 64));
+  unsigned int* nullf = (unsigned int*)(P<uint8_t>(c, B_IT_KEPT) + 8);
+  HIPCHK(hipMemsetAsync(nullf, 0, 4, c->stream));
+  HIPCHK(hipMemcpyAsync(P<void>(c, B_IT_ENT), E.data(), nv * sizeof(srd_write_entry), hipMemcpyHostToDevice,
+                        c->stream));
+  TRY(launch_write(c, c->stream, d_file, nullptr, P<srd_write_entry>(c, B_IT_ENT), nv, d_out, 0,
+                   d_key_hash_out ? d_key_hash_out : P<uint64_t>(c, B_WKH),
+                   d_meta_off_out ? d_meta_off_out : P<uint64_t>(c, B_WMO), nullf));
+  unsigned int hn = 0;
+  HIPCHK(hipMemcpyAsync(&hn, nullf, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (hn) {  // write_stream rejects NULL-only payloads (data_store.rs:792-797); compact() fails with it
+    set_err("NULL-byte-only streams cannot be written directly.");
+    return SRD_ERR_ARG;
+  }
+  return 0;
 }
 
 // host self-test of the CRC algebra (no GPU): checks the tables against a

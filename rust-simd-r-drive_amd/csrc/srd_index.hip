@@ -55,6 +55,59 @@ __global__ void idx_get_packed_kernel(const uint64_t* tkeys, const uint64_t* tpa
     out[i] = idx_get_packed(tkeys, tpacked, log2cap, q[i]);
 }
 
+// The payload range of the entry whose metadata is at `off`, with the
+// reference's bounds, prepad and tombstone rules (read_entry_with_context
+// :524-553, par_iter_entries :322-353, EntryIterator::next
+// entry_iterator.rs:85-118); false for None (out of range / tombstone).
+__device__ __forceinline__ bool entry_range(const uint8_t* file, uint64_t flen, uint64_t off, uint64_t* start,
+                                            uint64_t* end) {
+  if (off + 20 > flen) return false;
+  const uint64_t prev = ld_u64_unaligned(file, off + 8);  // EntryMetadata.prev_offset
+  uint64_t s = prev + prepad64(prev);
+  if (off > prev && off - prev == 1 && file[prev] == 0) s = prev;  // tombstone: no prepad
+  if (s >= off) return false;
+  if (off - s == 1 && file[s] == 0) return false;  // tombstone -> None
+  *start = s;
+  *end = off;
+  return true;
+}
+
+// par_iter_entries over the index: flags, ranges and the kept bytes
+// (range + metadata, EntryHandle::file_size) for estimate_compaction_savings
+__global__ __launch_bounds__(256) void iter_flag_kernel(const uint8_t* file, uint64_t flen, const uint64_t* packed,
+                                                        uint64_t n, uint32_t* flag, uint64_t* st, uint64_t* en,
+                                                        unsigned long long* kept) {
+  __shared__ unsigned long long part[4];
+  unsigned long long mine = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t s = 0, e = 0;
+    const bool ok = entry_range(file, flen, packed[i] & 0xFFFFFFFFFFFFull, &s, &e);
+    flag[i] = ok;
+    st[i] = s;
+    en[i] = e;
+    if (ok) mine += e - s + 20;
+  }
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(kept, part[0] + part[1] + part[2] + part[3]);
+}
+
+// EntryIterator order (newest first = the index's file order reversed)
+__global__ void iter_emit_kernel(const uint8_t* file, const uint64_t* packed, const uint32_t* flag, const uint32_t* pos,
+                                 uint64_t n, uint64_t n_valid, const uint64_t* st, const uint64_t* en,
+                                 uint64_t* out_start, uint64_t* out_end, uint64_t* out_meta, uint64_t* out_kh) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (!flag[i]) continue;
+    const uint64_t j = n_valid - 1 - pos[i];
+    const uint64_t off = packed[i] & 0xFFFFFFFFFFFFull;
+    out_start[j] = st[i];
+    out_end[j] = en[i];
+    if (out_meta) out_meta[j] = off;
+    if (out_kh) out_kh[j] = ld_u64_unaligned(file, off);
+  }
+}
+
 // read_entry_with_context (data_store.rs:502-565) per query: [start, end) of
 // the entry's payload, or (0, 0) for None (absent, tag mismatch against the
 // verification hash, out of range, or a tombstone)
@@ -67,18 +120,7 @@ __global__ void batch_read_kernel(const uint64_t* tkeys, const uint64_t* tpacked
     const uint64_t off = p & 0xFFFFFFFFFFFFull;
     bool ok = p != TBL_EMPTY;
     if (ok && verify) ok = (p >> 48) == (verify[i] >> 48);  // tag_from_key(non_hashed_key), :513-521
-    ok = ok && off + 20 <= flen;                               // :524-526
-    if (ok) {
-      const uint64_t prev = ld_u64_unaligned(file, off + 8);  // EntryMetadata.prev_offset
-      uint64_t s = prev + prepad64(prev);                     // :533-535
-      if (off > prev && off - prev == 1 && file[prev] == 0) s = prev;  // tombstone: no prepad, :539-544
-      if (s < off) {                                         // :546-548 (off <= flen already)
-        if (!(off - s == 1 && file[s] == 0)) {               // tombstone -> None, :551-553
-          start = s;
-          end = off;
-        }
-      }
-    }
+    if (ok && !entry_range(file, flen, off, &start, &end)) start = end = 0;
     out_start[i] = start;
     out_end[i] = end;
   }

@@ -27,6 +27,7 @@ struct WriteArgs {
   uint64_t base;                // 64-aligned file offset of out[0]
   uint64_t* kh_out;             // [n] key hashes
   uint64_t* mo_out;             // [n] metadata offsets (the index's offsets)
+  unsigned int* null_only;      // nullable: write_stream's check (data_store.rs:783-797), set when a payload is all NULL bytes
 };
 
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
@@ -49,13 +50,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
   for (uint64_t i = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv; i < a.n; i += (uint64_t)gridDim.x * SCAN_WAVES_V2) {
     const srd_write_entry e = a.ent[i];
     // key hash (lane 0; compute_hash.rs:25-27 = xxh3_64 with seed 0)
-    uint64_t kh = 0;
-    if (lane == 0) kh = xxh3_64(a.keys + e.key_src, e.key_len);
+    uint64_t kh = e.key_src;  // SRD_ENTRY_HASHED: batch_write_with_key_hashes / write_stream_with_key_hash
+    if (!(e.flags & SRD_ENTRY_HASHED) && lane == 0) kh = xxh3_64(a.keys + e.key_src, e.key_len);
     kh = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(kh >> 32)) << 32) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)kh);
     uint32_t crc;
     uint64_t mo;
-    if (e.tomb) {
+    if (e.flags & SRD_ENTRY_TOMB) {
       // tombstone: the single NULL byte, no prepad (data_store.rs:864-897)
       if (lane == 0) a.out[e.tail - a.base] = 0;
       crc = 0xD202EF8Du;  // CRC32(b"\0")
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
       const uint8_t* src = a.pay + e.src;
       uint8_t* dst = a.out + (st - a.base);  // 64-aligned when out is
       const bool fast_src = ((uintptr_t)src & 15) == 0;
-      uint32_t acc = 0;
+      uint32_t acc = 0, any = 0;
       const uint64_t nb = (e.len + TILE - 1) / TILE;
       for (uint64_t b = 0; b < nb; b++) {
         const uint64_t o = b * TILE + 64ull * lane;
@@ -90,12 +91,15 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
             d[q >> 2] |= (uint32_t)v << (8 * (q & 3));
           }
         }
+#pragma unroll
+        for (int j = 0; j < 16; j++) any |= d[j];
         // raw CRC of this 4 KiB block (zero-padded past the payload)
         const uint32_t u = lane_weight(crc_line1(d, lds, R), lds.nib, lane);
         const uint32_t lo = wave_xor(lane < 32 ? u : 0u), hi = wave_xor(lane < 32 ? 0u : u);
         const uint32_t raw = mul16k(lo, &g_tabs.m16k[0][0]) ^ hi;
         acc = mul_tile(acc) ^ raw;
       }
+      if (a.null_only && !__ballot(any != 0) && lane == 0) atomicOr(a.null_only, 1u);
       const uint64_t z = nb * TILE - e.len;  // trailing zero padding of the last block, < 4096
       if (z) acc = mulp(g_tabs.invpow[z], acc);
       if (e.len != last_len) {

@@ -50,6 +50,7 @@ EXPORTS = [
     "srd_synth_span_device", "srd_batch_layout", "srd_batch_write", "srd_batch_write_device",
     "srd_index_table_bytes", "srd_index_table_build_device", "srd_index_get_packed_device",
     "srd_batch_read_hashed_device", "srd_batch_read",
+    "srd_iter_entries_device", "srd_estimate_compaction_savings_device", "srd_compact_device",
 ]
 
 
@@ -120,6 +121,9 @@ def lib():
         L.srd_index_get_packed_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
         L.srd_batch_read_hashed_device.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, vp, vp, vp]
         L.srd_batch_read.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, u64, vp, vp]
+        L.srd_iter_entries_device.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp, C.POINTER(u64)]
+        L.srd_estimate_compaction_savings_device.argtypes = [vp, vp, u64, vp, u64, C.POINTER(u64)]
+        L.srd_compact_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, C.POINTER(u64), vp, vp]
         for f in EXPORTS:
             if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
                          "srd_padded_size", "srd_index_table_bytes"):
@@ -131,7 +135,7 @@ def lib():
 class WriteEntry(C.Structure):
     """srd_write_entry (include/srd_amd.h)"""
     _fields_ = [("src", C.c_uint64), ("len", C.c_uint64), ("key_src", C.c_uint64), ("tail", C.c_uint64),
-                ("key_len", C.c_uint32), ("tomb", C.c_uint32)]
+                ("key_len", C.c_uint32), ("flags", C.c_uint32)]
 
 
 WRITE_ALLOW_NULL = 1
@@ -661,3 +665,44 @@ class DeviceIndex:
         _check(lib().srd_batch_read(self.ctx.h, C.c_void_p(self.table.data_ptr()), self.nbytes, C.c_void_p(d_file),
                                     file_len, _ptr(kb), _ptr(ko), _ptr(kl), n, _ptr(st), _ptr(en)))
         return [None if a == b else (int(a), int(b)) for a, b in zip(st[:n], en[:n])]
+
+
+# ---------------------------------------------------------------------------
+# EntryIterator / par_iter_entries, estimate_compaction_savings and compact
+# over the device index (data_store.rs:297-361, 605-749; entry_iterator.rs:69-126)
+
+def iter_entries_device(d_file: int, file_len: int, d_index_packed: int, n_index: int, ctx: Context | None = None):
+    """The latest non-tombstone entry per key, newest first (EntryIterator
+    order): numpy arrays (start, end, meta_off, key_hash)."""
+    import torch
+    ctx = ctx or default_ctx()
+    dev = f"cuda:{ctx.device}"
+    outs = [torch.empty(max(n_index, 1), dtype=torch.int64, device=dev) for _ in range(4)]
+    n = C.c_uint64()
+    _check(lib().srd_iter_entries_device(ctx.h, C.c_void_p(d_file), file_len, C.c_void_p(d_index_packed), n_index,
+                                         *[C.c_void_p(t.data_ptr()) for t in outs], C.byref(n)))
+    k = int(n.value)
+    return tuple(t[:k].cpu().numpy().view(np.uint64) for t in outs)
+
+
+def estimate_compaction_savings_device(d_file: int, file_len: int, d_index_packed: int, n_index: int,
+                                       ctx: Context | None = None) -> int:
+    ctx = ctx or default_ctx()
+    s = C.c_uint64()
+    _check(lib().srd_estimate_compaction_savings_device(ctx.h, C.c_void_p(d_file), file_len,
+                                                        C.c_void_p(d_index_packed), n_index, C.byref(s)))
+    return int(s.value)
+
+
+def compact_device(d_file: int, file_len: int, d_index_packed: int, n_index: int, ctx: Context | None = None):
+    """compact(): the compacted store's bytes as a device tensor."""
+    import torch
+    ctx = ctx or default_ctx()
+    nl = C.c_uint64()
+    _check(lib().srd_compact_device(ctx.h, C.c_void_p(d_file), file_len, C.c_void_p(d_index_packed), n_index, None,
+                                    0, C.byref(nl), None, None))
+    out = torch.zeros(max(int(nl.value), 1) + 64, dtype=torch.uint8, device=f"cuda:{ctx.device}")
+    _check(lib().srd_compact_device(ctx.h, C.c_void_p(d_file), file_len, C.c_void_p(d_index_packed), n_index,
+                                    C.c_void_p(out.data_ptr()), out.numel(), C.byref(nl), None, None))
+    torch.cuda.synchronize()
+    return out[: int(nl.value)]
