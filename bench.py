@@ -172,12 +172,84 @@ def bench_c5(args, ctx, local):
     print(json.dumps(res), flush=True)
 
 
+def bench_ops(args, ctx, local):
+    """SURVEY.md 8(f) rows 2-4 on the C2 store (1M x 4 KiB, one validate pass
+    first): device KeyIndexer adoption, batched keyed reads (batch_read_hashed_keys
+    of every key, tag-verified), the EntryIterator, estimate_compaction_savings
+    and compact (a full rewrite here: every key is live).  Device-resident;
+    times are HIP-event / wall times per call (not the headline metric)."""
+    import ctypes as C
+    n = args.entries_per_gpu or (1 << 20)
+    size = S.synth_store_len(n)
+    dev = f"cuda:{local}"
+    store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=dev)
+    S.synth_store_device(store.data_ptr(), n, 4096, ctx=ctx)
+    r = S.validate_index_device(store.data_ptr(), size, 0, ctx)
+    assert r.final_len == size and r.n_index == n
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    packed = torch.empty(n, dtype=torch.int64, device=dev)
+    keys.copy_(torch.from_numpy(S.device_to_numpy(r.index_key_hash, n).view(np.int64)).to(dev))
+    packed.copy_(torch.from_numpy(S.device_to_numpy(r.index_packed, n).view(np.int64)).to(dev))
+    torch.cuda.synchronize()
+
+    def timed(fn, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps * 1e3
+    idx = S.DeviceIndex(keys.data_ptr(), packed.data_ptr(), n, ctx)
+    t_build = timed(lambda: S.DeviceIndex(keys.data_ptr(), packed.data_ptr(), n, ctx))
+    st, en = torch.empty_like(keys), torch.empty_like(keys)
+
+    def reads():
+        S._check(S.lib().srd_batch_read_hashed_device(ctx.h, C.c_void_p(idx.table.data_ptr()), idx.nbytes,
+                                                      C.c_void_p(store.data_ptr()), size, C.c_void_p(keys.data_ptr()),
+                                                      C.c_void_p(keys.data_ptr()), n, C.c_void_p(st.data_ptr()),
+                                                      C.c_void_p(en.data_ptr()), C.c_void_p(ctx.stream)))
+        torch.cuda.synchronize()
+    t_read = timed(reads)
+    assert int((en - st).min()) == 4096
+    outs = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(4)]
+    nn = C.c_uint64()
+
+    def it():
+        S._check(S.lib().srd_iter_entries_device(ctx.h, C.c_void_p(store.data_ptr()), size,
+                                                 C.c_void_p(packed.data_ptr()), n,
+                                                 *[C.c_void_p(t.data_ptr()) for t in outs], C.byref(nn)))
+    t_iter = timed(it)
+    assert nn.value == n
+    t_sav = timed(lambda: S.estimate_compaction_savings_device(store.data_ptr(), size, packed.data_ptr(), n, ctx))
+    cout = torch.empty(size + 64, dtype=torch.uint8, device=dev)
+    nl = C.c_uint64()
+
+    def compact():
+        S._check(S.lib().srd_compact_device(ctx.h, C.c_void_p(store.data_ptr()), size, C.c_void_p(packed.data_ptr()),
+                                            n, C.c_void_p(cout.data_ptr()), size + 64, C.byref(nl), None, None))
+    t_comp = timed(compact, 3)
+    res = {
+        "metric": "device index + iterator + compaction ops on the C2 store (8(f) rows 2-4)",
+        "config": {"workload": f"C2: {n} x 4096 B entries, {size} B store, every key live", "entries": n},
+        "index_table_build_ms": round(t_build, 3),
+        "batch_read_hashed_keys_all_ms": round(t_read, 3),
+        "batch_read_Mkeys_per_s": round(n / t_read / 1e3, 1),
+        "iter_entries_ms": round(t_iter, 3),
+        "estimate_compaction_savings_ms": round(t_sav, 3),
+        "compact_ms": round(t_comp, 3),
+        "compact_GBps_read_plus_write": round(2 * nl.value / (t_comp * 1e-3) / 1e9, 1),
+        "compacted_bytes": int(nl.value),
+    }
+    print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c5", "ops"], default="c2",
                     help="c2: 4 KiB entries (headline); c3: Zipf-sized entries 64 B..1 MiB (variable length); "
                          "c5: checksum-on-append batch write of 1M x 4 KiB from pinned host memory")
     ap.add_argument("--entries-per-gpu", type=int, default=None)
@@ -201,6 +273,8 @@ def main():
 
     if args.config == "c5":
         return bench_c5(args, ctx, local)
+    if args.config == "ops":
+        return bench_ops(args, ctx, local)
     n, L = args.entries_per_gpu, args.payload
     if n is None:
         n = 1 << 20 if args.config == "c2" else 10_000_000
