@@ -367,7 +367,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     const u32x4* q = (const u32x4*)(file + k * (uint64_t)TILE + 64ull * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const u32x4 v = q[j];  // plain loads: this 64 B-per-lane pattern runs at ~3.8 TB/s with nt, ~6.1 without
+      // plain loads: this 64 B-per-lane pattern runs at ~3.8 TB/s with nt, ~6.1 without
+#ifdef SRD_NT_LAST  // timing experiment: the line's last 16 B as a streaming (nt) load
+      const u32x4 v = j == 3 ? __builtin_nontemporal_load(q + j) : q[j];
+#else
+      const u32x4 v = q[j];
+#endif
       o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
     }
   };
