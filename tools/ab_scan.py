@@ -16,14 +16,16 @@ for p in libs:
     assert L.srd_ctx_create(0, C.byref(h)) == 0
     handles.append((L, h))
 ctx = S.Context(0)
-n = int(os.environ.get("N_ENTRIES", 1 << 20))
-size = S.synth_store_len(n)
+c3 = os.environ.get("CONFIG") == "c3"  # C3: 10M Zipf-sized entries
+n = int(os.environ.get("N_ENTRIES", 10_000_000 if c3 else 1 << 20))
+lens = S.zipf_lens(n) if c3 else None
+size = S.synth_store_len(n, 4096, lens)
 t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
-S.synth_store_device(t.data_ptr(), n, 4096, ctx=ctx)
+S.synth_store_device(t.data_ptr(), n, 4096, lens, seed=0x5EED0004 if c3 else 0x5EED0001, ctx=ctx)
 torch.cuda.synchronize()
 res = {p: [] for p in libs}
 tot = {p: [] for p in libs}
-for rnd in range(12):
+for rnd in range(int(os.environ.get('ROUNDS', 12))):
     for p, (L, h) in zip(libs, handles):
         r = S.DeviceResult()
         rc = L.srd_validate_index_device(h, C.c_void_p(t.data_ptr()), size, 0, C.byref(r))
