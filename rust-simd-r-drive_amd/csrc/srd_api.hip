@@ -155,6 +155,10 @@ int upload_tables() {
   t.x32768 = g_host_tabs.x32768;
   t.xtile[0] = kX0;
   for (int e = 1; e <= 64; e++) t.xtile[e] = mulp(g_host_tabs.x32768, t.xtile[e - 1]);
+  t.xt64[0] = kX0;
+  for (int q = 1; q <= 64; q++) t.xt64[q] = mulp(t.xtile[64], t.xt64[q - 1]);
+  for (int tb = 0; tb < 4; tb++)
+    for (int b = 0; b < 256; b++) t.mx64[tb][b] = mulp(t.xtile[64], (uint32_t)b << (8 * tb));
   memcpy(t.pow8, g_host_tabs.pow8, sizeof t.pow8);
   memcpy(t.invpow, g_host_tabs.invpow, sizeof t.invpow);
   for (int pos = 0; pos < 8; pos++)
@@ -455,7 +459,7 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
     KCHK(c, "finalize_kernel");
     HIPCHK(hipGetLastError());
     if (!f.no_crc) {
-      slow_kernel<<<1024, 64, 0, c->stream>>>(f);
+      slow_kernel<<<2048, 64, 0, c->stream>>>(f);
       KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
     }
@@ -814,7 +818,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.n_bad = (unsigned long long*)&pl->n_bad;
       finalize_kernel<<<2048, 256, 0, c->stream>>>(f);
       KCHK(c, "finalize_kernel");
-      if (!f.no_crc) slow_kernel<<<1024, 64, 0, c->stream>>>(f);
+      if (!f.no_crc) slow_kernel<<<2048, 64, 0, c->stream>>>(f);
       KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
       // ---- KeyIndexer::build (bucketed; SRD_INDEX_GLOBAL=1: one global table, timing experiments) ----

@@ -79,6 +79,8 @@ struct DevTables {
   uint32_t m128[4][256];
   uint32_t m256[4][256];
   uint32_t xtile[65];              // X^e, X = x^32768 (one tile), e = 0..64
+  uint32_t xt64[65];               // X^(64 q), q = 0..64 (with xtile: X^n for n < 4160 in one multiply)
+  uint32_t mx64[4][256];           // v -> v * X^64 byte tables (the long-entry Horner step)
 };
 __device__ DevTables g_tabs;
 
@@ -1134,7 +1136,7 @@ __device__ __forceinline__ uint32_t xpow8_any(uint64_t n) { return xpow8_dev(n);
 // Horner-combines tiles k0+1+l, +65+l, ... with X^64 steps, weights its sum by
 // X^(distance of its last tile to tile k1-1), and the wave XOR-reduces.
 __device__ uint32_t crc_from_pieces_wave(uint64_t s, uint64_t m, uint32_t suf, uint32_t sxm, uint32_t tail,
-                                         const uint32_t* tile) {
+                                         const uint32_t* tile, const uint32_t* mx64) {
   const int lane = threadIdx.x & 63;
   const uint64_t len = m - s;
   if (len < 64) return tail ^ g_tabs.zero_crc[len];
@@ -1150,14 +1152,14 @@ __device__ uint32_t crc_from_pieces_wave(uint64_t s, uint64_t m, uint32_t suf, u
     uint64_t jl = 0;
     bool any = false;
     for (uint64_t j = lane; j < n; j += 64) {
-      h = mulp(g_tabs.xtile[64], h) ^ tile_T(tile, k0 + 1 + j);
+      h = mulfix(h, mx64) ^ tile_T(tile, k0 + 1 + j);  // h * X^64 by byte tables (LDS)
       jl = j;
       any = true;
     }
     uint32_t v = any ? mulp(g_tabs.xtile[n - 1 - jl], h) : 0u;  // n-1-jl < 64
     for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
     // acc * X^n ^ mid, then one more tile step into k1
-    const uint32_t xn = xpow8_any(n * (uint64_t)TILE);
+    const uint32_t xn = n < 64 * 65 ? mulp(g_tabs.xt64[n >> 6], g_tabs.xtile[n & 63]) : xpow8_any(n * (uint64_t)TILE);
     acc = mulp(xn, acc) ^ v;
     y = mulp(g_tabs.x32768, acc) ^ tile_T(tile, k1) ^ sxm;
   }
@@ -1169,9 +1171,13 @@ __device__ uint32_t crc_from_pieces_wave(uint64_t s, uint64_t m, uint32_t suf, u
 // entry spans more than LONG_TILES whole tiles)
 __global__ __launch_bounds__(64) void slow_kernel(FinArgs a) {
   __shared__ uint32_t tab[1024];
+  __shared__ uint32_t mx[1024];
   const unsigned long long ns = *a.n_slow;
   if (blockIdx.x >= ns) return;
-  for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = g_tabs.tab[i >> 8][i & 255];
+  for (int i = threadIdx.x; i < 1024; i += 64) {
+    tab[i] = g_tabs.tab[i >> 8][i & 255];
+    mx[i] = (&g_tabs.mx64[0][0])[i];
+  }
   __syncthreads();
   for (uint64_t w = blockIdx.x; w < ns; w += gridDim.x) {
     const uint64_t c = a.slow_list[w];
@@ -1179,7 +1185,7 @@ __global__ __launch_bounds__(64) void slow_kernel(FinArgs a) {
     uint32_t pieces = a.o_pieces[c], suf = a.o_suf[c], sxm = a.o_sxm[c], tail = a.o_tail[c];
     if (!(pieces & 1)) suf = tile_probe_sx(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64), tab);
     if (!(pieces & 2)) sxm = tile_probe_sx(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64), tab);
-    const uint32_t crc = crc_from_pieces_wave(s, m, suf, sxm, tail, a.tile);
+    const uint32_t crc = crc_from_pieces_wave(s, m, suf, sxm, tail, a.tile, mx);
     if ((threadIdx.x & 63) == 0) {
       a.o_crc[c] = crc;
       a.o_ok[c] = crc == a.o_crc_st[c];
