@@ -187,9 +187,18 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     const uint64_t mp = p - 20;  // p >= 20 for nodes
     const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
     int64_t par = PAR_MISS;
+    // In a store without garbage the parent is the previous record in file
+    // order (the same span's slot i-1, else the previous span's last slot):
+    // one load instead of a binary search.  Otherwise the search below.
+    if (i > 0) {
+      if (a.c_m[gi - 1] == mp) par = (int64_t)(g - 1);
+    } else if (sp > a.s_lo) {
+      const uint32_t np = min(a.span_count[sp - 1], a.cap);
+      if (np && a.c_m[(sp - 1) * a.cap + np - 1] == mp) par = (int64_t)(gb - 1);
+    }
     // the lookup does not wait for the node test (its loads overlap the
     // lean record's file reads); a failed test discards it below
-    if (sp2 >= a.s_lo && sp2 < a.n_spans) {
+    if (par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
       const uint32_t n2 = min(a.span_count[sp2], a.cap);
       uint32_t lo = 0, hi = n2;
       const uint64_t* cm = a.c_m + sp2 * a.cap;
