@@ -680,7 +680,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
     HIPCHK(hipMemsetAsync(cnt, 0, 64, c->stream));
     // the scan writes every span's count; only the scan sentinel needs a zero
-    HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT) + ns_rel, 0, 4, c->stream));
+    // the scan-count sentinel and the plan are zeroed by the scan kernel
     // per-tile / per-span arrays hold the resident range only: their base
     // pointers are shifted so kernels index them by absolute tile / span
     ScanArgs a{};
@@ -697,6 +697,9 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
     a.k_lo = k_lo;
     a.m_lo = lo;
+    a.zero_words = (uint32_t*)pl;
+    a.n_zero_words = (uint32_t)(sizeof(Plan) / 4);
+    a.sentinel = P<uint32_t>(c, B_SPAN_COUNT) + ns_rel;
     {
       const char* ab = getenv("SRD_SCAN_ABLATE");
       a.ablate = ab ? (uint32_t)atoi(ab) : 0u;
@@ -748,7 +751,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     uint32_t mgen = c->gen;
     bool timed = false;
     for (int rounds = 0;; rounds += 2) {
-      HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
+      if (rounds) HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));  // round 0: zeroed by the scan
       ShapeArgs sa{};
       sa.file = d_file;
       sa.flen = flen;

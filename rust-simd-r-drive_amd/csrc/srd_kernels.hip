@@ -101,6 +101,11 @@ struct ScanArgs {
   // shard's lower tail; 0 = whole file, where m >= 1)
   uint64_t k_lo;
   uint64_t m_lo;
+  // zeroed by block 0 before its scan (folds two memset launches into the
+  // scan): the glue's plan words and the span-count scan's sentinel
+  uint32_t* zero_words;
+  uint32_t n_zero_words;
+  uint32_t* sentinel;
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -319,6 +324,10 @@ __device__ __forceinline__ void crc_lane_bases(uint32_t (&R)[4], int lane) {
 template <bool FULL>
 __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
   __shared__ ScanLds lds;
+  if (blockIdx.x == 0) {
+    for (uint32_t i = threadIdx.x; i < a.n_zero_words; i += blockDim.x) a.zero_words[i] = 0;
+    if (threadIdx.x == 0 && a.sentinel) *a.sentinel = 0;
+  }
   load_crc_lds(lds);
 
   const int lane = threadIdx.x & 63;
