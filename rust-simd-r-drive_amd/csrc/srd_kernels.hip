@@ -366,15 +366,15 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // timing experiments (SRD_ABLATE_NOLOAD builds only): runtime ablation
   // bits; otherwise a compile-time 0, so no branch splits the tile's
   // straight-line code (CRC, lane weights, suffix XOR, filter) into blocks
-#ifdef SRD_ABLATE_NOLOAD
+#if defined(SRD_ABL_CT)
+  constexpr uint32_t ABL = SRD_ABL_CT;  // compile-time ablation variant (no runtime branches)
+#elif defined(SRD_ABLATE_NOLOAD)
   const uint32_t ABL = a.ablate;
 #else
   constexpr uint32_t ABL = 0;
 #endif
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
-#ifdef SRD_ABLATE_NOLOAD
-    if (a.ablate & 16) k = k0;  // timing experiment: compute-only (re-reads one L2-resident tile)
-#endif
+    if (ABL & 16) k = k0;  // timing experiment: compute-only (re-reads one L2-resident tile)
     const u32x4* q = (const u32x4*)(file + k * (uint64_t)TILE + 64ull * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {

@@ -55,7 +55,7 @@ def test_layout_matches_reference_arithmetic(tail):
     assert nt == want
     for i, p in enumerate(pays):
         assert ents[i].tail == tails[i]
-        assert ents[i].tomb == (1 if p == b"\x00" else 0)
+        assert ents[i].flags == (1 if p == b"\x00" else 0)
         assert ents[i].len == len(p) and ents[i].key_len == len(keys[i])
 
 
@@ -66,10 +66,10 @@ def test_layout_errors():
         S.batch_layout(0, [b"k"], [b"\x00"])
     # with allow_null (the delete path) the NULL byte is a tombstone
     ents, nt = S.batch_layout(0, [b"k"], [b"\x00"], allow_null=True)
-    assert ents[0].tomb == 1 and nt == 21
+    assert ents[0].flags == 1 and nt == 21
     # a zero byte inside a longer payload is data, not a tombstone
     ents, nt = S.batch_layout(0, [b"k"], [b"\x00\x00"])
-    assert ents[0].tomb == 0 and nt == 22
+    assert ents[0].flags == 0 and nt == 22
 
 
 # ---------------------------------------------------------------------------- GPU
