@@ -733,20 +733,49 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     process(k0 + j + 3, Dv, body);
   }
 #else
+  // vmcnt counts loads and stores in issue order, and the compiler's wait
+  // counts at the loop header are the minimum over its entries.  In the
+  // steady state every tile's loads are followed by process()'s 5
+  // unconditional stores (tile values, span records, span count); without
+  // them on the entry path the first iteration's shorter queue sets every
+  // wait of the loop, which then waits for part of the next tile early.
+  // Dummy stores (out-of-range offsets: dropped by the hardware; distinct,
+  // or the compiler merges them as dead stores) give the entry the same queue.
+  auto pad_stores = [&](uint32_t g) {
+#ifndef SRD_NO_PAD
+    constexpr uint32_t NST = 5u;  // process()'s unconditional stores
+#pragma unroll
+    for (uint32_t i = 0; i < NST; i++)
+      __builtin_amdgcn_raw_buffer_store_b32(0u, out_rsrc(a.tile, 256), OOB_OFF - 64u * (NST * g + i), 0, 0);
+#endif
+  };
+  // Whole rounds of 3 tiles only: a break between the tiles of a round
+  // reaches the loop latch, and that (never taken) latch -> header path
+  // would shorten the compiler's wait counts as well.  The <= 2 remaining
+  // ring tiles run in the unpipelined loop below with the file's tail tiles.
+  const uint32_t nfull = nk / 3;
   load_tile(k0, A);
+  pad_stores(0);
   load_tile(k0 + 1, Bv);
-  for (uint32_t j = 0; j < nk; j += 3) {
+  pad_stores(1);
+  for (uint32_t i = 0; i < nfull; i++) {
+    const uint32_t j = 3 * i;
     load_tile(k0 + min(j + 2, nk), Cv);
     process(k0 + j, A, body);
-    if (j + 1 >= nk) break;
     load_tile(k0 + min(j + 3, nk), A);
     process(k0 + j + 1, Bv, body);
-    if (j + 2 >= nk) break;
     load_tile(k0 + min(j + 4, nk), Bv);
     process(k0 + j + 2, Cv, body);
   }
 #endif
-  for (uint64_t k = km; k < k1; k++) {  // the file's last <= 2 tiles
+#if SRD_RING == 4
+  const uint64_t kr = km;
+#else
+  const uint64_t kr = k0 + 3ull * nfull;
+#endif
+  // the ring's remainder and the file's last <= 2 tiles (masked: a tail
+  // tile's bytes past file_len read as 0; a no-op on the others)
+  for (uint64_t k = kr; k < k1; k++) {
     load_tile(k, A);
     process(k, A, std::true_type{});
   }
