@@ -459,7 +459,7 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
     KCHK(c, "finalize_kernel");
     HIPCHK(hipGetLastError());
     if (!f.no_crc) {
-      slow_kernel<<<2048, 64, 0, c->stream>>>(f);
+      slow_kernel<<<2048 / SLOW_WAVES, SLOW_WAVES * 64, 0, c->stream>>>(f);
       KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
     }
@@ -821,7 +821,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.n_bad = (unsigned long long*)&pl->n_bad;
       finalize_kernel<<<2048, 256, 0, c->stream>>>(f);
       KCHK(c, "finalize_kernel");
-      if (!f.no_crc) slow_kernel<<<2048, 64, 0, c->stream>>>(f);
+      if (!f.no_crc) slow_kernel<<<2048 / SLOW_WAVES, SLOW_WAVES * 64, 0, c->stream>>>(f);
       KCHK(c, "slow_kernel");
       HIPCHK(hipGetLastError());
       // ---- KeyIndexer::build (bucketed; SRD_INDEX_GLOBAL=1: one global table, timing experiments) ----

@@ -1099,6 +1099,25 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
       pieces |= 1;
     }
   }
+  // A piece no record holds (the root entry's metadata-line suffix, its
+  // child's start-line suffix: the root has no candidate record) comes from
+  // the per-tile values when its line is 0, 1 or 32 of the tile (C1/C2/C5:
+  // root metadata at 4096, the child's start at 4160); else slow_kernel
+  // recomputes it
+  if (!(pieces & 1)) {
+    const uint64_t k = start / TILE;
+    const uint32_t j = (uint32_t)((start % TILE) / 64);
+    if (j == 0) { suf = tile_T(a.tile, k); pieces |= 1; }
+    else if (j == 1) { suf = tile_SX1(a.tile, k); pieces |= 1; }
+    else if (j == 32) { suf = a.tile[4 * k + 2]; pieces |= 1; }
+  }
+  if (!(pieces & 2)) {
+    const uint64_t k = mo / TILE;
+    const uint32_t j = (uint32_t)((mo % TILE) / 64);
+    if (j == 0) { sxm = tile_T(a.tile, k); pieces |= 2; }
+    else if (j == 1) { sxm = tile_SX1(a.tile, k); pieces |= 2; }
+    else if (j == 32) { sxm = a.tile[4 * k + 2]; pieces |= 2; }
+  }
   len = mo - start;
   a.o_mo[c] = mo;
   a.o_kh[c] = kh;
@@ -1207,17 +1226,21 @@ __device__ uint32_t crc_from_pieces_wave(uint64_t s, uint64_t m, uint32_t suf, u
 
 // one wave per slow entry (a piece of the combine was not recorded, or the
 // entry spans more than LONG_TILES whole tiles)
-__global__ __launch_bounds__(64) void slow_kernel(FinArgs a) {
+// (SLOW_WAVES waves per block share the LDS tables; few blocks keep the
+// launch cheap when the list is empty, the common case)
+constexpr int SLOW_WAVES = 4;
+__global__ __launch_bounds__(SLOW_WAVES * 64) void slow_kernel(FinArgs a) {
   __shared__ uint32_t tab[1024];
   __shared__ uint32_t mx[1024];
   const unsigned long long ns = *a.n_slow;
-  if (blockIdx.x >= ns) return;
-  for (int i = threadIdx.x; i < 1024; i += 64) {
+  if ((uint64_t)blockIdx.x * SLOW_WAVES >= ns) return;
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
     tab[i] = g_tabs.tab[i >> 8][i & 255];
     mx[i] = (&g_tabs.mx64[0][0])[i];
   }
   __syncthreads();
-  for (uint64_t w = blockIdx.x; w < ns; w += gridDim.x) {
+  for (uint64_t w = (uint64_t)blockIdx.x * SLOW_WAVES + (threadIdx.x >> 6); w < ns;
+       w += (uint64_t)gridDim.x * SLOW_WAVES) {
     const uint64_t c = a.slow_list[w];
     const uint64_t s = a.o_start[c], m = a.o_mo[c];
     uint32_t pieces = a.o_pieces[c], suf = a.o_suf[c], sxm = a.o_sxm[c], tail = a.o_tail[c];

@@ -136,6 +136,16 @@ def test_mixed_sizes(ctx, flags):
     check_against_oracle(O.synth_store(len(lens), lens=lens), ctx, flags, "zipf")
 
 
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_root_entry_metadata_lines(ctx, flags):
+    # the root entry (prev 0) has no candidate record: finalize takes its
+    # metadata-line suffix from the per-tile values for lines 0 / 1 / 32 of a
+    # tile, the slow kernel otherwise -- every first-entry length class
+    for first in [4096, 8192, 64, 100, 127, 2048, 2100, 4160, 4200, 6144 + 40, 12288, 3000, 20, 63, 1 << 17]:
+        lens = np.array([first] + [4096, 77, 2048, 5000] * 3, np.uint64)
+        check_against_oracle(O.synth_store(len(lens), lens=lens), ctx, flags, f"root{first}")
+
+
 def test_tombstones_and_overwrites_random(ctx):
     rnd = random.Random(11)
     buf = bytearray()
