@@ -183,6 +183,13 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
       node = p >= 20 && p < m && (tomb || dp > prepad64(p));
       a.c_rec[2 * gi] = u32x4{r0[0], r0[1], (uint32_t)kh, (uint32_t)(kh >> 32)};
       a.c_rec[2 * gi + 1] = u32x4{crc, r1[1], r1[2], (r1[3] & ~F_LEAN) | (tomb ? F_TOMB : 0u)};
+    } else if (r1[3] & F_NT) {
+      // full record, deferred node test (data_store.rs:404-470); F_ZB is the
+      // byte at m - 1, the tombstone byte when p == m - 1
+      const uint64_t dp = m - p;
+      const bool tomb = dp == 1 && (r1[3] & F_ZB);
+      node = p >= 20 && p < m && (tomb || dp > prepad64(p));
+      if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
     }
     const uint64_t mp = p - 20;  // p >= 20 for nodes
     const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)

@@ -41,7 +41,8 @@ constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
 #define SRD_CRC_LINE crc_line4
 #endif
 #ifndef SRD_LEAN
-#define SRD_LEAN 0  // 1: single-candidate records without key_hash / crc (link2_kernel reads them)
+#define SRD_LEAN 2  // single-candidate records: 0 full, node test in the scan; 1 without key_hash / crc
+                    // (link2_kernel reads them from the file); 2 full, node test deferred to link2_kernel
 #endif
 #ifndef SRD_RING
 #define SRD_RING 3
@@ -65,6 +66,9 @@ constexpr uint32_t F_SXM_LO = 32u, F_SUF_LO = 64u;
 // {-, sxm, suf, flags} are written; link2_kernel reads key_hash / crc from
 // the file, applies the node test and completes the record (clearing F_LEAN)
 constexpr uint32_t F_LEAN = 128u;
+// SRD_LEAN 2: full record whose node test link2_kernel applies (F_NT); F_ZB =
+// the byte at m - 1 is 0 (the tombstone rule's byte when p == m - 1)
+constexpr uint32_t F_NT = 256u, F_ZB = 512u;
 
 struct DevTables {
   uint32_t tab[4][256];
@@ -355,9 +359,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
   uint32_t tacc = 0, scnt = 0;
-  uint32_t rq[SRD_LEAN ? 7 : 10];
+  uint32_t rq[SRD_LEAN == 1 ? 7 : 10];
 #pragma unroll
-  for (int i = 0; i < (SRD_LEAN ? 7 : 10); i++) rq[i] = 0;
+  for (int i = 0; i < (SRD_LEAN == 1 ? 7 : 10); i++) rq[i] = 0;
   uint64_t rvalid = 0;  // wave-uniform: record slots buffered in rq
 
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
@@ -567,7 +571,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const int rs = 64 * f + bl - 14;
           const uint64_t m = B + (int64_t)rs;
           const uint32_t s2 = __builtin_amdgcn_readlane(f2, bl), s3 = __builtin_amdgcn_readlane(f3, bl);  // p
-#if !SRD_LEAN
+#if SRD_LEAN == 0
           // full record: the node test here (data_store.rs:404-470) and the
           // key hash / crc from the window
           const uint64_t p = (uint64_t)s2 | ((uint64_t)s3 << 32);
@@ -580,6 +584,15 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const uint32_t s1 = __builtin_amdgcn_readlane(alignb(W[2], W[1], sh), bl);
           const uint32_t s4 = __builtin_amdgcn_readlane(f4, bl);
           constexpr uint32_t REC_KIND = 0u;
+#elif SRD_LEAN == 2
+          // full record, node test deferred to link2_kernel (F_NT)
+          const uint32_t os = (uint32_t)bl + 2;
+          const uint32_t stb = (__builtin_amdgcn_readlane(tdw, bl) >> (((os - 1) & 3) * 8)) & 0xffu;
+          const uint32_t s0 = __builtin_amdgcn_readlane(alignb(W[1], W[0], sh), bl);
+          const uint32_t s1 = __builtin_amdgcn_readlane(alignb(W[2], W[1], sh), bl);
+          const uint32_t s4 = __builtin_amdgcn_readlane(f4, bl);
+          constexpr bool tomb = false;
+          const uint32_t REC_KIND = F_NT | (stb == 0 ? F_ZB : 0u);
 #else
           constexpr uint32_t s0 = 0u, s1 = 0u, s4 = 0u;
           constexpr bool tomb = false;
@@ -606,7 +619,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
               rq[4] = mine ? fl : rq[4];
               rq[5] = mine ? s2 : rq[5];
               rq[6] = mine ? s3 : rq[6];
-#if !SRD_LEAN
+#if SRD_LEAN != 1
               rq[7] = mine ? s0 : rq[7];
               rq[8] = mine ? s1 : rq[8];
               rq[9] = mine ? s4 : rq[9];
@@ -675,7 +688,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const bool w = span_end && ((rvalid >> lane) & 1);
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + span * a.cap, 64 * 8),
                                             w ? 8u * lane : OOB_OFF, 0, 0);
-#if SRD_LEAN  // lean records: link2_kernel completes key_hash and crc
+#if SRD_LEAN == 1  // lean records: link2_kernel completes key_hash and crc
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[5], rq[6]}, out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
                                             w ? 32u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, rq[2], rq[3], rq[4]},
