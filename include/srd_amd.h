@@ -126,6 +126,17 @@ int srd_validate_span_device(srd_ctx *ctx, const uint8_t *d_span,
                              uint64_t span_off, uint64_t lo, uint64_t hi,
                              uint32_t flags, srd_device_result *out);
 
+/* Shard boundaries of an arbitrary store (host pre-pass, no GPU): cuts[0] = 0,
+ * cuts[world] = file_len, and cuts[r] (0 < r < world) the highest byte t at
+ * or below r * file_len / world (searched down to 64 MiB below it) whose
+ * backward walk passes recover_valid_chain's node test (data_store.rs:404-470)
+ * for 8 hops without reaching offset 0.  Non-decreasing; a cut with no candidate repeats the previous
+ * one (an empty shard).  The cuts are guesses that srd_validate_span_device
+ * plus the composition check prove or refute: [cuts[r], cuts[r+1]) are rank
+ * r's lo / hi. */
+int srd_shard_cuts(const uint8_t *file, uint64_t file_len, uint32_t world,
+                   uint64_t *cuts);
+
 /* Index exchange between shards (KeyIndexer semantics, key_indexer.rs:98-124).
  * Partition n (key_hash, value) pairs (device arrays) by owner rank
  * owner = ((key_hash >> 32) * world) >> 32 into d_out_pairs ([2n] u64,

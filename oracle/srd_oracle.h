@@ -28,7 +28,7 @@ extern "C" {
 #define ORC_METADATA_SIZE 20u
 #define ORC_PAYLOAD_ALIGNMENT 64u
 
-/* ---- digest (src/storage_engine/digest/*) ---- */
+/* ---- digest (src/storage_engine/digest/) ---- */
 uint64_t orc_xxh3_64(const void *data, size_t len);
 void orc_xxh3_64_batch(const uint8_t *buf, const uint64_t *offs,
                        const uint64_t *lens, uint64_t n, uint64_t *out);
@@ -37,7 +37,7 @@ uint32_t orc_crc32_update(uint32_t crc, const void *data, size_t len);
 uint32_t orc_crc32_table(const void *data, size_t len); /* portable slice-by-8 */
 int orc_has_pclmul(void);
 
-/* ---- format (simd-r-drive-entry-handle/src/*) ---- */
+/* ---- format (simd-r-drive-entry-handle/src/) ---- */
 uint64_t orc_prepad_len(uint64_t offset);
 
 /* ---- writer (data_store.rs:847-939) ----

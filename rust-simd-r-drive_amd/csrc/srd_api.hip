@@ -1107,6 +1107,63 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
 
 extern "C" uint64_t srd_padded_size(uint64_t flen) { return ((flen + TILE - 1) / TILE) * TILE + 2 * TILE; }
 
+// ---------------------------------------------------------- shard boundaries
+// Host pre-pass for the entry-range shards of an arbitrary store (SURVEY.md
+// 8(e)): cut r is a guessed entry tail at or below r*file_len/world.  A byte
+// t is taken as a tail when [t-20, t) passes recover_valid_chain's node test
+// (data_store.rs:404-421, 429-470) and the backward walk from it stays valid
+// for kCutHops hops without reaching offset 0 (so the first 8 entries are
+// never a cut).  The guess is checked, not trusted: the shards' chains
+// compose only if every cut is the tail the real chain passes through
+// (srd_shard.sharded_validate_index), and otherwise the caller runs the
+// whole-file path.
+static inline uint64_t host_rd64(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+
+static bool host_node(const uint8_t* f, uint64_t flen, uint64_t t, uint64_t* prev) {
+  if (t < 20 || t > flen) return false;
+  const uint64_t mo = t - 20, p = host_rd64(f + mo + 8);
+  if (p >= mo) return false;
+  const uint64_t start = (mo - p == 1 && f[p] == 0) ? p : p + ((64 - (p & 63)) & 63);
+  if (start >= mo) return false;
+  *prev = p;
+  return true;
+}
+
+static constexpr int kCutHops = 8;
+static constexpr uint64_t kCutScan = 64ull << 20;  // bytes searched below a cut target
+
+static bool plausible_tail(const uint8_t* f, uint64_t flen, uint64_t t) {
+  uint64_t cur = t;
+  for (int h = 0; h < kCutHops; h++) {
+    uint64_t p;
+    if (!host_node(f, flen, cur, &p)) return false;
+    // p == 0 is what zero-filled payloads (and crc bytes read through a
+    // zero prepad) look like: a walk that reaches the root early is no cut
+    if (p == 0) return false;
+    cur = p;
+  }
+  return true;
+}
+
+extern "C" int srd_shard_cuts(const uint8_t* file, uint64_t flen, uint32_t world, uint64_t* cuts) {
+  if (!cuts || world == 0 || (!file && flen)) { set_err("bad argument"); return SRD_ERR_ARG; }
+  cuts[0] = 0;
+  cuts[world] = flen;
+  for (uint32_t r = 1; r < world; r++) {
+    const uint64_t target = (uint64_t)(((unsigned __int128)flen * r) / world);
+    const uint64_t floor_ = std::max(cuts[r - 1], target > kCutScan ? target - kCutScan : 0);
+    uint64_t got = cuts[r - 1];  // none found: an empty shard
+    for (uint64_t t = target; t > floor_; t--)
+      if (plausible_tail(file, flen, t)) { got = t; break; }
+    cuts[r] = got;
+  }
+  return 0;
+}
+
 // ---------------------------------------------------------------- host input
 static int stage_file(Ctx* c, const uint8_t* file, uint64_t flen, const uint8_t** d) {
   const uint64_t need = srd_padded_size(flen);

@@ -51,6 +51,7 @@ EXPORTS = [
     "srd_index_table_bytes", "srd_index_table_build_device", "srd_index_get_packed_device",
     "srd_batch_read_hashed_device", "srd_batch_read",
     "srd_iter_entries_device", "srd_estimate_compaction_savings_device", "srd_compact_device",
+    "srd_shard_cuts",
 ]
 
 
@@ -109,6 +110,7 @@ def lib():
         L.srd_padded_size.restype = u64
         L.srd_synth_store_device.argtypes = [vp, vp, u64, u64, vp, u64, C.POINTER(u64)]
         L.srd_validate_span_device.argtypes = [vp, vp, u64, u64, u64, u32, C.POINTER(DeviceResult)]
+        L.srd_shard_cuts.argtypes = [vp, u64, u32, vp]
         L.srd_index_partition_device.argtypes = [vp, vp, vp, u64, u32, vp, vp]
         L.srd_index_build_device.argtypes = [vp, vp, u64, vp, vp, C.POINTER(u64)]
         L.srd_synth_span_device.argtypes = [vp, vp, u64, u64, u64, u64, vp, u64, C.POINTER(u64), C.POINTER(u64)]
@@ -482,6 +484,15 @@ class DataStore:
 
     def len(self) -> int:
         return len(self.key_indexer)
+
+
+def shard_cuts(file: np.ndarray, world: int) -> list[int]:
+    """Entry-tail cuts [0, c_1, .., file_len] splitting a host store into
+    `world` byte-balanced entry ranges (host pre-pass, srd_shard_cuts)."""
+    f = np.ascontiguousarray(file, dtype=np.uint8)
+    cuts = np.zeros(world + 1, np.uint64)
+    _check(lib().srd_shard_cuts(f.ctypes.data, f.size, world, cuts.ctypes.data))
+    return [int(x) for x in cuts]
 
 
 def padded_size(file_len: int) -> int:

@@ -99,6 +99,39 @@ class HipBackend:
         return ok[:ni], op[:ni]
 
 
+def plan_byte_shards(file: np.ndarray, world: int) -> list[tuple[int, int]]:
+    """(lo, hi) entry tails per rank for an arbitrary host store: the cuts of
+    the host pre-pass srd_shard_cuts (byte-balanced guesses that the
+    composition check below proves or refutes)."""
+    c = S.shard_cuts(file, world)
+    return [(c[r], c[r + 1]) for r in range(world)]
+
+
+def span_of(lo: int) -> int:
+    """First byte a rank holds: lo rounded down to the span alignment (16 KiB)."""
+    return lo - lo % S.SPAN_ALIGN
+
+
+def sharded_open_host(backend, file: np.ndarray, group=None) -> ShardedResult:
+    """DataStore::open over a host store (the mmap) on W ranks: every rank
+    computes the same cuts, copies its span [span_off, hi) into its HBM and
+    joins sharded_validate_index.  `composed` False (a torn tail, corruption or
+    a cut that is not a real chain tail) means the whole-file path decides."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, hi = plan_byte_shards(file, world)[rank]
+    span_off = span_of(lo)
+    dev = backend_device(backend)
+    buf = torch.zeros(S.padded_size(hi - span_off) if hi > lo else 1, dtype=torch.uint8, device=dev)
+    if hi > lo:
+        buf[: hi - span_off].copy_(torch.from_numpy(np.ascontiguousarray(file[span_off:hi])))
+    return sharded_validate_index(backend, buf, span_off, lo, hi, int(file.size), group)
+
+
+def backend_device(backend) -> torch.device:
+    d = getattr(backend, "device", None)
+    return torch.device("cpu") if d is None else torch.device("cuda", d) if isinstance(d, int) else torch.device(d)
+
+
 def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, hi: int, file_len: int,
                            group=None) -> ShardedResult:
     """One rank's part of the sharded open: validate its shard, check the
@@ -108,7 +141,12 @@ def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, h
     # collectives run where the backend lives: device memory for nccl (RCCL
     # over xGMI), host memory for gloo (CPU tests, several ranks on one GPU)
     cd = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
-    st, keys, packed, local = backend.validate_span(buf, span_off, lo, hi)
+    if lo == hi:  # an empty shard (srd_shard_cuts found no tail in its range): composes trivially
+        st = ShardStatus(True, lo, hi, 0, 0)
+        keys = packed = torch.empty(0, dtype=torch.int64, device=dev)
+        local = None
+    else:
+        st, keys, packed, local = backend.validate_span(buf, span_off, lo, hi)
     # 1. boundaries
     mine = torch.tensor([int(st.proven), st.lo, st.hi, st.n_chain, st.n_crc_bad], dtype=torch.int64, device=cd)
     allst = torch.empty(world * 5, dtype=torch.int64, device=cd)
@@ -122,7 +160,10 @@ def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, h
         empty = torch.empty(0, dtype=torch.int64, device=dev)
         return ShardedResult(0, False, 0, 0, 0, empty, empty, local)
     # 2. index exchange
-    pairs, counts = backend.partition(keys, packed, world)
+    if keys.numel():
+        pairs, counts = backend.partition(keys, packed, world)
+    else:
+        pairs, counts = torch.empty(0, dtype=torch.int64, device=dev), [0] * world
     send = torch.tensor(counts, dtype=torch.int64, device=cd)
     recv = torch.empty(world, dtype=torch.int64, device=cd)
     dist.all_to_all_single(recv, send, group=group)

@@ -65,3 +65,84 @@ def test_sharded_open_two_processes(world):
         assert not (merged.keys() & idx.keys())
         merged.update(idx)
     assert merged == want
+
+
+def _host_worker(rank, world, port, store_bytes, q):
+    """sharded_open_host on the product path: cuts from srd_shard_cuts, the
+    rank's span copied from the host store into HBM, HipBackend."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import srd_amd as S
+    import srd_shard as SH
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        ctx = S.Context(0)
+        store = np.frombuffer(store_bytes, np.uint8)
+        res = SH.sharded_open_host(SH.HipBackend(ctx, 0), store)
+        q.put((rank, res.composed, res.final_len, res.n_chain, res.n_crc_bad, res.n_index,
+               dict(zip(res.owner_keys.cpu().numpy().view(np.uint64).tolist(),
+                        res.owner_packed.cpu().numpy().view(np.uint64).tolist()))))
+        torch.cuda.synchronize()
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_host(world, store):
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_host_worker, args=(r, world, port, store.tobytes(), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return out
+
+
+def _zipf_host_store(n=1500):
+    import srd_amd as S
+    import oracle as O
+    return O.synth_store(n, lens=S.zipf_lens(n, s=2.0))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_open_host_zipf(world):
+    """Arbitrary store (C3's Zipf sizes, 64 B .. 1 MiB, unaligned tails): byte
+    cuts guessed by the host pre-pass, proven by the shards; the merged index
+    equals the oracle's whole-file KeyIndexer::build."""
+    import oracle as O
+    store = _zipf_host_store()
+    out = _run_host(world, store)
+    want = O.key_indexer_build(store, store.size)
+    merged = {}
+    for rank, composed, final_len, n_chain, n_bad, n_index, idx in out:
+        assert (composed, final_len, n_chain, n_bad, n_index) == (True, store.size, 1500, 0, len(want))
+        assert not (merged.keys() & idx.keys())
+        merged.update(idx)
+    assert merged == want
+
+
+def test_sharded_open_host_refutes_bad_cuts():
+    """A forged tail under the cut target, and a torn tail: the shards do not
+    compose, so the whole-file path decides (checked here against the oracle)."""
+    import oracle as O
+    import srd_amd as S
+    from test_shard_gloo import fake_cut_store
+    fake, _ = fake_cut_store()
+    torn = np.concatenate([_zipf_host_store(600), np.frombuffer(b"CORRUPT", np.uint8)])
+    for store in (fake, torn):
+        out = _run_host(2, store)
+        assert all(not composed for _, composed, *_ in out)
+        r = S.validate_index(store)
+        assert r.final_len == O.recover_valid_chain(store)
+        assert r.index() == O.key_indexer_build(store, r.final_len)

@@ -138,3 +138,135 @@ def test_sharded_torn_tail_is_not_composed():
     store = _store()
     out = _run(2, store, [0, 150, 300], torn=9)
     assert all(not composed for _, composed, *_ in out)
+
+
+# ---- shard boundaries of an arbitrary store (srd_shard_cuts host pre-pass)
+
+def _zipf_store(n=400):
+    import srd_amd as S
+    import oracle as O
+    lens = S.zipf_lens(n, s=2.0)
+    lens = np.minimum(lens, 1 << 16)  # keep the CPU oracle fast; still 64 B .. 64 KiB, unaligned tails
+    return O.synth_store(n, lens=lens)
+
+
+def _true_tails(store):
+    import oracle as O
+    t = O.recover_valid_chain(store)
+    return {0} | {e["meta_off"] + 20 for e in O.chain(store, t, compute_crc=False)}
+
+
+@pytest.mark.parametrize("name", ["mixed", "zipf", "alignment", "tombstones", "overwrite_delete", "nested"])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_shard_cuts_are_chain_tails(name, world):
+    sys.path[:0] = [os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    import srd_amd as S
+    if name == "mixed":
+        store = _store()
+    elif name == "zipf":
+        store = _zipf_store()
+    else:
+        store = np.fromfile(os.path.join(ROOT, "tests", "golden", name + ".bin"), np.uint8)
+    cuts = S.shard_cuts(store, world)
+    assert len(cuts) == world + 1 and cuts[0] == 0 and cuts[-1] == store.size
+    assert cuts == sorted(cuts)
+    tails = _true_tails(store)
+    assert set(cuts[:-1]) <= tails, (cuts, sorted(tails)[:20])
+    if store.size > 1 << 20:  # large stores: every target has a tail within one entry below it
+        assert len(set(cuts)) == world + 1
+
+
+def test_shard_cuts_edge_cases():
+    sys.path[:0] = [os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    import srd_amd as S
+    assert S.shard_cuts(np.zeros(0, np.uint8), 4) == [0, 0, 0, 0, 0]
+    z = np.zeros(100000, np.uint8)  # zero bytes look like p == 0 nodes everywhere: never a cut
+    assert S.shard_cuts(z, 3) == [0, 0, 0, z.size]
+    g = np.fromfile(os.path.join(ROOT, "tests", "golden", "garbage_1k.bin"), np.uint8)
+    c = S.shard_cuts(g, 2)
+    assert c[0] == 0 and c[-1] == g.size
+
+
+def _host_worker(rank, world, port, store_bytes, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import srd_shard as SH
+        store = np.frombuffer(store_bytes, np.uint8)
+        res = SH.sharded_open_host(OracleBackend(store), store)
+        q.put((rank, res.composed, res.final_len, res.n_chain, res.n_index,
+               dict(zip(res.owner_keys.numpy().view(np.uint64).tolist(), res.owner_packed.numpy().view(np.uint64).tolist()))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_open_host_byte_cuts(world):
+    """Arbitrary store (Zipf sizes, unaligned tails): cuts from the pre-pass,
+    spans copied from the host store, index equal to the whole-file build."""
+    import oracle as O
+    store = _zipf_store()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_worker, args=(r, world, port, store.tobytes(), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    want = O.key_indexer_build(store, store.size)
+    merged = {}
+    for rank, composed, final_len, n_chain, n_index, idx in out:
+        assert composed and final_len == store.size and n_chain == 400 and n_index == len(want)
+        assert not (merged.keys() & idx.keys())
+        merged.update(idx)
+    assert merged == want
+
+
+def fake_cut_store():
+    """A store whose byte-balanced cut lands in a 200 KB payload that holds a
+    forged metadata record (prev = the real previous tail) below the target:
+    srd_shard_cuts picks the forged tail, and composition must refute it."""
+    import oracle as O
+    rnd = np.random.default_rng(7)
+
+    def build(fake_off):
+        buf, t = bytearray(), 0
+        for i in range(30):
+            t = O.write_entries(buf, t, [(1000 + i, rnd.bytes(4096))])
+        t_prev = t
+        big = bytearray(rnd.bytes(200000))
+        if fake_off is not None:
+            big[fake_off:fake_off + 20] = (77).to_bytes(8, "little") + t_prev.to_bytes(8, "little") + b"\x01\x02\x03\x04"
+        t = O.write_entries(buf, t, [(2000, bytes(big))])
+        for i in range(30):
+            t = O.write_entries(buf, t, [(3000 + i, rnd.bytes(4096))])
+        return np.frombuffer(bytes(buf), np.uint8), t_prev
+
+    s, t_prev = build(None)
+    start = t_prev + ((64 - t_prev % 64) % 64)
+    off = s.size // 2 - start - 520
+    s, _ = build(off)
+    return s, start + off + 20
+
+
+def test_fake_tail_cut_is_refuted():
+    sys.path[:0] = [os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    import srd_amd as S
+    store, fake = fake_cut_store()
+    assert S.shard_cuts(store, 2)[1] == fake
+    assert fake not in _true_tails(store)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_worker, args=(r, 2, port, store.tobytes(), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(not composed for _, composed, *_ in out)
