@@ -222,13 +222,18 @@ def bench_ops(args, ctx, local):
     t_iter = timed(it)
     assert nn.value == n
     t_sav = timed(lambda: S.estimate_compaction_savings_device(store.data_ptr(), size, packed.data_ptr(), n, ctx))
-    cout = torch.empty(size + 64, dtype=torch.uint8, device=dev)
+    cout = torch.empty(S.padded_size(size), dtype=torch.uint8, device=dev)
     nl = C.c_uint64()
 
     def compact():
         S._check(S.lib().srd_compact_device(ctx.h, C.c_void_p(store.data_ptr()), size, C.c_void_p(packed.data_ptr()),
                                             n, C.c_void_p(cout.data_ptr()), size + 64, C.byref(nl), None, None))
     t_comp = timed(compact, 3)
+    # the compacted store reopens to the same live key set, every CRC valid
+    r2 = S.validate_index_device(cout.data_ptr(), nl.value, 0, ctx)
+    assert (r2.final_len, r2.n_chain, r2.n_crc_bad, r2.n_index) == (nl.value, n, 0, n)
+    k2 = torch.from_numpy(S.device_to_numpy(r2.index_key_hash, n).view(np.int64)).to(dev)
+    assert torch.equal(torch.sort(k2).values, torch.sort(keys).values)
     res = {
         "metric": "device index + iterator + compaction ops on the C2 store (8(f) rows 2-4)",
         "config": {"workload": f"C2: {n} x 4096 B entries, {size} B store, every key live", "entries": n},

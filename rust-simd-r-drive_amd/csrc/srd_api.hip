@@ -102,7 +102,7 @@ enum BufId {
   B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
   B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
-  B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT,
+  B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_COUNT_
 };
 
@@ -1692,32 +1692,39 @@ extern "C" int srd_compact_device(srd_ctx* c, const uint8_t* d_file, uint64_t fl
   uint64_t nv = 0;
   TRY(iter_run(c, d_file, flen, d_packed, n_index, P<uint64_t>(c, B_IT_OST), P<uint64_t>(c, B_IT_OEN), nullptr,
                P<uint64_t>(c, B_IT_OKH), &nv, nullptr));
-  // layout of the compacted file: write_stream_with_key_hash per entry in
-  // iter_entries order (data_store.rs:706-719, 758-825), tail from 0
-  std::vector<uint64_t> st(nv), en(nv), kh(nv);
-  if (nv) {
-    HIPCHK(hipMemcpyAsync(st.data(), P<uint64_t>(c, B_IT_OST), nv * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(en.data(), P<uint64_t>(c, B_IT_OEN), nv * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(kh.data(), P<uint64_t>(c, B_IT_OKH), nv * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-  }
-  std::vector<srd_write_entry> E(nv);
-  uint64_t tail = 0;
-  for (uint64_t j = 0; j < nv; j++) {
-    E[j] = srd_write_entry{st[j], en[j] - st[j], kh[j], tail, 0u, SRD_ENTRY_HASHED};
-    tail += ((64 - (tail & 63)) & 63) + (en[j] - st[j]) + 20;
-  }
-  *new_len = tail;
-  if (!d_out || !nv) return 0;
-  if (tail > out_cap) { set_err("out_cap too small for the compacted store"); return SRD_ERR_ARG; }
+  // layout of the compacted file on the device: write_stream_with_key_hash
+  // per entry in iter_entries order (data_store.rs:706-719, 758-825), tail
+  // from 0 -- a prefix sum (compact_sizes_kernel), then the write entries
+  if (!nv) return 0;
+  const uint64_t* st = P<uint64_t>(c, B_IT_OST);
+  const uint64_t* en = P<uint64_t>(c, B_IT_OEN);
+  TRY(ensure(c, B_IT_RLEN, nv * 8));
+  TRY(ensure(c, B_IT_PST, nv * 8));
   TRY(ensure(c, B_IT_ENT, nv * sizeof(srd_write_entry)));
+  TRY(ensure(c, B_IT_KEPT, 64));
+  size_t tb = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)nv));
+  TRY(ensure(c, B_CUB_TMP, tb + 256));
+  tb = c->bufs[B_CUB_TMP].n;
+  compact_sizes_kernel<<<grid_for(nv), 256, 0, c->stream>>>(st, en, nv, P<uint64_t>(c, B_IT_RLEN));
+  KCHK(c, "compact_sizes_kernel");
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint64_t>(c, B_IT_RLEN),
+                                          P<uint64_t>(c, B_IT_PST), (int)nv, c->stream));
+  uint64_t* d_new_len = P<uint64_t>(c, B_IT_KEPT) + 2;
+  compact_entries_kernel<<<grid_for(nv), 256, 0, c->stream>>>(st, en, P<uint64_t>(c, B_IT_OKH), P<uint64_t>(c, B_IT_PST),
+                                                             nv, P<srd_write_entry>(c, B_IT_ENT), d_new_len);
+  KCHK(c, "compact_entries_kernel");
+  HIPCHK(hipGetLastError());
+  uint64_t tail = 0;
+  HIPCHK(hipMemcpyAsync(&tail, d_new_len, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *new_len = tail;
+  if (!d_out) return 0;
+  if (tail > out_cap) { set_err("out_cap too small for the compacted store"); return SRD_ERR_ARG; }
   TRY(ensure(c, B_WKH, nv * 8));
   TRY(ensure(c, B_WMO, nv * 8));
-  TRY(ensure(c, B_IT_KEPT, 64));
   unsigned int* nullf = (unsigned int*)(P<uint8_t>(c, B_IT_KEPT) + 8);
   HIPCHK(hipMemsetAsync(nullf, 0, 4, c->stream));
-  HIPCHK(hipMemcpyAsync(P<void>(c, B_IT_ENT), E.data(), nv * sizeof(srd_write_entry), hipMemcpyHostToDevice,
-                        c->stream));
   TRY(launch_write(c, c->stream, d_file, nullptr, P<srd_write_entry>(c, B_IT_ENT), nv, d_out, 0,
                    d_key_hash_out ? d_key_hash_out : P<uint64_t>(c, B_WKH),
                    d_meta_off_out ? d_meta_off_out : P<uint64_t>(c, B_WMO), nullf));

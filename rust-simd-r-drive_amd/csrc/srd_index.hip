@@ -126,4 +126,23 @@ __global__ void batch_read_kernel(const uint64_t* tkeys, const uint64_t* tpacked
   }
 }
 
+// compact's layout (data_store.rs:706-719 -> write_stream_with_key_hash per
+// entry, :758-825, tail from 0): entry j's payload starts at
+// P_j = roundup64(tail_j) and tail_{j+1} = P_j + len_j + 20, so
+// P_{j+1} = P_j + roundup64(len_j + 20) -- an exclusive prefix sum of
+// roundup64(len + 20), no sequential walk.
+__global__ void compact_sizes_kernel(const uint64_t* st, const uint64_t* en, uint64_t n, uint64_t* rlen) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    rlen[i] = (en[i] - st[i] + 20 + 63) & ~63ull;
+}
+
+__global__ void compact_entries_kernel(const uint64_t* st, const uint64_t* en, const uint64_t* kh,
+                                       const uint64_t* pstart, uint64_t n, srd_write_entry* ent, uint64_t* new_len) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t tail = j ? pstart[j - 1] + (en[j - 1] - st[j - 1]) + 20 : 0;
+    ent[j] = srd_write_entry{st[j], en[j] - st[j], kh[j], tail, 0u, SRD_ENTRY_HASHED};
+    if (j == n - 1) *new_len = pstart[j] + (en[j] - st[j]) + 20;
+  }
+}
+
 }  // namespace srd
