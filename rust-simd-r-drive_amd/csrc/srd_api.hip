@@ -575,8 +575,7 @@ static int alloc_index(Ctx* c, uint64_t n_cap, uint32_t log2_nbk) {
   const uint64_t nh = ((uint64_t)1 << log2_nbk) * IDX_HBLOCKS + 1;
   TRY(ensure(c, B_HIST, nh * 4));
   TRY(ensure(c, B_HOFF, nh * 4));
-  TRY(ensure(c, B_SKEY, (n_cap + 1) * 8));
-  TRY(ensure(c, B_SIDX, (n_cap + 1) * 4));
+  TRY(ensure(c, B_SKEY, (n_cap + 1) * 16));
   TRY(ensure(c, B_LATEST8, n_cap + 1));
   TRY(ensure(c, B_PART, GLUE_BLOCKS * 4));
   TRY(ensure(c, B_PARTEX, GLUE_BLOCKS * 4));
@@ -599,8 +598,7 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   ia.log2_nbk = log2_nbk;
   ia.histT = P<uint32_t>(c, B_HIST);
   ia.hoff = P<uint32_t>(c, B_HOFF);
-  ia.skey = P<uint64_t>(c, B_SKEY);
-  ia.sidx = P<uint32_t>(c, B_SIDX);
+  ia.srec = P<u64x2>(c, B_SKEY);
   ia.latest = P<uint8_t>(c, B_LATEST8);
   ia.part = P<uint32_t>(c, B_PART);
   ia.part_ex = P<uint32_t>(c, B_PARTEX);

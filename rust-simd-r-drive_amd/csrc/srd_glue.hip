@@ -386,7 +386,10 @@ __global__ __launch_bounds__(256) void scatter_plan_kernel(ShapeArgs a) {
 // --------------------------------------------------------------------------
 // KeyIndexer::build, bucketed
 // --------------------------------------------------------------------------
-constexpr int IDX_HBLOCKS = 512;     // histogram / scatter blocks
+#ifndef SRD_IDX_HBLOCKS
+#define SRD_IDX_HBLOCKS 256
+#endif
+constexpr int IDX_HBLOCKS = SRD_IDX_HBLOCKS;  // histogram / scatter blocks
 constexpr int IDX_TSLOTS = 4096;     // LDS open-addressing slots per bucket block (max)
 constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
 constexpr int IDX_BUCKET_AVG = 1024; // host sizes the bucket count for this average
@@ -400,8 +403,7 @@ struct IdxArgs {
   uint32_t log2_nbk;
   uint32_t* histT;       // [nbk * IDX_HBLOCKS + 1]
   uint32_t* hoff;        // exclusive scan of histT
-  uint64_t* skey;        // bucket-ordered keys
-  uint32_t* sidx;        // bucket-ordered chain indices
+  u64x2* srec;           // bucket-ordered (key, chain index): one 16-B store per entry
   uint8_t* latest;       // [n] 1 = latest entry of its key
   uint32_t* part;
   uint32_t* part_ex;
@@ -436,8 +438,7 @@ __global__ __launch_bounds__(256) void idx_scatter_kernel(IdxArgs a) {
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) {
     const uint64_t k = a.kh[c];
     const uint32_t pos = atomicAdd(&lds_u32[xxh3_64_u64(k) >> (64 - a.log2_nbk)], 1u);
-    a.skey[pos] = k;
-    a.sidx[pos] = (uint32_t)c;
+    a.srec[pos] = u64x2{k, c};
   }
 }
 
@@ -453,7 +454,7 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
   if (hi - lo > IDX_TCAP) {  // skewed bucket: the host reruns the global-table build
     if (threadIdx.x == 0) a.plan->idx_overflow = 1;
     // keep count/emit in bounds: this bucket contributes nothing
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.latest[a.sidx[i]] = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.latest[a.srec[i][1]] = 0;
     return;
   }
   uint32_t slots = 64;
@@ -463,8 +464,9 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
   if (threadIdx.x == 0) special = 0;
   __syncthreads();
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const uint64_t key = a.skey[i];
-    const uint32_t v = a.sidx[i] + 1;
+    const u64x2 rec = a.srec[i];
+    const uint64_t key = rec[0];
+    const uint32_t v = (uint32_t)rec[1] + 1;
     if (key == IDX_EMPTY) { atomicMax(&special, v); continue; }
     uint32_t s = (uint32_t)xxh3_64_u64(key) & M;
     while (true) {
@@ -475,8 +477,9 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
   }
   __syncthreads();
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const uint64_t key = a.skey[i];
-    const uint32_t c = a.sidx[i];
+    const u64x2 rec = a.srec[i];
+    const uint64_t key = rec[0];
+    const uint32_t c = (uint32_t)rec[1];
     uint32_t best;
     if (key == IDX_EMPTY) best = special;
     else {

@@ -32,6 +32,7 @@
 namespace srd {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int TILE = 4096;
