@@ -279,3 +279,44 @@ def test_c3_shape_200k_stays_optimistic(ctx):
     for i in np.random.default_rng(1).integers(0, n, 200):
         s0 = int(mo[i] - ln[i])
         assert int(crc[i]) == zlib.crc32(host[s0:int(mo[i])].tobytes())
+
+
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_hot_key_overflows_its_bucket(ctx, flags):
+    """One key overwritten 3000 times (more than a bucket's LDS table holds,
+    IDX_TCAP = 2048) among 700 other keys, plus tombstones of the hot key:
+    the index build's skewed-bucket fallback must still give latest-wins
+    (key_indexer.rs:98-124) exactly as the oracle does."""
+    rnd = random.Random(5)
+    hot = xxhash.xxh3_64_intdigest(b"hot")
+    buf, t = bytearray(), 0
+    for i in range(3700):
+        if i % 5 == 4 or rnd.random() < 0.6:
+            kh = hot
+        else:
+            kh = xxhash.xxh3_64_intdigest(b"k%d" % rnd.randrange(700))
+        if kh == hot and rnd.random() < 0.05:
+            t = O.write_entries(buf, t, [(kh, b"\x00")], allow_null=True)
+        else:
+            pl = rnd.randbytes(rnd.choice([1, 8, 60, 64, 200]))
+            t = O.write_entries(buf, t, [(kh, b"\x01" if pl == b"\x00" else pl)])
+    r = check_against_oracle(bytes(buf), ctx, flags, "hot")
+    assert r.n_index < 710
+
+
+def test_index_build_device_hot_key(ctx):
+    """srd_index_build_device (the sharded exchange's owner build) on pairs
+    with one key repeated 5000 times: latest position wins."""
+    import torch
+    rnd = random.Random(9)
+    keys = [0xABCDEF if rnd.random() < 0.7 else rnd.getrandbits(64) for _ in range(7000)]
+    pairs = np.array([[k, 64 * i + 7] for i, k in enumerate(keys)], np.uint64).reshape(-1)
+    d = torch.from_numpy(pairs.view(np.int64)).cuda()
+    ok = torch.empty(7000, dtype=torch.int64, device="cuda")
+    op = torch.empty(7000, dtype=torch.int64, device="cuda")
+    n = S.index_build_device(d.data_ptr(), 7000, ok.data_ptr(), op.data_ptr(), ctx)
+    want = {}
+    for i, k in enumerate(keys):
+        want[k] = ((k >> 48) << 48) | (64 * i + 7)
+    got = dict(zip(ok[:n].cpu().numpy().view(np.uint64).tolist(), op[:n].cpu().numpy().view(np.uint64).tolist()))
+    assert n == len(want) and got == want
