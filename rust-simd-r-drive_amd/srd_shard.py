@@ -8,7 +8,8 @@ reaches an entry whose prev_offset is its lower tail lo_r.  No data-path
 collective is needed for that: shards are independent.
 
 The exchange step is small and real:
-  1. boundaries: all_gather of (proven, lo, hi, n_chain, n_crc_bad) -- the
+  1. boundaries: all_gather of (proven, lo, hi, n_chain, n_crc_bad) and the
+     rank's per-owner index counts (so no separate count exchange) -- the
      shard chains compose into the whole file's chain iff every shard is
      proven, lo_0 == 0, hi_r == lo_{r+1} and hi_{W-1} == file_len.  That is
      recover_valid_chain's answer (data_store.rs:383-482) for a clean store:
@@ -147,11 +148,20 @@ def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, h
         local = None
     else:
         st, keys, packed, local = backend.validate_span(buf, span_off, lo, hi)
-    # 1. boundaries
-    mine = torch.tensor([int(st.proven), st.lo, st.hi, st.n_chain, st.n_crc_bad], dtype=torch.int64, device=cd)
-    allst = torch.empty(world * 5, dtype=torch.int64, device=cd)
+    # owner partition of the shard-local index (needed only when the shards
+    # compose, but done first so that one all_gather carries both the
+    # boundary rows and every rank's per-owner send counts)
+    if keys.numel():
+        pairs, counts = backend.partition(keys, packed, world)
+    else:
+        pairs, counts = torch.empty(0, dtype=torch.int64, device=dev), [0] * world
+    # 1. boundaries (+ the count matrix of the index all_to_all)
+    w = 5 + world
+    mine = torch.tensor([int(st.proven), st.lo, st.hi, st.n_chain, st.n_crc_bad] + list(counts),
+                        dtype=torch.int64, device=cd)
+    allst = torch.empty(world * w, dtype=torch.int64, device=cd)
     dist.all_gather_into_tensor(allst, mine, group=group)
-    rows = allst.view(world, 5).cpu().tolist()
+    rows = allst.view(world, w).cpu().tolist()
     composed = all(r[0] for r in rows) and rows[0][1] == 0 and rows[-1][2] == file_len and all(
         rows[i][2] == rows[i + 1][1] for i in range(world - 1))
     n_chain = sum(r[3] for r in rows)
@@ -159,15 +169,9 @@ def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, h
     if not composed:
         empty = torch.empty(0, dtype=torch.int64, device=dev)
         return ShardedResult(0, False, 0, 0, 0, empty, empty, local)
-    # 2. index exchange
-    if keys.numel():
-        pairs, counts = backend.partition(keys, packed, world)
-    else:
-        pairs, counts = torch.empty(0, dtype=torch.int64, device=dev), [0] * world
-    send = torch.tensor(counts, dtype=torch.int64, device=cd)
-    recv = torch.empty(world, dtype=torch.int64, device=cd)
-    dist.all_to_all_single(recv, send, group=group)
-    rc = recv.cpu().tolist()
+    # 2. index exchange: pairs to their owners
+    me = dist.get_rank(group)
+    rc = [rows[r][5 + me] for r in range(world)]
     got = torch.empty(2 * sum(rc), dtype=torch.int64, device=cd)
     dist.all_to_all_single(got, pairs.to(cd), [2 * c for c in rc], [2 * c for c in counts], group=group)
     okeys, opacked = backend.build(got.to(dev))
