@@ -102,7 +102,7 @@ enum BufId {
   B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
   B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
-  B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
+  B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST, B_XPART,
   B_COUNT_
 };
 
@@ -200,6 +200,24 @@ int ensure_cub(Ctx* c, uint64_t n) {
                                 (uint64_t*)nullptr, (uint64_t*)nullptr, nn);
   t5 = std::max(std::max(t1, t2), std::max(t3, t4));
   return ensure(c, B_CUB_TMP, t5 + 256);
+}
+
+// exclusive scan of n u32 counts into u32 / u64 offsets on the call's stream
+// (xscan_* kernels; SRD_CUB_SCAN builds keep hipCUB for A/B timing)
+template <class OUT>
+static int xscan(Ctx* c, const uint32_t* in, OUT* out, uint64_t n) {
+#ifdef SRD_CUB_SCAN
+  size_t tb = c->bufs[B_CUB_TMP].n;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, in, out, (int)n, c->stream));
+#else
+  TRY(ensure(c, B_XPART, GLUE_BLOCKS * 4));
+  xscan_sum_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(in, n, P<uint32_t>(c, B_XPART));
+  KCHK(c, "xscan_sum_kernel");
+  xscan_apply_kernel<OUT><<<GLUE_BLOCKS, 256, 0, c->stream>>>(in, n, P<uint32_t>(c, B_XPART), out);
+  KCHK(c, "xscan_apply_kernel");
+  HIPCHK(hipGetLastError());
+#endif
+  return 0;
 }
 
 int read_counters(Ctx* c, uint64_t* h) {
@@ -609,8 +627,7 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   const int nh = (int)((uint64_t)nbk * IDX_HBLOCKS + 1);
   idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
   KCHK(c, "idx_hist_kernel");
-  size_t tb = c->bufs[B_CUB_TMP].n;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, ia.histT, ia.hoff, nh, c->stream));
+  TRY(xscan(c, ia.histT, ia.hoff, (uint64_t)nh));
   idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
   KCHK(c, "idx_scatter_kernel");
   idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
@@ -719,9 +736,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       return SRD_ERR_INTERNAL;
     }
 #endif
-    size_t tb = c->bufs[B_CUB_TMP].n;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_SPAN_COUNT),
-                                            P<uint64_t>(c, B_SPAN_BASE), (int)(ns_rel + 1), c->stream));
+    TRY(xscan(c, P<uint32_t>(c, B_SPAN_COUNT), P<uint64_t>(c, B_SPAN_BASE), ns_rel + 1));
     Link2Args l{};
     l.file = d_file;
     l.flen = flen;

@@ -121,6 +121,55 @@ __device__ __forceinline__ void block_prefix(const uint32_t* part, uint32_t np, 
   *total = block_sum256(t, wsum);
 }
 
+// Device exclusive scan of n u32 values in two launches (replaces hipCUB's
+// lookback-state init + scan pair on the per-call path): per-block chunk sums,
+// then every block derives its own prefix (block_prefix) and scans its chunk
+// 256 values at a time.  Totals must fit in u32 (counts of one call).
+__global__ __launch_bounds__(256) void xscan_sum_kernel(const uint32_t* in, uint64_t n, uint32_t* part) {
+  __shared__ uint32_t wsum[4];
+  uint64_t lo, hi;
+  chunk_of(n, &lo, &hi);
+  uint32_t s = 0;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) s += in[i];
+  const uint32_t t = block_sum256(s, wsum);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+template <class OUT>
+__global__ __launch_bounds__(256) void xscan_apply_kernel(const uint32_t* in, uint64_t n, const uint32_t* part,
+                                                          OUT* out) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t wpre[4];
+  uint64_t before, total;
+  block_prefix(part, gridDim.x, wsum, &before, &total);
+  uint64_t lo, hi;
+  chunk_of(n, &lo, &hi);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t run = before;
+  for (uint64_t base = lo; base < hi; base += blockDim.x) {
+    const uint64_t i = base + threadIdx.x;
+    const uint32_t v = i < hi ? in[i] : 0u;
+    uint32_t x = v;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wpre[w] = x;
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t q = wpre[k];
+      wb += k < w ? q : 0u;
+      tot += q;
+    }
+    __syncthreads();
+    if (i < hi) out[i] = (OUT)(run + wb + x - v);
+    run += tot;
+  }
+}
+
 // exclusive scan of up to 1024 partials with one 1024-thread block
 __device__ uint64_t block_scan_partials(const uint32_t* part, uint32_t np, uint32_t* part_ex) {
   __shared__ uint64_t s[1024];
