@@ -203,21 +203,32 @@ int ensure_cub(Ctx* c, uint64_t n) {
 }
 
 // exclusive scan of n u32 counts into u32 / u64 offsets on the call's stream
-// (xscan_* kernels; SRD_CUB_SCAN builds keep hipCUB for A/B timing)
+// (xscan_* kernels: chunk sums, then per-block prefix + scan)
 template <class OUT>
 static int xscan(Ctx* c, const uint32_t* in, OUT* out, uint64_t n) {
-#ifdef SRD_CUB_SCAN
-  size_t tb = c->bufs[B_CUB_TMP].n;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, in, out, (int)n, c->stream));
-#else
-  TRY(ensure(c, B_XPART, GLUE_BLOCKS * 4));
-  xscan_sum_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(in, n, P<uint32_t>(c, B_XPART));
+  TRY(ensure(c, B_XPART, GLUE_BLOCKS * 8));
+  xscan_sum_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(in, n, P<uint64_t>(c, B_XPART));
   KCHK(c, "xscan_sum_kernel");
-  xscan_apply_kernel<OUT><<<GLUE_BLOCKS, 256, 0, c->stream>>>(in, n, P<uint32_t>(c, B_XPART), out);
+  xscan_apply_kernel<OUT><<<GLUE_BLOCKS, 256, 0, c->stream>>>(in, n, P<uint64_t>(c, B_XPART), out);
   KCHK(c, "xscan_apply_kernel");
   HIPCHK(hipGetLastError());
-#endif
   return 0;
+}
+
+// stores above 2^40 bytes take the WIDE scan (48-bit prev offsets)
+constexpr uint64_t kWide = 1ull << 40;
+constexpr uint64_t kMaxFile = 1ull << 48;  // packed offsets are 48-bit (key_indexer.rs:12-15, 79-85)
+template <bool FULL>
+static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s) {
+  if (a.flen > kWide)
+    scan_kernel<FULL, true><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(a);
+  else
+    scan_kernel<FULL, false><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(a);
+}
+
+static bool debug_env() {
+  static const bool v = [] { const char* e = getenv("SRD_DEBUG"); return e && *e && *e != '0'; }();
+  return v;
 }
 
 int read_counters(Ctx* c, uint64_t* h) {
@@ -516,17 +527,13 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.c_rec = P<u32x4>(c, B_CREC);
     a.counters = (unsigned long long*)cnt;
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
-    {
-      const char* ab = getenv("SRD_SCAN_ABLATE");
-      a.ablate = ab ? (uint32_t)atoi(ab) : 0u;
-    }
     if (n_spans) {
       unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
       if (full)
-        scan_kernel<true><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
+        launch_scan<true>(g, a, c->stream);
       else
-        scan_kernel<false><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
+        launch_scan<false>(g, a, c->stream);
       KCHK(c, "scan_kernel");
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev[1], c->stream));
@@ -677,7 +684,9 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
   for (int attempt = 0; attempt < 6; attempt++) {
     if (!c->capK) c->capK = (flen - span_off) / 1024 + 4096;
     const uint64_t capK = c->capK;
-    if (capK >= (1ull << 32) - 2) { set_err("too many chain candidates"); return SRD_ERR_INTERNAL; }
+    // capacity exhausted (dense small-entry stores): not provable here, the
+    // full pass (whole file) decides / the span is reported unproven
+    if (capK >= (1ull << 31)) { c->capK = 0; return 0; }
     // index buckets: ~IDX_BUCKET_AVG chain entries per bucket
     const uint64_t n_est = std::max<uint64_t>(std::max<uint64_t>(c->last_n, (flen - span_off) / 4096), 1);
     const uint32_t log2_nbk = index_log2_buckets(n_est);
@@ -715,27 +724,12 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.zero_words = (uint32_t*)pl;
     a.n_zero_words = (uint32_t)(sizeof(Plan) / 4);
     a.sentinel = P<uint32_t>(c, B_SPAN_COUNT) + ns_rel;
-    {
-      const char* ab = getenv("SRD_SCAN_ABLATE");
-      a.ablate = ab ? (uint32_t)atoi(ab) : 0u;
-    }
     const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    scan_kernel<false><<<g, SCAN_WAVES_V2 * 64, 0, c->stream>>>(a);
+    launch_scan<false>(g, a, c->stream);
     KCHK(c, "scan_kernel");
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-#ifdef SRD_ABLATE_NOLOAD
-    if (a.ablate & (16 | 256)) {  // timing experiment only (16: no HBM loads, 256: stop after the scan)
-      HIPCHK(hipEventSynchronize(c->ev[1]));
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-      c->scan_ms += ms;
-      c->scan_launches++;
-      set_err("ablate 16: scan only");
-      return SRD_ERR_INTERNAL;
-    }
-#endif
     TRY(xscan(c, P<uint32_t>(c, B_SPAN_COUNT), P<uint64_t>(c, B_SPAN_BASE), ns_rel + 1));
     Link2Args l{};
     l.file = d_file;
@@ -844,7 +838,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       hp = *c->h_plan;
-      if (getenv("SRD_DEBUG")) {
+      if (debug_env()) {
         fprintf(stderr, "plan K=%lu n_chain=%lu root_t=%lu start=%lu n_index=%lu bad=%lu slow=%lu st=%u nroot=%u "
                 "troot=%u idxov=%u log2nbk=%u capK=%lu rounds=%d\n",
                 (unsigned long)hp.K, (unsigned long)hp.n_chain, (unsigned long)hp.root_t, (unsigned long)hp.start,
@@ -869,7 +863,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     out->n_candidates = hp.K;
     out->n_weak = hp.n_weak;
     if (hp.status & ST_OVERFLOW) {
-      if (c->cap >= SPAN_BYTES) { set_err("candidate overflow"); return SRD_ERR_INTERNAL; }
+      if (c->cap >= SPAN_BYTES) return 0;  // cannot happen (<= one candidate per byte); not provable here
       c->cap = (uint32_t)std::min<uint64_t>((uint64_t)c->cap * 4, SPAN_BYTES);
       continue;
     }
@@ -917,8 +911,8 @@ extern "C" int srd_validate_span_device(srd_ctx* c, const uint8_t* d_span, uint6
     if (span_off) { set_err("bad argument: a span starting at tail 0 is the whole file (span_off must be 0)"); return SRD_ERR_ARG; }
     return srd_validate_index_device(c, d_span, hi, flags, out);
   }
-  if (span_off % SPAN_BYTES || span_off > lo || hi < lo + 21 || hi >= (1ull << 40)) {
-    set_err("bad span: need span_off % 16384 == 0, span_off <= lo, lo + 21 <= hi < 2^40");
+  if (span_off % SPAN_BYTES || span_off > lo || hi < lo + 21 || hi > kMaxFile) {
+    set_err("bad span: need span_off % 16384 == 0, span_off <= lo, lo + 21 <= hi <= 2^48");
     return SRD_ERR_ARG;
   }
   HIPCHK(hipSetDevice(c->device));
@@ -1021,7 +1015,7 @@ extern "C" int srd_ctx_timings(srd_ctx* c, double* scan_ms, int* scan_launches, 
 static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen, uint32_t flags,
                                 srd_device_result* out) {
   if (!c || !out || (!d_file && flen)) { set_err("bad argument"); return SRD_ERR_ARG; }
-  if (flen >= (1ull << 40)) { set_err("stores >= 1 TiB are not supported"); return SRD_ERR_ARG; }
+  if (flen > kMaxFile) { set_err("stores above 2^48 bytes cannot be indexed (48-bit packed offsets)"); return SRD_ERR_ARG; }
   HIPCHK(hipSetDevice(c->device));
   memset(out, 0, sizeof *out);
   out->file_len = flen;

@@ -50,20 +50,6 @@ struct Plan {
   uint64_t dbg[16];    // (m, p) of the first dangling core nodes
   uint64_t dbg_g[8];   // their dense indices
 };
-// debug: children of dense node `tgt` (SRD_DEBUG)
-__global__ void dbg_children_kernel(const int64_t* par, const uint64_t* d_m, const uint64_t* slot, const u32x4* c_rec,
-                                    uint64_t K, uint64_t tgt, unsigned long long* out) {
-  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x)
-    if (par[g] == (int64_t)tgt) {
-      const unsigned long long w = atomicAdd(out, 1ull);
-      if (w < 4) {
-        const u32x4 r0 = c_rec[2 * slot[g]];
-        out[1 + 3 * w] = d_m[g];
-        out[2 + 3 * w] = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-        out[3 + 3 * w] = g;
-      }
-    }
-}
 constexpr uint32_t ST_NOSTART = 1, ST_SHAPE = 2, ST_ROOTS = 4, ST_CAPK = 8, ST_OVERFLOW = 16;
 constexpr uint64_t NO_NODE = ~0ull;
 
@@ -121,46 +107,62 @@ __device__ __forceinline__ void block_prefix(const uint32_t* part, uint32_t np, 
   *total = block_sum256(t, wsum);
 }
 
+__device__ __forceinline__ uint64_t block_sum256_u64(uint64_t v, uint64_t* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+  if (lane == 0) wsum[w] = v;
+  __syncthreads();
+  const uint64_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return t;
+}
+
 // Device exclusive scan of n u32 values in two launches (replaces hipCUB's
-// lookback-state init + scan pair on the per-call path): per-block chunk sums,
-// then every block derives its own prefix (block_prefix) and scans its chunk
-// 256 values at a time.  Totals must fit in u32 (counts of one call).
-__global__ __launch_bounds__(256) void xscan_sum_kernel(const uint32_t* in, uint64_t n, uint32_t* part) {
-  __shared__ uint32_t wsum[4];
+// lookback-state init + scan pair on the per-call path): per-block chunk sums
+// (u64), then every block derives its own prefix and scans its chunk 256
+// values at a time.  Sums are u64 (a u64 output never wraps); a u32 output
+// holds counts of one call that fit in u32 by construction.
+__global__ __launch_bounds__(256) void xscan_sum_kernel(const uint32_t* in, uint64_t n, uint64_t* part) {
+  __shared__ uint64_t wsum[4];
   uint64_t lo, hi;
   chunk_of(n, &lo, &hi);
-  uint32_t s = 0;
+  uint64_t s = 0;
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) s += in[i];
-  const uint32_t t = block_sum256(s, wsum);
+  const uint64_t t = block_sum256_u64(s, wsum);
   if (threadIdx.x == 0) part[blockIdx.x] = t;
 }
 
 template <class OUT>
-__global__ __launch_bounds__(256) void xscan_apply_kernel(const uint32_t* in, uint64_t n, const uint32_t* part,
+__global__ __launch_bounds__(256) void xscan_apply_kernel(const uint32_t* in, uint64_t n, const uint64_t* part,
                                                           OUT* out) {
-  __shared__ uint32_t wsum[4];
-  __shared__ uint32_t wpre[4];
-  uint64_t before, total;
-  block_prefix(part, gridDim.x, wsum, &before, &total);
+  __shared__ uint64_t wsum[4];
+  __shared__ uint64_t wpre[4];
+  uint64_t before = 0;
+  {
+    uint64_t b = 0;
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) b += i < blockIdx.x ? part[i] : 0ull;
+    before = block_sum256_u64(b, wsum);
+  }
   uint64_t lo, hi;
   chunk_of(n, &lo, &hi);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint64_t run = before;
   for (uint64_t base = lo; base < hi; base += blockDim.x) {
     const uint64_t i = base + threadIdx.x;
-    const uint32_t v = i < hi ? in[i] : 0u;
-    uint32_t x = v;  // inclusive wave scan
+    const uint64_t v = i < hi ? in[i] : 0u;
+    uint64_t x = v;  // inclusive wave scan
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
+      const uint64_t y = __shfl_up(x, o);
       if (lane >= o) x += y;
     }
     if (lane == 63) wpre[w] = x;
     __syncthreads();
-    uint32_t wb = 0, tot = 0;
+    uint64_t wb = 0, tot = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const uint32_t q = wpre[k];
+      const uint64_t q = wpre[k];
       wb += k < w ? q : 0u;
       tot += q;
     }
@@ -197,7 +199,7 @@ struct Link2Args {
   const uint32_t* span_count;
   const uint64_t* span_base;
   const uint64_t* c_m;
-  u32x4* c_rec;  // lean records are completed in place
+  u32x4* c_rec;  // tombstone flags are set in place
   uint64_t* d_m;
   int64_t* d_par;
   uint64_t* d_slot;
@@ -218,23 +220,9 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
     const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     bool node = true;
-    if (r1[3] & F_LEAN) {
-      // lean record: key_hash / crc from the file (these loads issue beside
-      // the parent lookup's first one), recover_valid_chain's node test
-      // (data_store.rs:404-470), then the full record for the kernels
-      // downstream.  A candidate that fails the test gets no parent: it can
-      // never be core, and a chain through it fails the shape check.
-      uint64_t kh, p2;
-      uint32_t crc;
-      ld_meta(a.file, m, &kh, &p2, &crc);
-      const uint64_t dp = m - p;
-      const bool tomb = dp == 1 && a.file[p] == 0;  // tombstone byte at prev_tail (p = m - 1 here)
-      node = p >= 20 && p < m && (tomb || dp > prepad64(p));
-      a.c_rec[2 * gi] = u32x4{r0[0], r0[1], (uint32_t)kh, (uint32_t)(kh >> 32)};
-      a.c_rec[2 * gi + 1] = u32x4{crc, r1[1], r1[2], (r1[3] & ~F_LEAN) | (tomb ? F_TOMB : 0u)};
-    } else if (r1[3] & F_NT) {
-      // full record, deferred node test (data_store.rs:404-470); F_ZB is the
-      // byte at m - 1, the tombstone byte when p == m - 1
+    if (r1[3] & F_NT) {
+      // single-candidate record, deferred node test (data_store.rs:404-470);
+      // F_ZB is the byte at m - 1, the tombstone byte when p == m - 1
       const uint64_t dp = m - p;
       const bool tomb = dp == 1 && (r1[3] & F_ZB);
       node = p >= 20 && p < m && (tomb || dp > prepad64(p));

@@ -38,22 +38,6 @@ typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 constexpr int TILE = 4096;
 constexpr int SPAN_TILES = 4;
 constexpr uint64_t SPAN_BYTES = (uint64_t)TILE * SPAN_TILES;
-#ifndef SRD_CRC_LINE
-#define SRD_CRC_LINE crc_line4
-#endif
-#ifndef SRD_LEAN
-#define SRD_LEAN 2  // single-candidate records: 0 full, node test in the scan; 1 without key_hash / crc
-                    // (link2_kernel reads them from the file); 2 full, node test deferred to link2_kernel
-#endif
-#ifndef SRD_RING
-#define SRD_RING 3
-#endif
-#ifndef SRD_REPL
-#define SRD_REPL 32
-#endif
-constexpr int REPL = SRD_REPL;       // LDS table replication: lane l reads copy l%32 -> conflict-free
-constexpr int SCAN_WAVES = 8;        // waves per scan block
-constexpr int TCAP = 128;            // per-tile candidate list in LDS
 constexpr int64_t PAR_ROOT = -1;
 constexpr int64_t PAR_MISS = -2;
 
@@ -63,12 +47,9 @@ constexpr int F_SUF_SHIFT = 3;        // 2 bits: 0 value, 1 next-tile T, 2 next-
 // the recorded sxm / suf value is a lower-half partial (line < 32): true value =
 // mul16k(v) ^ SX_32 of the tile holding m (sxm) or the entry start (suf kind 0) -- see lo_fix()
 constexpr uint32_t F_SXM_LO = 32u, F_SUF_LO = 64u;
-// lean record (optimistic scan, one candidate in the line): only c_m, p and
-// {-, sxm, suf, flags} are written; link2_kernel reads key_hash / crc from
-// the file, applies the node test and completes the record (clearing F_LEAN)
-constexpr uint32_t F_LEAN = 128u;
-// SRD_LEAN 2: full record whose node test link2_kernel applies (F_NT); F_ZB =
-// the byte at m - 1 is 0 (the tombstone rule's byte when p == m - 1)
+// single-candidate record of the optimistic scan: link2_kernel applies the
+// node test (F_NT); F_ZB = the byte at m - 1 is 0 (the tombstone rule's byte
+// when p == m - 1)
 constexpr uint32_t F_NT = 256u, F_ZB = 512u;
 
 struct DevTables {
@@ -99,8 +80,7 @@ struct ScanArgs {
   uint64_t* c_m;                   // [n_spans*cap] candidate metadata offsets
   u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
   unsigned long long* counters;    // [0] max root tail, [1] unused, [2] overflow
-  uint32_t ablate;                 // timing experiments only (SRD_SCAN_ABLATE): 1 no CRC, 2 no slow path, 4 slow path stops after the exact test
-  uint32_t filt_hb;                // (file_len-1) >> 32: bound of a node's p-byte 4 (p < file_len < 2^40)
+  uint32_t filt_hb;               // (file_len-1) >> 32: bound of a node's p-byte 4 (p < file_len < 2^40)
   // span mode (entry-range shard): tiles [k_lo, n_tiles) are resident, k_lo a
   // multiple of SPAN_TILES; only nodes with m > m_lo are recorded (m_lo = the
   // shard's lower tail; 0 = whole file, where m >= 1)
@@ -180,13 +160,12 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // --------------------------------------------------------------------------
 // 1. the fused streaming scan
 // --------------------------------------------------------------------------
-// LDS: slice-by-4 CRC tables replicated REPL times (lane l reads copy l%REPL,
+// LDS: slice-by-4 CRC tables replicated 32 times (lane l reads copy l%32,
 // so the 32 lanes of a ds_read_b32 group hit at most 2 distinct addresses per
 // bank), the lane-weight nibble tables (entry (pos,nib) of lane l at word
 // ((pos*16+nib)*64 + l): every lane its own bank, conflict-free) and one
-// 25-dword window per wave for the cooperative candidate check.
+// 24-dword window per wave for the cooperative candidate check.
 constexpr int SCAN_WAVES_V2 = 16;
-constexpr int MREPL = 8;  // replication of the x^256 multiply table
 struct ScanLds {
   uint32_t tab[4 * 256 * 32];      // 128 KiB slice-by-4 tables, conflict-free (layout: tab_lookup)
   uint32_t nib[8 * 16 * 32];       // 16 KiB: c -> c * x^(512*(31 - l%32)), bank = l%32
@@ -240,22 +219,6 @@ __device__ __forceinline__ uint32_t crc_line4(const uint32_t (&d)[16], const Sca
   const uint32_t cd = mulfix(s[2], L.m128) ^ s[3];
   return mulfix(ab, L.m256) ^ cd;
 }
-// 2 independent 32-byte chains joined by c = a*x^256 ^ b
-__device__ __forceinline__ uint32_t crc_line2(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
-  constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
-  uint32_t s[2] = {d[0], d[8]};
-#pragma unroll
-  for (int j = 0; j < 8; j++) {
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const uint32_t t3 = tab_lookup(L, s[q], R[3], SEL0), t2 = tab_lookup(L, s[q], R[2], SEL1);
-      const uint32_t t1 = tab_lookup(L, s[q], R[1], SEL2), t0 = tab_lookup(L, s[q], R[0], SEL3);
-      s[q] = xor3(xor3(t3, t2, j < 7 ? d[8 * q + (j < 7 ? j + 1 : 7)] : 0u), t1, t0);
-    }
-  }
-  return mulfix(s[0], L.m256) ^ s[1];
-}
-
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
@@ -326,7 +289,9 @@ __device__ __forceinline__ void crc_lane_bases(uint32_t (&R)[4], int lane) {
   for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
 }
 
-template <bool FULL>
+// WIDE: stores above 2^40 bytes (prev offsets up to 48 bits, key_indexer.rs:12-15):
+// the level-1 filter looks for the two zero bytes m+14, m+15 at any alignment
+template <bool FULL, bool WIDE>
 __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
   __shared__ ScanLds lds;
   if (blockIdx.x == 0) {
@@ -360,35 +325,21 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
   uint32_t tacc = 0, scnt = 0;
-  uint32_t rq[SRD_LEAN == 1 ? 7 : 10];
+  uint32_t rq[10];
 #pragma unroll
-  for (int i = 0; i < (SRD_LEAN == 1 ? 7 : 10); i++) rq[i] = 0;
+  for (int i = 0; i < 10; i++) rq[i] = 0;
   uint64_t rvalid = 0;  // wave-uniform: record slots buffered in rq
 
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
   // (no loads under divergent/uniform branches, so the compiler's vmcnt
-  // waits never have to drain the prefetch ring).
-  // timing experiments (SRD_ABLATE_NOLOAD builds only): runtime ablation
-  // bits; otherwise a compile-time 0, so no branch splits the tile's
-  // straight-line code (CRC, lane weights, suffix XOR, filter) into blocks
-#if defined(SRD_ABL_CT)
-  constexpr uint32_t ABL = SRD_ABL_CT;  // compile-time ablation variant (no runtime branches)
-#elif defined(SRD_ABLATE_NOLOAD)
-  const uint32_t ABL = a.ablate;
-#else
-  constexpr uint32_t ABL = 0;
-#endif
+  // waits never have to drain the prefetch ring).  The tile's code (CRC,
+  // lane weights, suffix XOR, filter) is one basic block.
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
-    if (ABL & 16) k = k0;  // timing experiment: compute-only (re-reads one L2-resident tile)
     const u32x4* q = (const u32x4*)(file + k * (uint64_t)TILE + 64ull * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       // plain loads: this 64 B-per-lane pattern runs at ~3.8 TB/s with nt, ~6.1 without
-#ifdef SRD_NT_LAST  // timing experiment: the line's last 16 B as a streaming (nt) load
-      const u32x4 v = j == 3 ? __builtin_nontemporal_load(q + j) : q[j];
-#else
       const u32x4 v = q[j];
-#endif
       o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
     }
   };
@@ -415,7 +366,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const u32x4 v = q[j];
       pl[4 * j] = v[0]; pl[4 * j + 1] = v[1]; pl[4 * j + 2] = v[2]; pl[4 * j + 3] = v[3];
     }
-    const uint32_t cp = SRD_CRC_LINE(pl, lds, R);
+    const uint32_t cp = crc_line4(pl, lds, R);
     if (lane == 0) {
 #pragma unroll
       for (int j = 0; j < 4; j++) win[j] = has_prev ? pl[12 + j] : 0u;
@@ -451,18 +402,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       for (int j = 0; j < 16; j++) d[j] = mask_past_end32(d[j], 64u * lane + 4 * j, remu);
     }
 
-#if SRD_EXP == 1  // timing experiment: consume the tile only
-    {
-      uint32_t x = 0;
-#pragma unroll
-      for (int j = 0; j < 16; j++) x ^= d[j];
-      if (x == 0x9E3779B9u && lane == 63 && k == 0) a.tile[0] = x;
-      return;
-    }
-#endif
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
-    const uint32_t c = (ABL & 1) ? (d[0] ^ d[5] ^ d[15]) : SRD_CRC_LINE(d, lds, R);
-    const uint32_t hx = (ABL & 1) ? c : half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
+    const uint32_t c = crc_line4(d, lds, R);
+    const uint32_t hx = half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
     // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
     // tiles.  Every store of this loop is an UNCONDITIONAL buffer store whose
@@ -481,22 +423,32 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint32_t off = (flush && (uint32_t)lane >= lo && lane < 4 * t + 4) ? 4u * lane : OOB_OFF;
       __builtin_amdgcn_raw_buffer_store_b32(tacc, out_rsrc(a.tile + 4 * g, 256), off, 0, 0);
     }
-#if SRD_EXP == 2  // timing experiment: + CRC / tile values
-    return;
-#endif
 
     // ---- filter, level 1: any aligned zero halfword in the lane's line
     //      (packed 16-bit min over the 16 dwords: 1 VALU per dword); level 2
-    //      (exact, per position) in the slow path ----
-    u16x2 zmin = __builtin_bit_cast(u16x2, d[0]);
+    //      (exact, per position) in the slow path.  WIDE: any two adjacent
+    //      zero bytes, the last one possibly the next line's first ----
+    uint64_t slow;
+    if (!WIDE) {
+      u16x2 zmin = __builtin_bit_cast(u16x2, d[0]);
 #pragma unroll
-    for (int i = 1; i < 16; i++) zmin = __builtin_elementwise_min(zmin, __builtin_bit_cast(u16x2, d[i]));
-    uint64_t slow = __ballot(zmin.x == 0 || zmin.y == 0);
-    if (ABL & 2) slow = 0;
-#if SRD_EXP == 3  // timing experiment: + the level-1 filter
-    if (slow == 0x123456789ull && k == 0 && lane == 0) a.tile[1] = 1;
-    return;
-#endif
+      for (int i = 1; i < 16; i++) zmin = __builtin_elementwise_min(zmin, __builtin_bit_cast(u16x2, d[i]));
+      slow = __ballot(zmin.x == 0 || zmin.y == 0);
+    } else {
+      uint32_t nx = __shfl_down(d[0], 1);
+      if (lane == 63) {
+        uint32_t n0, n1;
+        next_head(k, &n0, &n1);
+        nx = tail_tile ? mask_past_end32(n0, TILE, remu) : n0;
+      }
+      uint32_t hz = 0;
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const uint32_t y = d[i] | alignb(i < 15 ? d[i < 15 ? i + 1 : 15] : nx, d[i], 8);
+        hz |= (y - 0x01010101u) & ~y & 0x80808080u;  // a zero byte of y = two zero bytes in a row
+      }
+      slow = __ballot(hz != 0);
+    }
     // Re-define d by an empty asm once its loads have been consumed: a loop
     // that stores and uses a register last written by a pending VMEM load
     // makes the compiler flush vmcnt to 0 in the loop preheader, draining the
@@ -561,44 +513,23 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
         // != 0) are recorded; a chain through any other node fails the shape
         // check and goes to the full pass, so nothing else is needed here
         const uint64_t pm = __ballot(inrange && f3 <= hb && (f2 | f3) != 0 && f4 != 0);
-        if (!pm || (ABL & 4)) continue;
+        if (!pm) continue;
         if ((pm & (pm - 1)) == 0) {
           // one possible node (the common case: one metadata record per
-          // line): a LEAN record -- m, p, the two suffix values only the
-          // scan has, and the position flags.  link2_kernel reads key_hash /
-          // crc from the file (beside its parent lookup, which needs p) and
-          // applies the node test (data_store.rs:404-470).
+          // line): the record -- m, p, key_hash, crc, the two suffix values
+          // only the scan has, and the position flags -- goes to lane `count`
+          // of the record registers; link2_kernel applies the node test
+          // (data_store.rs:404-470) beside its parent lookup (F_NT).
           const int bl = __builtin_ctzll(pm);
           const int rs = 64 * f + bl - 14;
           const uint64_t m = B + (int64_t)rs;
           const uint32_t s2 = __builtin_amdgcn_readlane(f2, bl), s3 = __builtin_amdgcn_readlane(f3, bl);  // p
-#if SRD_LEAN == 0
-          // full record: the node test here (data_store.rs:404-470) and the
-          // key hash / crc from the window
-          const uint64_t p = (uint64_t)s2 | ((uint64_t)s3 << 32);
-          const uint64_t dp = m - p;
-          const uint32_t os = (uint32_t)bl + 2;
-          const uint32_t stb = (__builtin_amdgcn_readlane(tdw, bl) >> (((os - 1) & 3) * 8)) & 0xffu;
-          const bool tomb = dp == 1 && stb == 0;
-          if (!(p >= 20 && p < m && (tomb || dp > ((0u - s2) & 63u)))) continue;
-          const uint32_t s0 = __builtin_amdgcn_readlane(alignb(W[1], W[0], sh), bl);
-          const uint32_t s1 = __builtin_amdgcn_readlane(alignb(W[2], W[1], sh), bl);
-          const uint32_t s4 = __builtin_amdgcn_readlane(f4, bl);
-          constexpr uint32_t REC_KIND = 0u;
-#elif SRD_LEAN == 2
-          // full record, node test deferred to link2_kernel (F_NT)
           const uint32_t os = (uint32_t)bl + 2;
           const uint32_t stb = (__builtin_amdgcn_readlane(tdw, bl) >> (((os - 1) & 3) * 8)) & 0xffu;
           const uint32_t s0 = __builtin_amdgcn_readlane(alignb(W[1], W[0], sh), bl);
           const uint32_t s1 = __builtin_amdgcn_readlane(alignb(W[2], W[1], sh), bl);
           const uint32_t s4 = __builtin_amdgcn_readlane(f4, bl);
-          constexpr bool tomb = false;
           const uint32_t REC_KIND = F_NT | (stb == 0 ? F_ZB : 0u);
-#else
-          constexpr uint32_t s0 = 0u, s1 = 0u, s4 = 0u;
-          constexpr bool tomb = false;
-          constexpr uint32_t REC_KIND = F_LEAN;
-#endif
           const uint32_t us = (uint32_t)(rs + 20);
           const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
           const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
@@ -606,7 +537,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const uint32_t hm = lm < 0 ? __builtin_amdgcn_readfirstlane(hxp) : __builtin_amdgcn_readlane(hx, lm & 63);
           if (count < a.cap) {
             const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
-            const uint32_t fl = REC_KIND | (tomb ? F_TOMB : 0u) | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
+            const uint32_t fl = REC_KIND | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
                                 (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
                                 ((js & 63) < 32 ? F_SUF_LO : 0u);
             if (count < 64) {
@@ -620,11 +551,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
               rq[4] = mine ? fl : rq[4];
               rq[5] = mine ? s2 : rq[5];
               rq[6] = mine ? s3 : rq[6];
-#if SRD_LEAN != 1
               rq[7] = mine ? s0 : rq[7];
               rq[8] = mine ? s1 : rq[8];
               rq[9] = mine ? s4 : rq[9];
-#endif
               rvalid |= 1ull << count;
             } else if (lane == 0) {
               const uint64_t gi = span * a.cap + count;
@@ -689,20 +618,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const bool w = span_end && ((rvalid >> lane) & 1);
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + span * a.cap, 64 * 8),
                                             w ? 8u * lane : OOB_OFF, 0, 0);
-#if SRD_LEAN == 1  // lean records: link2_kernel completes key_hash and crc
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[5], rq[6]}, out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
-                                            w ? 32u * lane : OOB_OFF, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, rq[2], rq[3], rq[4]},
-                                             out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
-                                             w ? 32u * lane + 16u : OOB_OFF, 0, 0);
-#else
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]},
                                              out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
                                              w ? 32u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]},
                                              out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
                                              w ? 32u * lane + 16u : OOB_OFF, 0, 0);
-#endif
       const uint32_t sp = (uint32_t)(span & 63);
       scnt = (span_end && (uint32_t)lane == sp) ? count : scnt;
       const bool sfl = span_end && (sp == 63 || k + 1 == k1);
@@ -718,9 +639,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
   };
 
-  // register ring (SRD_RING buffers: RING-1 tiles in flight while one is
-  // processed; 3 measured best with the 4-chain line CRC, whose registers a
-  // 4th buffer would spill).
+  // register ring (3 buffers: 2 tiles in flight while one is processed;
+  // measured best with the 4-chain line CRC, whose registers a 4th buffer
+  // would spill).
   // Loads are clamped, never skipped (tiles up to n_tiles+1 are readable).
   // kt = the first tail tile (flen - kt*TILE < TILE + 64)
   const uint64_t kt = flen >= (uint64_t)TILE + 64 ? (flen - TILE - 64) / TILE + 1 : 0;
@@ -728,25 +649,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   const uint32_t nk = (uint32_t)(km - k0);
   const std::false_type body{};
   uint32_t A[16], Bv[16], Cv[16];
-#if SRD_RING == 4
-  uint32_t Dv[16];
-  load_tile(k0, A);
-  load_tile(k0 + 1, Bv);
-  load_tile(k0 + 2, Cv);
-  for (uint32_t j = 0; j < nk; j += 4) {
-    load_tile(k0 + min(j + 3, nk), Dv);
-    process(k0 + j, A, body);
-    if (j + 1 >= nk) break;
-    load_tile(k0 + min(j + 4, nk), A);
-    process(k0 + j + 1, Bv, body);
-    if (j + 2 >= nk) break;
-    load_tile(k0 + min(j + 5, nk), Bv);
-    process(k0 + j + 2, Cv, body);
-    if (j + 3 >= nk) break;
-    load_tile(k0 + min(j + 6, nk), Cv);
-    process(k0 + j + 3, Dv, body);
-  }
-#else
   // vmcnt counts loads and stores in issue order, and the compiler's wait
   // counts at the loop header are the minimum over its entries.  In the
   // steady state every tile's loads are followed by process()'s 5
@@ -756,12 +658,10 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // Dummy stores (out-of-range offsets: dropped by the hardware; distinct,
   // or the compiler merges them as dead stores) give the entry the same queue.
   auto pad_stores = [&](uint32_t g) {
-#ifndef SRD_NO_PAD
     constexpr uint32_t NST = 5u;  // process()'s unconditional stores
 #pragma unroll
     for (uint32_t i = 0; i < NST; i++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, out_rsrc(a.tile, 256), OOB_OFF - 64u * (NST * g + i), 0, 0);
-#endif
   };
   // Whole rounds of 3 tiles only: a break between the tiles of a round
   // reaches the loop latch, and that (never taken) latch -> header path
@@ -781,12 +681,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     load_tile(k0 + min(j + 4, nk), Bv);
     process(k0 + j + 2, Cv, body);
   }
-#endif
-#if SRD_RING == 4
-  const uint64_t kr = km;
-#else
   const uint64_t kr = k0 + 3ull * nfull;
-#endif
   // the ring's remainder and the file's last <= 2 tiles (masked: a tail
   // tile's bytes past file_len read as 0; a no-op on the others)
   for (uint64_t k = kr; k < k1; k++) {

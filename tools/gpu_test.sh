@@ -4,4 +4,3 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ${PYTEST_ARGS} ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log
-if [ -n "$ABL" ]; then timeout -k 10 200 python tools/scan_ablate.py > gpurun_out/ablate.log 2>&1 || { echo ABL_FAIL; tail gpurun_out/ablate.log; exit 1; }; cat gpurun_out/ablate.log; fi
