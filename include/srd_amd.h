@@ -61,6 +61,12 @@ extern "C" {
 /* option flags */
 #define SRD_FLAG_FORCE_FULL 1u   /* skip the optimistic (strong-candidate) pass */
 #define SRD_FLAG_NO_CRC 2u       /* structural recovery + index only */
+/* host-input staging (srd_validate_index / _multi).  Default: pinned input is
+ * copied directly; otherwise the mapped range is hipHostRegister'ed
+ * (read-only) for one DMA copy, and when registration is refused host threads
+ * fill double-buffered pinned bounce buffers while the previous chunks DMA. */
+#define SRD_FLAG_STAGE_PAGEABLE 4u /* one pageable hipMemcpy (measurement baseline) */
+#define SRD_FLAG_STAGE_BOUNCE 8u   /* bounce buffers without trying registration */
 
 typedef struct srd_ctx srd_ctx; /* one device + stream + reusable workspace */
 
@@ -162,6 +168,31 @@ typedef srd_device_result srd_result;
 int srd_validate_index(srd_ctx *ctx, const uint8_t *file, uint64_t file_len,
                        uint32_t flags, srd_result *out);
 void srd_result_free(srd_result *res);
+
+/* DataStore::open of one host store (the mmap) on n GPUs in ONE process,
+ * without RCCL (data_store.rs:84-117).  ctxs[i] are contexts
+ * (one per GPU; the same device may repeat).  The host pre-pass
+ * srd_shard_cuts splits the store into n entry ranges; one host thread per
+ * context stages its span [span_off, hi) and runs srd_validate_span_device.
+ * The host composes the shards (every shard proven, each lo == the previous
+ * hi); then the chain arrays are concatenated and the per-shard indexes are
+ * gathered to ctxs[0]'s device (hipMemcpyPeer over xGMI) in shard order and
+ * merged latest-wins there (KeyIndexer::build, key_indexer.rs:98-124).  A
+ * store that does not compose (a torn tail, corruption, a wrong cut, a shard
+ * error) is decided by the whole-file path on ctxs[0].  The result is
+ * identical to srd_validate_index's. */
+int srd_validate_index_multi(srd_ctx *const *ctxs, uint32_t n_ctx,
+                             const uint8_t *file, uint64_t file_len,
+                             uint32_t flags, srd_result *out);
+/* Staging mode of the last host-input call on ctx: 0 pinned input, 1
+ * registered mapping, 2 bounce buffers, 3 pageable copy (-1 none yet). */
+int srd_ctx_stage_mode(srd_ctx *ctx);
+
+/* The index bucket hash on the device: out[i] = xxh3_64(le8(keys[i])), the
+ * Xxh3BuildHasher's Hasher::write (digest/xxh3_build_hasher.rs:11-13) the
+ * KeyIndexer HashMap applies to every key_hash.  Asynchronous on `stream`. */
+int srd_index_hash_device(srd_ctx *ctx, const uint64_t *d_keys, uint64_t n,
+                          uint64_t *d_out, void *stream);
 
 /* recover_valid_chain: final_len only (host input). */
 int srd_recover_valid_chain(srd_ctx *ctx, const uint8_t *file,

@@ -118,6 +118,27 @@ def chain(file, tail: int, compute_crc: bool = True) -> list[dict]:
     return [{f: getattr(out[i], f) for f, _ in Entry._fields_} for i in range(n)]
 
 
+def chain_arrays(file, tail: int, compute_crc: bool = True) -> np.ndarray:
+    """The chain as a numpy structured array (Entry fields), for large stores."""
+    a = as_u8(file)
+    n = lib().orc_chain(a.ctypes.data_as(C.c_void_p), tail, None, 0, 0)
+    out = (Entry * max(n, 1))()
+    lib().orc_chain(a.ctypes.data_as(C.c_void_p), tail, out, n, int(compute_crc))
+    dt = np.dtype([(f, np.uint64 if t is C.c_uint64 else np.uint32) for f, t in Entry._fields_])
+    return np.frombuffer(bytes(out), dt)[:n].copy()
+
+
+def key_indexer_arrays(file, tail: int) -> tuple[np.ndarray, np.ndarray]:
+    """KeyIndexer::build as (keys, packed) arrays, sorted by key_hash."""
+    a = as_u8(file)
+    cap = max(1, lib().orc_chain(a.ctypes.data_as(C.c_void_p), tail, None, 0, 0))
+    k = np.zeros(cap, np.uint64)
+    v = np.zeros(cap, np.uint64)
+    n = lib().orc_key_indexer_build(a.ctypes.data_as(C.c_void_p), tail,
+                                    k.ctypes.data_as(_u64p), v.ctypes.data_as(_u64p), cap)
+    return k[:n], v[:n]
+
+
 def key_indexer_build(file, tail: int) -> dict[int, int]:
     """key_indexer.rs:98-124 -> {key_hash: packed}"""
     a = as_u8(file)

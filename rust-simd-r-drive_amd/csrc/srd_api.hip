@@ -13,9 +13,11 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "srd_amd.h"
+#include "srd_host.cpp"
 #include "srd_kernels.hip"
 #include "srd_glue.hip"
 #include "srd_writer.hip"
@@ -86,6 +88,12 @@ struct Ctx {
   hipStream_t cstream = nullptr;
   hipEvent_t wev_copied[2] = {nullptr, nullptr}, wev_done[2] = {nullptr, nullptr};
   void* pin_ent[2] = {nullptr, nullptr};
+  // host-input staging (stage_host): bounce buffers, one stream per worker
+  int stage_workers = 8;
+  int stage_mode = -1;  // last call: 0 pinned input, 1 registered, 2 bounce buffers, 3 pageable
+  std::vector<void*> stage_pin;
+  std::vector<hipStream_t> stage_streams;
+  std::vector<hipEvent_t> stage_ev;
 };
 
 enum BufId {
@@ -103,6 +111,7 @@ enum BufId {
   B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST, B_XPART,
+  B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_COUNT_
 };
 
@@ -303,6 +312,7 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   if (r) { delete c; return r; }
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipHostMalloc((void**)&c->h_plan, sizeof(Plan), hipHostMallocDefault));
+  c->stage_workers = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->scan_blocks = (unsigned)ncu;
@@ -325,6 +335,12 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
     if (c->wev_done[i]) hipEventDestroy(c->wev_done[i]);
   }
   if (c->cstream) hipStreamDestroy(c->cstream);
+  for (auto p : c->stage_pin)
+    if (p) hipHostFree(p);
+  for (auto e : c->stage_ev)
+    if (e) hipEventDestroy(e);
+  for (auto st : c->stage_streams)
+    if (st) hipStreamDestroy(st);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -974,15 +990,13 @@ extern "C" int srd_index_partition_device(srd_ctx* c, const uint64_t* d_keys, co
 
 __global__ void set_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
 
-extern "C" int srd_index_build_device(srd_ctx* c, const uint64_t* d_pairs, uint64_t n, uint64_t* d_out_keys,
-                                      uint64_t* d_out_packed, uint64_t* n_index) {
-  if (!c || !n_index || (n && (!d_pairs || !d_out_keys || !d_out_packed))) { set_err("bad argument"); return SRD_ERR_ARG; }
-  if (n >= (1ull << 32) - 2) { set_err("too many pairs"); return SRD_ERR_ARG; }
-  HIPCHK(hipSetDevice(c->device));
+// KeyIndexer::build over n (key_hash, meta_off or packed) device pairs given
+// as two arrays, in file order (latest position wins); output in chain order
+// of each key's latest entry.  Synchronises.
+static int index_build_sep(Ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, uint64_t* okeys,
+                           uint64_t* opacked, uint64_t* n_index) {
   *n_index = 0;
   if (!n) return 0;
-  TRY(ensure(c, B_MKEY, n * 8));
-  TRY(ensure(c, B_MVAL, n * 8));
   TRY(ensure(c, B_MPLAN, sizeof(Plan)));
   const uint32_t log2_nbk = index_log2_buckets(n);
   TRY(alloc_index(c, n, log2_nbk));
@@ -990,18 +1004,28 @@ extern "C" int srd_index_build_device(srd_ctx* c, const uint64_t* d_pairs, uint6
   HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
   set_u64_kernel<<<1, 1, 0, c->stream>>>(&pl->n_chain, n);
   KCHK(c, "set_u64_kernel");
+  TRY(launch_index_bucketed(c, keys, vals, &pl->n_chain, &pl->status, log2_nbk, okeys, opacked, pl));
+  HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->h_plan->idx_overflow) return index_global(c, n, n_index, keys, vals, okeys, opacked);
+  *n_index = c->h_plan->n_index;
+  return 0;
+}
+
+extern "C" int srd_index_build_device(srd_ctx* c, const uint64_t* d_pairs, uint64_t n, uint64_t* d_out_keys,
+                                      uint64_t* d_out_packed, uint64_t* n_index) {
+  if (!c || !n_index || (n && (!d_pairs || !d_out_keys || !d_out_packed))) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (n >= (1ull << 31)) { set_err("too many pairs"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
+  *n_index = 0;
+  if (!n) return 0;
+  TRY(ensure(c, B_MKEY, n * 8));
+  TRY(ensure(c, B_MVAL, n * 8));
   deinterleave_kernel<<<blocks(std::min<uint64_t>(n, 1 << 20), 256), 256, 0, c->stream>>>(
       d_pairs, n, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL));
   KCHK(c, "deinterleave_kernel");
   HIPCHK(hipGetLastError());
-  TRY(launch_index_bucketed(c, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL), &pl->n_chain, &pl->status, log2_nbk,
-                            d_out_keys, d_out_packed, pl));
-  HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  if (c->h_plan->idx_overflow)
-    return index_global(c, n, n_index, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL), d_out_keys, d_out_packed);
-  *n_index = c->h_plan->n_index;
-  return 0;
+  return index_build_sep(c, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL), n, d_out_keys, d_out_packed, n_index);
 }
 
 extern "C" int srd_ctx_timings(srd_ctx* c, double* scan_ms, int* scan_launches, double* total_ms) {
@@ -1116,63 +1140,30 @@ extern "C" uint64_t srd_padded_size(uint64_t flen) { return ((flen + TILE - 1) /
 
 // ---------------------------------------------------------- shard boundaries
 // Host pre-pass for the entry-range shards of an arbitrary store (SURVEY.md
-// 8(e)): cut r is a guessed entry tail at or below r*file_len/world.  A byte
-// t is taken as a tail when [t-20, t) passes recover_valid_chain's node test
-// (data_store.rs:404-421, 429-470) and the backward walk from it stays valid
-// for kCutHops hops without reaching offset 0 (so the first 8 entries are
-// never a cut).  The guess is checked, not trusted: the shards' chains
-// compose only if every cut is the tail the real chain passes through
-// (srd_shard.sharded_validate_index), and otherwise the caller runs the
-// whole-file path.
-static inline uint64_t host_rd64(const uint8_t* p) {
-  uint64_t v;
-  memcpy(&v, p, 8);
-  return v;
-}
-
-static bool host_node(const uint8_t* f, uint64_t flen, uint64_t t, uint64_t* prev) {
-  if (t < 20 || t > flen) return false;
-  const uint64_t mo = t - 20, p = host_rd64(f + mo + 8);
-  if (p >= mo) return false;
-  const uint64_t start = (mo - p == 1 && f[p] == 0) ? p : p + ((64 - (p & 63)) & 63);
-  if (start >= mo) return false;
-  *prev = p;
-  return true;
-}
-
-static constexpr int kCutHops = 8;
-static constexpr uint64_t kCutScan = 64ull << 20;  // bytes searched below a cut target
-
-static bool plausible_tail(const uint8_t* f, uint64_t flen, uint64_t t) {
-  uint64_t cur = t;
-  for (int h = 0; h < kCutHops; h++) {
-    uint64_t p;
-    if (!host_node(f, flen, cur, &p)) return false;
-    // p == 0 is what zero-filled payloads (and crc bytes read through a
-    // zero prepad) look like: a walk that reaches the root early is no cut
-    if (p == 0) return false;
-    cur = p;
-  }
-  return true;
-}
-
+// 8(e)); the parser lives in srd_host.cpp (no HIP, sanitizer-tested).
 extern "C" int srd_shard_cuts(const uint8_t* file, uint64_t flen, uint32_t world, uint64_t* cuts) {
-  if (!cuts || world == 0 || (!file && flen)) { set_err("bad argument"); return SRD_ERR_ARG; }
-  cuts[0] = 0;
-  cuts[world] = flen;
-  for (uint32_t r = 1; r < world; r++) {
-    const uint64_t target = (uint64_t)(((unsigned __int128)flen * r) / world);
-    const uint64_t floor_ = std::max(cuts[r - 1], target > kCutScan ? target - kCutScan : 0);
-    uint64_t got = cuts[r - 1];  // none found: an empty shard
-    for (uint64_t t = target; t > floor_; t--)
-      if (plausible_tail(file, flen, t)) { got = t; break; }
-    cuts[r] = got;
-  }
-  return 0;
+  const char* why = "";
+  const int r = srd_host::shard_cuts(file, flen, world, cuts, &why);
+  if (r) set_err(why);
+  return r;
 }
 
 // ---------------------------------------------------------------- host input
-static int stage_file(Ctx* c, const uint8_t* file, uint64_t flen, const uint8_t** d) {
+// The path starts in host memory: the mmap'd single-file store
+// (data_store.rs:172-174 init_mmap, called from open :84-117).  Staging modes:
+//  - already pinned host memory: one DMA copy;
+//  - default: hipHostRegister (read-only) of the mapped range, one DMA copy
+//    straight from the page cache, unregister;
+//  - registration refused (or SRD_FLAG_STAGE_BOUNCE): host threads copy
+//    16 MiB chunks into double-buffered pinned bounce buffers, each worker
+//    DMA-ing its previous chunk on its own stream meanwhile (the memcpy also
+//    takes the mapping's page faults on several cores);
+//  - SRD_FLAG_STAGE_PAGEABLE: one pageable hipMemcpy (the runtime's own
+//    staging; measurement baseline).
+constexpr uint32_t kStageFlags = SRD_FLAG_STAGE_PAGEABLE | SRD_FLAG_STAGE_BOUNCE;
+constexpr uint64_t kBounceBytes = 16ull << 20;
+
+static int ensure_file_buf(Ctx* c, uint64_t flen, uint8_t** d) {
   const uint64_t need = srd_padded_size(flen);
   if (c->file.n < need) {
     if (c->file.p) HIPCHK(hipFree(c->file.p));
@@ -1181,9 +1172,85 @@ static int stage_file(Ctx* c, const uint8_t* file, uint64_t flen, const uint8_t*
     if (hipMalloc(&c->file.p, need) != hipSuccess) { set_err("hipMalloc(file)"); return SRD_ERR_ALLOC; }
     c->file.n = need;
   }
-  if (flen) HIPCHK(hipMemcpyAsync(c->file.p, file, flen, hipMemcpyHostToDevice, c->stream));
-  *d = (const uint8_t*)c->file.p;
+  *d = (uint8_t*)c->file.p;
   return 0;
+}
+
+static int stage_bounce(Ctx* c, const uint8_t* src, uint64_t len, uint8_t* dst) {
+  const int T = c->stage_workers;
+  if (c->stage_pin.empty()) {
+    c->stage_pin.assign(2 * T, nullptr);
+    c->stage_streams.assign(T, nullptr);
+    c->stage_ev.assign(2 * T, nullptr);
+    for (int i = 0; i < 2 * T; i++) {
+      HIPCHK(hipHostMalloc(&c->stage_pin[i], kBounceBytes, hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
+    }
+    for (int w = 0; w < T; w++) HIPCHK(hipStreamCreateWithFlags(&c->stage_streams[w], hipStreamNonBlocking));
+  }
+  const uint64_t nch = (len + kBounceBytes - 1) / kBounceBytes;
+  std::vector<int> rc(T, 0);
+  auto work = [&](int w) {
+    if (hipSetDevice(c->device) != hipSuccess) { rc[w] = SRD_ERR_HIP; return; }
+    uint64_t j = 0;
+    for (uint64_t ch = w; ch < nch; ch += T, j++) {
+      const int b = 2 * w + (int)(j & 1);
+      if (j >= 2 && hipEventSynchronize(c->stage_ev[b]) != hipSuccess) { rc[w] = SRD_ERR_HIP; return; }
+      const uint64_t off = ch * kBounceBytes, n = std::min(kBounceBytes, len - off);
+      memcpy(c->stage_pin[b], src + off, n);
+      if (hipMemcpyAsync(dst + off, c->stage_pin[b], n, hipMemcpyHostToDevice, c->stage_streams[w]) != hipSuccess ||
+          hipEventRecord(c->stage_ev[b], c->stage_streams[w]) != hipSuccess) {
+        rc[w] = SRD_ERR_HIP;
+        return;
+      }
+    }
+    if (hipStreamSynchronize(c->stage_streams[w]) != hipSuccess) rc[w] = SRD_ERR_HIP;
+  };
+  std::vector<std::thread> th;
+  const int used = (int)std::min<uint64_t>((uint64_t)T, nch);
+  for (int w = 1; w < used; w++) th.emplace_back(work, w);
+  if (used) work(0);
+  for (auto& t : th) t.join();
+  for (int w = 0; w < T; w++)
+    if (rc[w]) { set_err("bounce-buffer staging failed"); return rc[w]; }
+  c->stage_mode = 2;
+  return 0;
+}
+
+// stage host bytes [src, src + len) into the context's device file buffer
+static int stage_host(Ctx* c, const uint8_t* src, uint64_t len, uint32_t flags, const uint8_t** d_out) {
+  uint8_t* d = nullptr;
+  TRY(ensure_file_buf(c, len, &d));
+  *d_out = d;
+  if (!len) return 0;
+  if (flags & SRD_FLAG_STAGE_PAGEABLE) {
+    HIPCHK(hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->stage_mode = 3;
+    return 0;
+  }
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, src) == hipSuccess && at.type == hipMemoryTypeHost) {
+    HIPCHK(hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream));  // already pinned
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->stage_mode = 0;
+    return 0;
+  }
+  (void)hipGetLastError();  // an unregistered pointer is not an error here
+  if (!(flags & SRD_FLAG_STAGE_BOUNCE)) {
+    const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095, e = ((uintptr_t)src + len + 4095) & ~(uintptr_t)4095;
+    if (hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly) == hipSuccess) {
+      const hipError_t e1 = hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream);
+      const hipError_t e2 = hipStreamSynchronize(c->stream);
+      hipHostUnregister((void*)a);
+      HIPCHK(e1);
+      HIPCHK(e2);
+      c->stage_mode = 1;
+      return 0;
+    }
+    (void)hipGetLastError();
+  }
+  return stage_bounce(c, src, len, d);
 }
 
 template <class T>
@@ -1198,9 +1265,9 @@ extern "C" int srd_validate_index(srd_ctx* c, const uint8_t* file, uint64_t flen
   if (!c || !out || (!file && flen)) { set_err("bad argument"); return SRD_ERR_ARG; }
   HIPCHK(hipSetDevice(c->device));
   const uint8_t* d = nullptr;
-  TRY(stage_file(c, file, flen, &d));
+  TRY(stage_host(c, file, flen, flags, &d));
   srd_device_result r;
-  TRY(srd_validate_index_device(c, d, flen, flags, &r));
+  TRY(srd_validate_index_device(c, d, flen, flags & ~kStageFlags, &r));
   *out = r;
   int rc = 0;
   uint64_t n = r.n_chain, ni = r.n_index;
@@ -1226,10 +1293,194 @@ extern "C" void srd_result_free(srd_result* r) {
   memset(r, 0, sizeof *r);
 }
 
+extern "C" int srd_ctx_stage_mode(srd_ctx* c) { return c ? c->stage_mode : -1; }
+
+// ---------------------------------------------------------------------------
+// DataStore::open on n GPUs in one process, no RCCL:
+// host cuts -> one host thread per context (stage span, validate span) ->
+// host composition -> chain arrays concatenated, shard indexes gathered to
+// ctxs[0] (peer copies) and merged latest-wins there in shard = file order.
+static void enable_peer(int dev0, int dev) {
+  static std::mutex mu;
+  static uint64_t done[64] = {};
+  if (dev0 == dev || dev0 >= 64 || dev >= 64) return;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done[dev0] & (1ull << dev)) return;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, dev0, dev) == hipSuccess && can) (void)hipDeviceEnablePeerAccess(dev, 0);
+  (void)hipGetLastError();  // already enabled / unsupported: copies still work (staged)
+  done[dev0] |= 1ull << dev;
+}
+
+extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const uint8_t* file, uint64_t flen,
+                                        uint32_t flags, srd_result* out) {
+  if (!ctxs || !nc || !out || (!file && flen)) { set_err("bad argument"); return SRD_ERR_ARG; }
+  for (uint32_t i = 0; i < nc; i++)
+    if (!ctxs[i]) { set_err("bad argument: null context"); return SRD_ERR_ARG; }
+  if (nc == 1) return srd_validate_index(ctxs[0], file, flen, flags, out);
+  std::vector<uint64_t> cuts(nc + 1);
+  {
+    const char* why = "";
+    const int r = srd_host::shard_cuts(file, flen, nc, cuts.data(), &why);
+    if (r) { set_err(why); return r; }
+  }
+  struct Shard {
+    int rc = 0;
+    std::string err;
+    srd_device_result r{};
+    bool proven = false;
+  };
+  std::vector<Shard> sh(nc);
+  const uint32_t vflags = flags & ~kStageFlags;
+  auto run = [&](uint32_t i) {
+    srd_ctx* c = ctxs[i];
+    Shard& s = sh[i];
+    const uint64_t lo = cuts[i], hi = cuts[i + 1];
+    if (lo == hi) { s.proven = true; return; }  // an empty shard composes trivially
+    if (hipSetDevice(c->device) != hipSuccess) { s.rc = SRD_ERR_HIP; s.err = "hipSetDevice"; return; }
+    const uint64_t span_off = lo - lo % SPAN_BYTES;
+    const uint8_t* d = nullptr;
+    s.rc = stage_host(c, file + span_off, hi - span_off, flags, &d);
+    if (!s.rc) s.rc = srd_validate_span_device(c, d, span_off, lo, hi, vflags, &s.r);
+    if (s.rc) { s.err = g_err; return; }
+    s.proven = s.r.final_len == hi && s.r.mode != SRD_MODE_SPAN_UNPROVEN;
+  };
+  {
+    std::vector<std::thread> th;
+    for (uint32_t i = 1; i < nc; i++) th.emplace_back(run, i);
+    run(0);
+    for (auto& t : th) t.join();
+  }
+  bool composed = true;
+  for (auto& x : sh) composed = composed && !x.rc && x.proven;
+  // a torn tail, corruption, a cut that is no chain tail, or a shard that
+  // failed (capacity, allocation): recover_valid_chain's byte-wise search is
+  // global, so the whole-file path decides
+  if (!composed) return srd_validate_index(ctxs[0], file, flen, flags, out);
+
+  memset(out, 0, sizeof *out);
+  std::vector<uint64_t> cb(nc), ib(nc);
+  uint64_t N = 0, NI = 0, bad = 0, cand = 0;
+  bool all_opt = true;
+  for (uint32_t i = 0; i < nc; i++) {
+    cb[i] = N;
+    ib[i] = NI;
+    N += sh[i].r.n_chain;
+    NI += sh[i].r.n_index;
+    bad += sh[i].r.n_crc_bad;
+    cand += sh[i].r.n_candidates;
+    if (cuts[i] != cuts[i + 1] && sh[i].r.mode != SRD_MODE_OPTIMISTIC) all_opt = false;
+  }
+  const uint64_t n1 = std::max<uint64_t>(N, 1);
+  out->meta_off = (uint64_t*)malloc(n1 * 8);
+  out->key_hash = (uint64_t*)malloc(n1 * 8);
+  out->prev_offset = (uint64_t*)malloc(n1 * 8);
+  out->payload_start = (uint64_t*)malloc(n1 * 8);
+  out->payload_len = (uint64_t*)malloc(n1 * 8);
+  out->crc_stored = (uint32_t*)malloc(n1 * 4);
+  out->crc_computed = (uint32_t*)malloc(n1 * 4);
+  out->crc_ok = (uint8_t*)malloc(n1);
+  if (!out->meta_off || !out->key_hash || !out->prev_offset || !out->payload_start || !out->payload_len ||
+      !out->crc_stored || !out->crc_computed || !out->crc_ok) {
+    srd_result_free(out);
+    set_err("host allocation failed");
+    return SRD_ERR_ALLOC;
+  }
+  // chain arrays: each shard's segment D2H on its own stream (file order)
+  std::vector<int> rc(nc, 0);
+  auto pull = [&](uint32_t i) {
+    srd_ctx* c = ctxs[i];
+    const srd_device_result& r = sh[i].r;
+    const uint64_t n = r.n_chain, b = cb[i];
+    if (!n) return;
+    if (hipSetDevice(c->device) != hipSuccess) { rc[i] = SRD_ERR_HIP; return; }
+    hipError_t e = hipSuccess;
+    auto cp = [&](void* dst, const void* src, uint64_t bytes) {
+      if (e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
+    };
+    cp(out->meta_off + b, r.meta_off, n * 8);
+    cp(out->key_hash + b, r.key_hash, n * 8);
+    cp(out->prev_offset + b, r.prev_offset, n * 8);
+    cp(out->payload_start + b, r.payload_start, n * 8);
+    cp(out->payload_len + b, r.payload_len, n * 8);
+    cp(out->crc_stored + b, r.crc_stored, n * 4);
+    cp(out->crc_computed + b, r.crc_computed, n * 4);
+    cp(out->crc_ok + b, r.crc_ok, n);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc[i] = SRD_ERR_HIP;
+  };
+  {
+    std::vector<std::thread> th;
+    for (uint32_t i = 1; i < nc; i++) th.emplace_back(pull, i);
+    pull(0);
+    for (auto& t : th) t.join();
+  }
+  for (uint32_t i = 0; i < nc; i++)
+    if (rc[i]) { srd_result_free(out); set_err("chain copy failed"); return rc[i]; }
+  // index: the shards' indexes to ctxs[0] in shard order, then latest wins
+  Ctx* c0 = ctxs[0];
+  int r = 0;
+  uint64_t ni = 0;
+  do {
+    if (hipSetDevice(c0->device) != hipSuccess) { r = SRD_ERR_HIP; set_err("hipSetDevice"); break; }
+    const uint64_t m1 = std::max<uint64_t>(NI, 1);
+    if ((r = ensure(c0, B_GKEY, m1 * 8)) || (r = ensure(c0, B_GVAL, m1 * 8)) || (r = ensure(c0, B_GOKEY, m1 * 8)) ||
+        (r = ensure(c0, B_GOPACKED, m1 * 8)))
+      break;
+    hipError_t e = hipSuccess;
+    for (uint32_t i = 0; i < nc && e == hipSuccess; i++) {
+      const uint64_t n = sh[i].r.n_index;
+      if (!n) continue;
+      enable_peer(c0->device, ctxs[i]->device);
+      e = hipMemcpyPeerAsync(P<uint64_t>(c0, B_GKEY) + ib[i], c0->device, sh[i].r.index_key_hash, ctxs[i]->device,
+                             n * 8, c0->stream);
+      if (e == hipSuccess)
+        e = hipMemcpyPeerAsync(P<uint64_t>(c0, B_GVAL) + ib[i], c0->device, sh[i].r.index_packed, ctxs[i]->device,
+                               n * 8, c0->stream);
+    }
+    if (e != hipSuccess) { r = SRD_ERR_HIP; set_err(std::string("index gather: ") + hipGetErrorString(e)); break; }
+    if ((r = index_build_sep(c0, P<uint64_t>(c0, B_GKEY), P<uint64_t>(c0, B_GVAL), NI, P<uint64_t>(c0, B_GOKEY),
+                             P<uint64_t>(c0, B_GOPACKED), &ni)))
+      break;
+    const uint64_t k1 = std::max<uint64_t>(ni, 1);
+    out->index_key_hash = (uint64_t*)malloc(k1 * 8);
+    out->index_packed = (uint64_t*)malloc(k1 * 8);
+    if (!out->index_key_hash || !out->index_packed) { r = SRD_ERR_ALLOC; set_err("host allocation failed"); break; }
+    if (ni) {
+      e = hipMemcpyAsync(out->index_key_hash, P<uint64_t>(c0, B_GOKEY), ni * 8, hipMemcpyDeviceToHost, c0->stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(out->index_packed, P<uint64_t>(c0, B_GOPACKED), ni * 8, hipMemcpyDeviceToHost, c0->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
+      if (e != hipSuccess) { r = SRD_ERR_HIP; set_err("index copy failed"); break; }
+    }
+  } while (0);
+  if (r) { srd_result_free(out); return r; }
+  out->file_len = flen;
+  out->final_len = flen;
+  out->n_chain = N;
+  out->n_index = ni;
+  out->n_crc_bad = bad;
+  out->n_candidates = cand;
+  out->mode = all_opt ? SRD_MODE_OPTIMISTIC : SRD_MODE_FULL;
+  return 0;
+}
+
+extern "C" int srd_index_hash_device(srd_ctx* c, const uint64_t* d_keys, uint64_t n, uint64_t* d_out, void* stream) {
+  if (!c || (n && (!d_keys || !d_out))) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (!n) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  index_hash_kernel<<<(unsigned)std::min<uint64_t>((n + 255) / 256, 8192), 256, 0,
+                      stream ? (hipStream_t)stream : c->stream>>>(d_keys, n, d_out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 extern "C" int srd_recover_valid_chain(srd_ctx* c, const uint8_t* file, uint64_t flen, uint64_t* final_len) {
   if (!final_len) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
   const uint8_t* d = nullptr;
-  TRY(stage_file(c, file, flen, &d));
+  TRY(stage_host(c, file, flen, 0, &d));
   srd_device_result r;
   TRY(srd_validate_index_device(c, d, flen, SRD_FLAG_NO_CRC, &r));
   *final_len = r.final_len;
@@ -1239,8 +1490,10 @@ extern "C" int srd_recover_valid_chain(srd_ctx* c, const uint8_t* file, uint64_t
 extern "C" int srd_key_indexer_build(srd_ctx* c, const uint8_t* file, uint64_t tail, uint64_t* keys,
                                      uint64_t* packed, uint64_t cap, uint64_t* n_out) {
   if (!n_out) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
   const uint8_t* d = nullptr;
-  TRY(stage_file(c, file, tail, &d));
+  TRY(stage_host(c, file, tail, 0, &d));
   srd_device_result r;
   TRY(srd_validate_index_device(c, d, tail, SRD_FLAG_NO_CRC, &r));
   if (r.final_len != tail) {
@@ -1394,26 +1647,11 @@ extern "C" int srd_synth_span_device(srd_ctx* c, uint8_t* d_span, uint64_t span_
 extern "C" int srd_batch_layout(uint64_t tail, const uint8_t* payloads, const uint64_t* key_offs,
                                 const uint64_t* key_lens, const uint64_t* pay_offs, const uint64_t* pay_lens,
                                 uint64_t n, uint32_t flags, srd_write_entry* out, uint64_t* new_tail) {
-  if (n && (!key_offs || !key_lens || !pay_offs || !pay_lens)) { set_err("bad argument"); return SRD_ERR_ARG; }
-  for (uint64_t i = 0; i < n; i++) {
-    const uint64_t len = pay_lens[i];
-    if (key_lens[i] > 0xFFFFFFFFull) { set_err("key too long"); return SRD_ERR_ARG; }
-    srd_write_entry e{pay_offs[i], len, key_offs[i], tail, (uint32_t)key_lens[i], 0u};
-    if (payloads && len == 1 && payloads[pay_offs[i]] == 0) {  // payload == NULL_BYTE (data_store.rs:864)
-      if (!(flags & SRD_WRITE_ALLOW_NULL)) {
-        set_err("NULL-byte payloads cannot be written directly.");
-        return SRD_ERR_ARG;
-      }
-      e.flags = SRD_ENTRY_TOMB;
-      tail += 1 + 20;  // no prepad for a tombstone (:871-895)
-    } else {
-      if (len == 0) { set_err("Payload cannot be empty."); return SRD_ERR_ARG; }
-      tail += ((64 - (tail & 63)) & 63) + len + 20;  // prepad_len (:670-673), payload, metadata
-    }
-    if (out) out[i] = e;
-  }
-  if (new_tail) *new_tail = tail;
-  return 0;
+  const char* why = "";
+  const int r = srd_host::batch_layout(tail, payloads, key_offs, key_lens, pay_offs, pay_lens, n, flags, out, new_tail,
+                                       &why);
+  if (r) set_err(why);
+  return r;
 }
 
 static int launch_write(Ctx* c, hipStream_t s, const uint8_t* pay, const uint8_t* keys, const srd_write_entry* ent,

@@ -1200,6 +1200,11 @@ __global__ void index_latest_kernel(const uint64_t* kh, const uint64_t* mo, uint
   }
   latest[c] = best == v;
 }
+// Xxh3BuildHasher over a key_hash (xxh3_build_hasher.rs:11-13): xxh3_64(le8(k))
+__global__ void index_hash_kernel(const uint64_t* keys, uint64_t n, uint64_t* out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = xxh3_64_u64(keys[i]);
+}
 __global__ void index_emit_kernel(const uint64_t* kh, const uint64_t* mo, const uint32_t* latest,
                                   const uint32_t* pos, uint64_t n, uint64_t* okey, uint64_t* opacked) {
   uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

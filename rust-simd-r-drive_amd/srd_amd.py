@@ -30,6 +30,9 @@ LIB_PATH = os.environ.get("SRD_LIB_PATH") or os.path.join(HERE, "build", "libsrd
 
 SRD_FLAG_FORCE_FULL = 1
 SRD_FLAG_NO_CRC = 2
+SRD_FLAG_STAGE_PAGEABLE = 4  # host input: one pageable hipMemcpy (measurement baseline)
+SRD_FLAG_STAGE_BOUNCE = 8    # host input: pinned bounce buffers, no hipHostRegister
+STAGE_MODES = {0: "pinned input", 1: "registered mapping", 2: "bounce buffers", 3: "pageable copy"}
 SRD_MODE_OPTIMISTIC = 0
 SRD_MODE_FULL = 1
 SRD_MODE_SPAN_UNPROVEN = 3
@@ -51,7 +54,7 @@ EXPORTS = [
     "srd_index_table_bytes", "srd_index_table_build_device", "srd_index_get_packed_device",
     "srd_batch_read_hashed_device", "srd_batch_read",
     "srd_iter_entries_device", "srd_estimate_compaction_savings_device", "srd_compact_device",
-    "srd_shard_cuts",
+    "srd_shard_cuts", "srd_validate_index_multi", "srd_ctx_stage_mode", "srd_index_hash_device",
 ]
 
 
@@ -126,6 +129,9 @@ def lib():
         L.srd_iter_entries_device.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp, C.POINTER(u64)]
         L.srd_estimate_compaction_savings_device.argtypes = [vp, vp, u64, vp, u64, C.POINTER(u64)]
         L.srd_compact_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, C.POINTER(u64), vp, vp]
+        L.srd_validate_index_multi.argtypes = [C.POINTER(vp), u32, vp, u64, u32, C.POINTER(DeviceResult)]
+        L.srd_ctx_stage_mode.argtypes = [vp]
+        L.srd_index_hash_device.argtypes = [vp, vp, u64, vp, vp]
         for f in EXPORTS:
             if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
                          "srd_padded_size", "srd_index_table_bytes"):
@@ -180,6 +186,10 @@ class Context:
     @property
     def stream(self) -> int:
         return lib().srd_ctx_stream(self.h)
+
+    def stage_mode(self) -> str:
+        """How the last host-input call staged the store (STAGE_MODES)."""
+        return STAGE_MODES.get(lib().srd_ctx_stage_mode(self.h), "none")
 
 
 _default_ctx = None
@@ -252,6 +262,27 @@ def validate_index(file, flags: int = 0, ctx: Context | None = None) -> Result:
         return Result(r)
     finally:
         lib().srd_result_free(C.byref(r))
+
+
+def validate_index_multi(file, ctxs, flags: int = 0) -> Result:
+    """DataStore::open's pass over one host store on len(ctxs) GPUs in one
+    process (srd_validate_index_multi): entry-range shards, host composition,
+    index merged latest-wins on ctxs[0]'s device; no RCCL.  Same result as
+    validate_index."""
+    a = _u8(file)
+    hs = (C.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
+    r = DeviceResult()
+    _check(lib().srd_validate_index_multi(hs, len(ctxs), _ptr(a), a.size, flags, C.byref(r)))
+    try:
+        return Result(r)
+    finally:
+        lib().srd_result_free(C.byref(r))
+
+
+def index_hash_device(d_keys: int, n: int, d_out: int, ctx: Context | None = None) -> None:
+    """xxh3_64(le8(k)) per key on the device (the KeyIndexer's Xxh3BuildHasher)."""
+    ctx = ctx or default_ctx()
+    _check(lib().srd_index_hash_device(ctx.h, C.c_void_p(d_keys), n, C.c_void_p(d_out), C.c_void_p(ctx.stream)))
 
 
 def validate_index_device(d_ptr: int, file_len: int, flags: int = 0, ctx: Context | None = None) -> DeviceResult:
@@ -448,13 +479,21 @@ class DataStore:
         self._pos = {int(m): i for i, m in enumerate(result.meta_off)}
 
     @classmethod
-    def open(cls, path, ctx: Context | None = None) -> "DataStore":
+    def open(cls, path, ctx: Context | None = None, ctxs=None, flags: int = 0) -> "DataStore":
+        """ctxs: contexts of several GPUs (one process, srd_validate_index_multi);
+        otherwise ctx (default: the default context).  The mapping is handed to
+        the library as is; it stages it (registered mapping or bounce buffers)."""
         with open(path, "a+b"):
             pass
         size = os.path.getsize(path)
         with open(path, "r+b") as f:
             mm = _mmap.mmap(f.fileno(), 0, access=_mmap.ACCESS_READ) if size else b""
-            res = validate_index(np.frombuffer(mm, np.uint8) if size else b"", ctx=ctx)
+            view = np.frombuffer(mm, np.uint8) if size else b""
+            if ctxs and len(ctxs) > 1:
+                res = validate_index_multi(view, ctxs, flags)
+            else:
+                res = validate_index(view, flags, ctx=(ctxs[0] if ctxs else ctx))
+            del view
         if res.final_len < size:
             # data_store.rs:91-104: warn, truncate to the valid tail, re-open
             import warnings
@@ -464,7 +503,7 @@ class DataStore:
             with open(path, "r+b") as f:
                 f.truncate(res.final_len)
                 os.fsync(f.fileno())
-            return cls.open(path, ctx)
+            return cls.open(path, ctx, ctxs, flags)
         return cls(path, mm, res)
 
     def read_entry(self, key_hash: int):

@@ -69,7 +69,9 @@ class ShardedResult:
     n_index: int            # global KeyIndexer size (disjoint union of owner indexes)
     owner_keys: torch.Tensor    # this rank's part of the global index (key_hash as int64 bits)
     owner_packed: torch.Tensor  # pack(tag16, offset48) as int64 bits
-    local: object = None        # backend's shard-local result (chain arrays)
+    local: object = None        # backend's shard-local result (chain arrays in the context's device
+                                # buffers: valid until the next call on that context), or the
+                                # exception of a failed shard
 
 
 class HipBackend:
@@ -142,12 +144,19 @@ def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, h
     # collectives run where the backend lives: device memory for nccl (RCCL
     # over xGMI), host memory for gloo (CPU tests, several ranks on one GPU)
     cd = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
+    keys = packed = torch.empty(0, dtype=torch.int64, device=dev)
+    local = None
     if lo == hi:  # an empty shard (srd_shard_cuts found no tail in its range): composes trivially
         st = ShardStatus(True, lo, hi, 0, 0)
-        keys = packed = torch.empty(0, dtype=torch.int64, device=dev)
-        local = None
     else:
-        st, keys, packed, local = backend.validate_span(buf, span_off, lo, hi)
+        # a rank whose shard fails (an argument, capacity or allocation error)
+        # still joins every collective below with proven = False, so all
+        # ranks reach the same "not composed" decision (no rank blocks)
+        try:
+            st, keys, packed, local = backend.validate_span(buf, span_off, lo, hi)
+        except (S.SrdError, RuntimeError) as e:
+            st = ShardStatus(False, lo, hi, 0, 0)
+            local = e
     # owner partition of the shard-local index (needed only when the shards
     # compose, but done first so that one all_gather carries both the
     # boundary rows and every rank's per-owner send counts)
