@@ -10,8 +10,9 @@ payload + compare (is_valid_checksum), and the latest-wins index rebuild
 ranks / max-over-ranks wall time of K steps.
 
 N>1 (torchrun, one process per GPU): ONE global store of N x --entries-per-gpu
-entries, sharded by entry range (SURVEY.md 8(e), config C4 at N=8 with 2^21
-entries per GPU): rank r holds entries [r*n, (r+1)*n) in its HBM and a step
+entries (default 2^21: the C4 partition, so N=8 is exactly C4 -- 16M x 4 KiB,
+65 GiB -- and N=1/2/4 its prefixes), sharded by entry range:
+rank r holds entries [r*n, (r+1)*n) in its HBM and a step
 is srd_shard.sharded_validate_index -- its shard's validate+index
 (srd_validate_span_device), the boundary composition check (all_gather) and
 the owner-partitioned index exchange (all_to_all over RCCL, 16 B per key) +
@@ -41,19 +42,54 @@ import srd_amd as S  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+def kernel_sources_hash() -> str:
+    """sha256 over the HIP sources of the library (the PMC traffic in
+    profiles/traffic.json is reported only for the sources it was measured on)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(ROOT, "rust-simd-r-drive_amd", "csrc", "*"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()
+
+
 def algorithmic_bytes(n_entries: int, payload: int) -> int:
     return n_entries * (payload + 20)  # SURVEY.md 8(d): sum(L_i + 20)
+
+
+def host_cpus():
+    """CPU model, the machine's logical CPUs, and the CPUs this process may
+    use (affinity mask, capped by a cgroup CPU quota when one is set)."""
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "machine_logical_cpus": os.cpu_count(), "affinity_cpus": usable,
+            "cgroup_cpu_quota": quota, "usable": min(usable, quota) if quota else usable}
 
 
 def cpu_baseline(store_dev: torch.Tensor, size: int, bytes_alg: int, budget_s: float):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # the checker / CPU restatement (test infrastructure)
 
+    cpus = host_cpus()
     host = store_dev[:size].cpu().numpy()
     O.validate_index(host[: min(size, 1 << 26)], 1)  # warm the page cache / tables
     res = {}
-    for threads in (1, os.cpu_count() or 1):
-        threads = min(threads, 16)
+    for threads in sorted({1, cpus["usable"]}):
         reps, t0 = 0, time.perf_counter()
         while True:
             st = O.validate_index(host, threads)
@@ -64,16 +100,86 @@ def cpu_baseline(store_dev: torch.Tensor, size: int, bytes_alg: int, budget_s: f
         res[threads] = (bytes_alg / dt / 2**30, st, dt)
     one = res[1]
     allc = max(k for k in res)
+    # C1 (BASELINE configs[0], benches/storage_benchmark.rs shape at 1000 x
+    # 4 KiB): the same CPU open+validate+index on the plumbing-size store
+    c1 = O.synth_store(1000)
+    O.validate_index(c1, 1)
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        O.validate_index(c1, 1)
+        reps += 1
+    c1_ms = (time.perf_counter() - t0) / reps * 1e3
     return {
         "value": round(one[0], 3),
         "unit": "GiB/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"full C2 store ({size} B), oracle/srd_oracle.c faithful single-thread open()+"
-        f"is_valid_checksum per chain entry (PCLMUL CRC), {one[2]*1e3:.1f} ms/pass",
-        "all_cores": {"value": round(res[allc][0], 3), "cores": allc, "ms_per_pass": round(res[allc][2] * 1e3, 2)},
+        "sample": f"full C2 store ({size} B) in host RAM (page cache warm: the bytes are resident, no I/O), "
+        f"oracle/srd_oracle.c faithful single-thread open() + is_valid_checksum per chain entry "
+        f"(PCLMUL CRC), {one[2]*1e3:.1f} ms/pass",
+        "host": cpus,
+        "all_cores": {"value": round(res[allc][0], 3), "cores": allc, "ms_per_pass": round(res[allc][2] * 1e3, 2),
+                      "note": "CRC pass split over the usable CPUs (par_iter_entries analogue)"},
+        "c1_plumbing": {"entries": 1000, "store_bytes": int(c1.size), "ms_per_open": round(c1_ms, 3),
+                        "cores": 1},
         "check": {"final_len": one[1].final_len, "n_chain": one[1].n_chain, "n_index": one[1].n_index},
     }
+
+
+def e2e(store, size, bytes_alg, ctx, reps=3):
+    """End to end from host memory (the path starts in the mmap'd file,
+    data_store.rs:172-174): host bytes -> HBM -> validate+index -> host
+    result arrays (srd_validate_index).  Variants: a pinned host buffer; the
+    store as a FILE, opened with DataStore.open (mmap, page cache warm) under
+    each staging mode; the same file after posix_fadvise(DONTNEED) (cold
+    page cache, when the kernel honours it)."""
+    import tempfile
+    res = {"store_bytes": size}
+
+    def timed(fn):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        return (time.perf_counter() - t0) / reps, r
+
+    host = torch.empty(size, dtype=torch.uint8).pin_memory()
+    host.copy_(store[:size])
+    torch.cuda.synchronize()
+    dt, r = timed(lambda: S.validate_index(host.numpy(), 0, ctx))
+    assert r.final_len == size
+    res["pinned_buffer"] = {"ms": round(dt * 1e3, 2), "GiBps": round(bytes_alg / dt / 2**30, 3)}
+    del host
+    d = tempfile.mkdtemp(prefix="srd_e2e_")
+    path = os.path.join(d, "c2.store")
+    try:
+        with open(path, "wb") as f:
+            store[:size].cpu().numpy().tofile(f)
+            f.flush()
+            os.fsync(f.fileno())
+        for name, flags in (("mmap_default", 0), ("mmap_bounce", S.SRD_FLAG_STAGE_BOUNCE),
+                            ("mmap_pageable", S.SRD_FLAG_STAGE_PAGEABLE)):
+            dt, ds = timed(lambda: S.DataStore.open(path, ctx, flags=flags))
+            assert ds.tail_offset == size
+            res[name] = {"ms": round(dt * 1e3, 2), "GiBps": round(bytes_alg / dt / 2**30, 3),
+                         "staging": ctx.stage_mode()}
+            del ds
+        fd = os.open(path, os.O_RDONLY)
+        os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+        os.close(fd)
+        t0 = time.perf_counter()
+        ds = S.DataStore.open(path, ctx)
+        dt = time.perf_counter() - t0
+        res["mmap_after_fadvise_dontneed"] = {"ms": round(dt * 1e3, 2), "GiBps": round(bytes_alg / dt / 2**30, 3),
+                                              "staging": ctx.stage_mode()}
+        del ds
+    finally:
+        try:
+            os.remove(path)
+            os.rmdir(d)
+        except OSError:
+            pass
+    return {"e2e": res}
 
 
 def bench_c5(args, ctx, local):
@@ -281,8 +387,8 @@ def main():
     if args.config == "ops":
         return bench_ops(args, ctx, local)
     n, L = args.entries_per_gpu, args.payload
-    if n is None:
-        n = 1 << 20 if args.config == "c2" else 10_000_000
+    if n is None:  # N=1: C2 (1M x 4 KiB); N>1: the C4 partition (2^21 per GPU; N=8 is C4)
+        n = (1 << 20 if world == 1 else 1 << 21) if args.config == "c2" else 10_000_000
     lens, seed = None, 0x5EED0001
     if args.config == "c3":
         lens, seed = S.zipf_lens(n * world), 0x5EED0004
@@ -346,13 +452,18 @@ def main():
     value = bytes_alg * world / dt * args.steps / 2**30
     scan_ms = scan_ms_sum / max(scan_n, 1)
     achieved = bytes_alg / (scan_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, traffic_note = None, None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tf) and world == 1 and n == 1 << 20 and L == 4096 and args.config == "c2":  # measured on the C2 workload only
+    if world == 1 and n == 1 << 20 and L == 4096 and args.config == "c2":  # measured on the C2 workload only
         try:
-            traffic = json.load(open(tf)).get("scan_kernel_hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+            t = json.load(open(tf))
+            if t.get("kernel_sources_sha256") == kernel_sources_hash():
+                traffic = t.get("scan_kernel_hbm_bytes_per_launch")
+                traffic_note = f"PMC FETCH_SIZE x2 (gfx950) + WRITE_SIZE of these kernel sources ({t.get('measured')})"
+            else:
+                traffic_note = "profiles/traffic.json was measured on other kernel sources: not reported"
+        except (OSError, ValueError):
+            traffic_note = "no profiles/traffic.json"
 
     out = {
         "metric": "GiB/s hashed (device-resident), full-file validate+index scan",
@@ -371,7 +482,9 @@ def main():
             "workload": (f"{args.config.upper()}: {n} x " + (f"{L} B" if lens is None else "Zipf 64 B..1 MiB") +
                          f" entries, {size} B store, validate+index (recover_valid_chain + CRC-32 every payload + "
                          f"KeyIndexer::build)") if world == 1 else
-                        (f"{args.config.upper()}: {n * world} entries, one store sharded by entry range over {world} "
+                        ((f"C4 partition ({'= C4' if world == 8 else f'prefix of C4, {world} of its 8 shards'})"
+                          if args.config == "c2" and n == 1 << 21 and L == 4096 else args.config.upper()) +
+                         f": {n * world} x {L} B entries, one store sharded by entry range over {world} "
                          f"GPUs ({n} entries per GPU), validate+index + index exchange"),
             "entries_per_gpu": n,
             "payload_bytes": L,
@@ -390,21 +503,17 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_note": traffic_note,
+            # the whole step (scan + glue + one host sync) against the same peak
+            "step_achieved": round(bytes_alg * world / (ms_per_step * 1e-3) / 1e9 / world, 1),
+            "step_frac": round(bytes_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu and args.config == "c2":
         out["cpu_baseline"] = cpu_baseline(store, size, bytes_alg, args.cpu_budget)
     if args.e2e and rank == 0:
-        host = torch.empty(size, dtype=torch.uint8).pin_memory()
-        host.copy_(store[:size])
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(3):
-            res = S.validate_index(host.numpy(), 0, ctx)
-        e2e = (time.perf_counter() - t0) / 3
-        print(json.dumps({"e2e_host_to_index_ms": round(e2e * 1e3, 2),
-                          "e2e_GiBps": round(bytes_alg / e2e / 2**30, 3),
-                          "final_len": res.final_len}), file=sys.stderr)
+        out_e2e = e2e(store, size, bytes_alg, ctx)
+        print(json.dumps(out_e2e), file=sys.stderr, flush=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

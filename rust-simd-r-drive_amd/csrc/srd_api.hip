@@ -347,6 +347,13 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
 
 extern "C" void* srd_ctx_stream(srd_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+// Candidate slots per span grow x4 on overflow and are remembered by the
+// context; a store much smaller per span than the one that grew them starts
+// lower again, so the records (40 B per slot) stay within ~2x the store.
+static void fit_cap(Ctx* c, uint64_t n_spans, uint64_t bytes) {
+  while (c->cap > 64 && (uint64_t)c->cap * 40 * n_spans > 2 * bytes + (64ull << 20)) c->cap /= 4;
+}
+
 static int alloc_scan(Ctx* c, uint64_t n_tiles, uint64_t n_spans) {
   const uint64_t slots = n_spans * c->cap;
   TRY(ensure(c, B_TILE, n_tiles * 16));
@@ -524,6 +531,7 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
 static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uint64_t* K, uint64_t* h) {
   const uint64_t n_tiles = (flen + TILE - 1) / TILE;
   const uint64_t n_spans = (n_tiles + SPAN_TILES - 1) / SPAN_TILES;
+  fit_cap(c, n_spans, flen);
   while (true) {
     TRY(alloc_scan(c, n_tiles, n_spans));
     TRY(ensure_cub(c, n_spans + 1));
@@ -697,6 +705,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
   const uint64_t k_lo = span_off / TILE, s_lo = k_lo / SPAN_TILES;
   const uint64_t nt_rel = n_tiles - k_lo, ns_rel = n_spans - s_lo;
   const uint32_t coff = lo ? 0u : 1u;
+  fit_cap(c, ns_rel, flen - span_off);
   for (int attempt = 0; attempt < 6; attempt++) {
     if (!c->capK) c->capK = (flen - span_off) / 1024 + 4096;
     const uint64_t capK = c->capK;
@@ -1217,26 +1226,41 @@ static int stage_bounce(Ctx* c, const uint8_t* src, uint64_t len, uint8_t* dst) 
   return 0;
 }
 
-// stage host bytes [src, src + len) into the context's device file buffer
-static int stage_host(Ctx* c, const uint8_t* src, uint64_t len, uint32_t flags, const uint8_t** d_out) {
+// pinned or registered host memory? (a pointer the runtime does not know is
+// not an error here)
+static bool host_is_pinned(const void* p) {
+  hipPointerAttribute_t at{};
+  const bool r = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
+  (void)hipGetLastError();
+  return r;
+}
+
+// stage host bytes [src, src + len) into the context's device file buffer;
+// pinned = the caller knows the range is pinned / registered
+static int stage_host(Ctx* c, const uint8_t* src, uint64_t len, uint32_t flags, const uint8_t** d_out,
+                      bool pinned = false) {
   uint8_t* d = nullptr;
   TRY(ensure_file_buf(c, len, &d));
   *d_out = d;
   if (!len) return 0;
+  if (pinned) {
+    HIPCHK(hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->stage_mode = 1;
+    return 0;
+  }
   if (flags & SRD_FLAG_STAGE_PAGEABLE) {
     HIPCHK(hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->stage_mode = 3;
     return 0;
   }
-  hipPointerAttribute_t at{};
-  if (hipPointerGetAttributes(&at, src) == hipSuccess && at.type == hipMemoryTypeHost) {
+  if (host_is_pinned(src)) {
     HIPCHK(hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream));  // already pinned
     HIPCHK(hipStreamSynchronize(c->stream));
     c->stage_mode = 0;
     return 0;
   }
-  (void)hipGetLastError();  // an unregistered pointer is not an error here
   if (!(flags & SRD_FLAG_STAGE_BOUNCE)) {
     const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095, e = ((uintptr_t)src + len + 4095) & ~(uintptr_t)4095;
     if (hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly) == hipSuccess) {
@@ -1332,6 +1356,23 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
   };
   std::vector<Shard> sh(nc);
   const uint32_t vflags = flags & ~kStageFlags;
+  // the mapping is registered once for all shards (their spans overlap by
+  // up to 16 KiB); registration refused -> every shard uses bounce buffers
+  uintptr_t reg_a = 0, reg_e = 0;
+  bool pinned = false;
+  if (flen && !(flags & kStageFlags)) {
+    if (host_is_pinned(file)) {
+      pinned = true;
+    } else {
+      HIPCHK(hipSetDevice(ctxs[0]->device));
+      reg_a = (uintptr_t)file & ~(uintptr_t)4095;
+      reg_e = ((uintptr_t)file + flen + 4095) & ~(uintptr_t)4095;
+      pinned = hipHostRegister((void*)reg_a, reg_e - reg_a, hipHostRegisterReadOnly | hipHostRegisterPortable) ==
+               hipSuccess;
+      (void)hipGetLastError();
+      if (!pinned) reg_a = reg_e = 0;
+    }
+  }
   auto run = [&](uint32_t i) {
     srd_ctx* c = ctxs[i];
     Shard& s = sh[i];
@@ -1340,7 +1381,7 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
     if (hipSetDevice(c->device) != hipSuccess) { s.rc = SRD_ERR_HIP; s.err = "hipSetDevice"; return; }
     const uint64_t span_off = lo - lo % SPAN_BYTES;
     const uint8_t* d = nullptr;
-    s.rc = stage_host(c, file + span_off, hi - span_off, flags, &d);
+    s.rc = stage_host(c, file + span_off, hi - span_off, flags, &d, pinned);
     if (!s.rc) s.rc = srd_validate_span_device(c, d, span_off, lo, hi, vflags, &s.r);
     if (s.rc) { s.err = g_err; return; }
     s.proven = s.r.final_len == hi && s.r.mode != SRD_MODE_SPAN_UNPROVEN;
@@ -1350,6 +1391,10 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
     for (uint32_t i = 1; i < nc; i++) th.emplace_back(run, i);
     run(0);
     for (auto& t : th) t.join();
+  }
+  if (reg_a) {
+    (void)hipSetDevice(ctxs[0]->device);
+    (void)hipHostUnregister((void*)reg_a);
   }
   bool composed = true;
   for (auto& x : sh) composed = composed && !x.rc && x.proven;

@@ -121,7 +121,7 @@ def _storage_benchmark_store(n=1_000_000):
 @pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
 def test_storage_benchmark_shape_1m(ctx, flags):
     store = _storage_benchmark_store()
-    assert store.size == 64 * 1_000_000 - 44
+    assert store.size == 64 * 1_000_000 - 36  # entry i: payload at 64 i, 8 + 20 bytes
     r = S.validate_index(store, flags, ctx)
     ch = O.chain_arrays(store, store.size)
     assert (r.final_len, r.n_chain, r.n_crc_bad) == (store.size, 1_000_000, 0)
