@@ -130,48 +130,74 @@ def e2e(store, size, bytes_alg, ctx, reps=3):
     """End to end from host memory (the path starts in the mmap'd file,
     data_store.rs:172-174): host bytes -> HBM -> validate+index -> host
     result arrays (srd_validate_index).  Variants: a pinned host buffer; the
-    store as a FILE, opened with DataStore.open (mmap, page cache warm) under
-    each staging mode; the same file after posix_fadvise(DONTNEED) (cold
-    page cache, when the kernel honours it)."""
+    store as a FILE in the page cache, mapped afresh each time (mmap ->
+    srd_validate_index -> munmap, page faults included) under each staging
+    mode, and with MAP_POPULATE; the same after posix_fadvise(DONTNEED) (a
+    cold page cache when the kernel honours it); and the whole Python
+    DataStore.open mirror (its dict-building is host Python, not the path).
+    `stage_ms` = the library's staging share of each call."""
+    import mmap as M
     import tempfile
     res = {"store_bytes": size}
 
-    def timed(fn):
-        fn()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            r = fn()
-        return (time.perf_counter() - t0) / reps, r
+    def row(dt, r=None):
+        mode, st = ctx.stage_info()
+        out = {"ms": round(dt * 1e3, 2), "GiBps": round(bytes_alg / dt / 2**30, 3), "staging": mode,
+               "stage_ms": round(st, 2)}
+        if r is not None:
+            assert r.final_len == size and r.n_crc_bad == 0
+        return out
 
     host = torch.empty(size, dtype=torch.uint8).pin_memory()
     host.copy_(store[:size])
     torch.cuda.synchronize()
-    dt, r = timed(lambda: S.validate_index(host.numpy(), 0, ctx))
-    assert r.final_len == size
-    res["pinned_buffer"] = {"ms": round(dt * 1e3, 2), "GiBps": round(bytes_alg / dt / 2**30, 3)}
+    S.validate_index(host.numpy(), 0, ctx)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = S.validate_index(host.numpy(), 0, ctx)
+    res["pinned_buffer"] = row((time.perf_counter() - t0) / reps, r)
     del host
     d = tempfile.mkdtemp(prefix="srd_e2e_")
     path = os.path.join(d, "c2.store")
+
+    def mapped(flags, populate=False):
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            mm = M.mmap(fd, 0, flags=M.MAP_SHARED | (M.MAP_POPULATE if populate else 0), prot=M.PROT_READ)
+            v = np.frombuffer(mm, np.uint8)
+            r = S.validate_index(v, flags, ctx)
+            del v
+            mm.close()
+            return r
+        finally:
+            os.close(fd)
+
     try:
         with open(path, "wb") as f:
             store[:size].cpu().numpy().tofile(f)
             f.flush()
             os.fsync(f.fileno())
-        for name, flags in (("mmap_default", 0), ("mmap_bounce", S.SRD_FLAG_STAGE_BOUNCE),
-                            ("mmap_pageable", S.SRD_FLAG_STAGE_PAGEABLE)):
-            dt, ds = timed(lambda: S.DataStore.open(path, ctx, flags=flags))
-            assert ds.tail_offset == size
-            res[name] = {"ms": round(dt * 1e3, 2), "GiBps": round(bytes_alg / dt / 2**30, 3),
-                         "staging": ctx.stage_mode()}
-            del ds
+        for name, flags, pop in (("mmap_default", 0, False), ("mmap_register", S.SRD_FLAG_STAGE_REGISTER, False),
+                                 ("mmap_pageable", S.SRD_FLAG_STAGE_PAGEABLE, False),
+                                 ("mmap_populate_register", S.SRD_FLAG_STAGE_REGISTER, True)):
+            best = None
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                r = mapped(flags, pop)
+                dt = time.perf_counter() - t0
+                if best is None or dt < best[0]:
+                    best = (dt, row(dt, r))
+            res[name] = best[1]
         fd = os.open(path, os.O_RDONLY)
         os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
         os.close(fd)
         t0 = time.perf_counter()
+        r = mapped(0)
+        res["mmap_after_fadvise_dontneed"] = row(time.perf_counter() - t0, r)
+        t0 = time.perf_counter()
         ds = S.DataStore.open(path, ctx)
-        dt = time.perf_counter() - t0
-        res["mmap_after_fadvise_dontneed"] = {"ms": round(dt * 1e3, 2), "GiBps": round(bytes_alg / dt / 2**30, 3),
-                                              "staging": ctx.stage_mode()}
+        res["datastore_open_python_mirror"] = row(time.perf_counter() - t0)
+        assert ds.tail_offset == size
         del ds
     finally:
         try:

@@ -62,11 +62,13 @@ extern "C" {
 #define SRD_FLAG_FORCE_FULL 1u   /* skip the optimistic (strong-candidate) pass */
 #define SRD_FLAG_NO_CRC 2u       /* structural recovery + index only */
 /* host-input staging (srd_validate_index / _multi).  Default: pinned input is
- * copied directly; otherwise the mapped range is hipHostRegister'ed
- * (read-only) for one DMA copy, and when registration is refused host threads
- * fill double-buffered pinned bounce buffers while the previous chunks DMA. */
+ * copied directly; any other memory (the mmap) goes through double-buffered
+ * pinned bounce buffers that host threads fill (taking the mapping's page
+ * faults on several cores) while the previous chunks DMA -- measured at the
+ * pinned-buffer rate on MI355X (end to end). */
 #define SRD_FLAG_STAGE_PAGEABLE 4u /* one pageable hipMemcpy (measurement baseline) */
-#define SRD_FLAG_STAGE_BOUNCE 8u   /* bounce buffers without trying registration */
+#define SRD_FLAG_STAGE_REGISTER 8u /* hipHostRegister the range (read-only) for one DMA copy;
+                                      bounce buffers when registration is refused */
 
 typedef struct srd_ctx srd_ctx; /* one device + stream + reusable workspace */
 
@@ -184,9 +186,11 @@ void srd_result_free(srd_result *res);
 int srd_validate_index_multi(srd_ctx *const *ctxs, uint32_t n_ctx,
                              const uint8_t *file, uint64_t file_len,
                              uint32_t flags, srd_result *out);
-/* Staging mode of the last host-input call on ctx: 0 pinned input, 1
- * registered mapping, 2 bounce buffers, 3 pageable copy (-1 none yet). */
-int srd_ctx_stage_mode(srd_ctx *ctx);
+/* Staging of the last host-input call on ctx: *mode = 0 pinned input, 1
+ * registered mapping, 2 bounce buffers, 3 pageable copy (-1 none yet);
+ * *stage_ms = host wall time from the call's start until the store was in
+ * HBM (registration / page faults / copies included).  Nullable outputs. */
+int srd_ctx_stage_info(srd_ctx *ctx, int *mode, double *stage_ms);
 
 /* The index bucket hash on the device: out[i] = xxh3_64(le8(keys[i])), the
  * Xxh3BuildHasher's Hasher::write (digest/xxh3_build_hasher.rs:11-13) the

@@ -8,6 +8,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -91,6 +92,7 @@ struct Ctx {
   // host-input staging (stage_host): bounce buffers, one stream per worker
   int stage_workers = 8;
   int stage_mode = -1;  // last call: 0 pinned input, 1 registered, 2 bounce buffers, 3 pageable
+  double stage_ms = 0;  // host wall time of the last staging
   std::vector<void*> stage_pin;
   std::vector<hipStream_t> stage_streams;
   std::vector<hipEvent_t> stage_ev;
@@ -1161,15 +1163,16 @@ extern "C" int srd_shard_cuts(const uint8_t* file, uint64_t flen, uint32_t world
 // The path starts in host memory: the mmap'd single-file store
 // (data_store.rs:172-174 init_mmap, called from open :84-117).  Staging modes:
 //  - already pinned host memory: one DMA copy;
-//  - default: hipHostRegister (read-only) of the mapped range, one DMA copy
-//    straight from the page cache, unregister;
-//  - registration refused (or SRD_FLAG_STAGE_BOUNCE): host threads copy
-//    16 MiB chunks into double-buffered pinned bounce buffers, each worker
-//    DMA-ing its previous chunk on its own stream meanwhile (the memcpy also
-//    takes the mapping's page faults on several cores);
+//  - default: host threads copy 16 MiB chunks into double-buffered pinned
+//    bounce buffers, each worker DMA-ing its previous chunk on its own stream
+//    meanwhile (the memcpy also takes the mapping's page faults on several
+//    cores): the pinned-buffer rate from a page-cache-warm mmap (C2: 87 ms,
+//    vs 114 ms registered and 133 ms pageable);
+//  - SRD_FLAG_STAGE_REGISTER: hipHostRegister (read-only) of the mapped
+//    range, one DMA copy, unregister (bounce buffers if refused);
 //  - SRD_FLAG_STAGE_PAGEABLE: one pageable hipMemcpy (the runtime's own
 //    staging; measurement baseline).
-constexpr uint32_t kStageFlags = SRD_FLAG_STAGE_PAGEABLE | SRD_FLAG_STAGE_BOUNCE;
+constexpr uint32_t kStageFlags = SRD_FLAG_STAGE_PAGEABLE | SRD_FLAG_STAGE_REGISTER;
 constexpr uint64_t kBounceBytes = 16ull << 20;
 
 static int ensure_file_buf(Ctx* c, uint64_t flen, uint8_t** d) {
@@ -1185,17 +1188,18 @@ static int ensure_file_buf(Ctx* c, uint64_t flen, uint8_t** d) {
   return 0;
 }
 
-static int stage_bounce(Ctx* c, const uint8_t* src, uint64_t len, uint8_t* dst) {
-  const int T = c->stage_workers;
+static int stage_bounce(Ctx* c, const uint8_t* src, uint64_t len, uint8_t* dst, int workers) {
+  const int T = std::max(1, std::min(workers, c->stage_workers));
   if (c->stage_pin.empty()) {
-    c->stage_pin.assign(2 * T, nullptr);
-    c->stage_streams.assign(T, nullptr);
-    c->stage_ev.assign(2 * T, nullptr);
-    for (int i = 0; i < 2 * T; i++) {
+    const int W = c->stage_workers;
+    c->stage_pin.assign(2 * W, nullptr);
+    c->stage_streams.assign(W, nullptr);
+    c->stage_ev.assign(2 * W, nullptr);
+    for (int i = 0; i < 2 * W; i++) {
       HIPCHK(hipHostMalloc(&c->stage_pin[i], kBounceBytes, hipHostMallocDefault));
       HIPCHK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
     }
-    for (int w = 0; w < T; w++) HIPCHK(hipStreamCreateWithFlags(&c->stage_streams[w], hipStreamNonBlocking));
+    for (int w = 0; w < W; w++) HIPCHK(hipStreamCreateWithFlags(&c->stage_streams[w], hipStreamNonBlocking));
   }
   const uint64_t nch = (len + kBounceBytes - 1) / kBounceBytes;
   std::vector<int> rc(T, 0);
@@ -1237,8 +1241,18 @@ static bool host_is_pinned(const void* p) {
 
 // stage host bytes [src, src + len) into the context's device file buffer;
 // pinned = the caller knows the range is pinned / registered
+static int stage_host_impl(Ctx* c, const uint8_t* src, uint64_t len, uint32_t flags, const uint8_t** d_out,
+                           bool pinned, int workers);
+// workers: bounce-buffer threads (the multi-GPU open splits them over its shards)
 static int stage_host(Ctx* c, const uint8_t* src, uint64_t len, uint32_t flags, const uint8_t** d_out,
-                      bool pinned = false) {
+                      bool pinned = false, int workers = 1 << 20) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int r = stage_host_impl(c, src, len, flags, d_out, pinned, workers);
+  c->stage_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return r;
+}
+static int stage_host_impl(Ctx* c, const uint8_t* src, uint64_t len, uint32_t flags, const uint8_t** d_out,
+                           bool pinned, int workers) {
   uint8_t* d = nullptr;
   TRY(ensure_file_buf(c, len, &d));
   *d_out = d;
@@ -1261,7 +1275,7 @@ static int stage_host(Ctx* c, const uint8_t* src, uint64_t len, uint32_t flags, 
     c->stage_mode = 0;
     return 0;
   }
-  if (!(flags & SRD_FLAG_STAGE_BOUNCE)) {
+  if (flags & SRD_FLAG_STAGE_REGISTER) {
     const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095, e = ((uintptr_t)src + len + 4095) & ~(uintptr_t)4095;
     if (hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly) == hipSuccess) {
       const hipError_t e1 = hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream);
@@ -1274,7 +1288,7 @@ static int stage_host(Ctx* c, const uint8_t* src, uint64_t len, uint32_t flags, 
     }
     (void)hipGetLastError();
   }
-  return stage_bounce(c, src, len, d);
+  return stage_bounce(c, src, len, d, workers);
 }
 
 template <class T>
@@ -1317,7 +1331,12 @@ extern "C" void srd_result_free(srd_result* r) {
   memset(r, 0, sizeof *r);
 }
 
-extern "C" int srd_ctx_stage_mode(srd_ctx* c) { return c ? c->stage_mode : -1; }
+extern "C" int srd_ctx_stage_info(srd_ctx* c, int* mode, double* stage_ms) {
+  if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (mode) *mode = c->stage_mode;
+  if (stage_ms) *stage_ms = c->stage_ms;
+  return 0;
+}
 
 // ---------------------------------------------------------------------------
 // DataStore::open on n GPUs in one process, no RCCL:
@@ -1356,14 +1375,16 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
   };
   std::vector<Shard> sh(nc);
   const uint32_t vflags = flags & ~kStageFlags;
+  // pinned input: each shard copies its span directly.  SRD_FLAG_STAGE_REGISTER:
   // the mapping is registered once for all shards (their spans overlap by
-  // up to 16 KiB); registration refused -> every shard uses bounce buffers
+  // up to 16 KiB).  Otherwise each shard's bounce workers (the host threads
+  // split over the shards) stage its span.
   uintptr_t reg_a = 0, reg_e = 0;
   bool pinned = false;
-  if (flen && !(flags & kStageFlags)) {
+  if (flen && !(flags & SRD_FLAG_STAGE_PAGEABLE)) {
     if (host_is_pinned(file)) {
       pinned = true;
-    } else {
+    } else if (flags & SRD_FLAG_STAGE_REGISTER) {
       HIPCHK(hipSetDevice(ctxs[0]->device));
       reg_a = (uintptr_t)file & ~(uintptr_t)4095;
       reg_e = ((uintptr_t)file + flen + 4095) & ~(uintptr_t)4095;
@@ -1381,7 +1402,8 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
     if (hipSetDevice(c->device) != hipSuccess) { s.rc = SRD_ERR_HIP; s.err = "hipSetDevice"; return; }
     const uint64_t span_off = lo - lo % SPAN_BYTES;
     const uint8_t* d = nullptr;
-    s.rc = stage_host(c, file + span_off, hi - span_off, flags, &d, pinned);
+    s.rc = stage_host(c, file + span_off, hi - span_off, flags, &d, pinned,
+                      std::max(1, ctxs[0]->stage_workers / (int)nc));
     if (!s.rc) s.rc = srd_validate_span_device(c, d, span_off, lo, hi, vflags, &s.r);
     if (s.rc) { s.err = g_err; return; }
     s.proven = s.r.final_len == hi && s.r.mode != SRD_MODE_SPAN_UNPROVEN;

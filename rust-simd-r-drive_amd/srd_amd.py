@@ -31,7 +31,7 @@ LIB_PATH = os.environ.get("SRD_LIB_PATH") or os.path.join(HERE, "build", "libsrd
 SRD_FLAG_FORCE_FULL = 1
 SRD_FLAG_NO_CRC = 2
 SRD_FLAG_STAGE_PAGEABLE = 4  # host input: one pageable hipMemcpy (measurement baseline)
-SRD_FLAG_STAGE_BOUNCE = 8    # host input: pinned bounce buffers, no hipHostRegister
+SRD_FLAG_STAGE_REGISTER = 8  # host input: hipHostRegister the range (default: pinned bounce buffers)
 STAGE_MODES = {0: "pinned input", 1: "registered mapping", 2: "bounce buffers", 3: "pageable copy"}
 SRD_MODE_OPTIMISTIC = 0
 SRD_MODE_FULL = 1
@@ -54,7 +54,7 @@ EXPORTS = [
     "srd_index_table_bytes", "srd_index_table_build_device", "srd_index_get_packed_device",
     "srd_batch_read_hashed_device", "srd_batch_read",
     "srd_iter_entries_device", "srd_estimate_compaction_savings_device", "srd_compact_device",
-    "srd_shard_cuts", "srd_validate_index_multi", "srd_ctx_stage_mode", "srd_index_hash_device",
+    "srd_shard_cuts", "srd_validate_index_multi", "srd_ctx_stage_info", "srd_index_hash_device",
 ]
 
 
@@ -130,7 +130,7 @@ def lib():
         L.srd_estimate_compaction_savings_device.argtypes = [vp, vp, u64, vp, u64, C.POINTER(u64)]
         L.srd_compact_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, C.POINTER(u64), vp, vp]
         L.srd_validate_index_multi.argtypes = [C.POINTER(vp), u32, vp, u64, u32, C.POINTER(DeviceResult)]
-        L.srd_ctx_stage_mode.argtypes = [vp]
+        L.srd_ctx_stage_info.argtypes = [vp, C.POINTER(i32), C.POINTER(C.c_double)]
         L.srd_index_hash_device.argtypes = [vp, vp, u64, vp, vp]
         for f in EXPORTS:
             if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
@@ -187,9 +187,14 @@ class Context:
     def stream(self) -> int:
         return lib().srd_ctx_stream(self.h)
 
+    def stage_info(self) -> tuple[str, float]:
+        """(how the last host-input call staged the store (STAGE_MODES), its host wall ms)."""
+        m, ms = C.c_int(), C.c_double()
+        _check(lib().srd_ctx_stage_info(self.h, C.byref(m), C.byref(ms)))
+        return STAGE_MODES.get(m.value, "none"), ms.value
+
     def stage_mode(self) -> str:
-        """How the last host-input call staged the store (STAGE_MODES)."""
-        return STAGE_MODES.get(lib().srd_ctx_stage_mode(self.h), "none")
+        return self.stage_info()[0]
 
 
 _default_ctx = None
@@ -410,10 +415,26 @@ def compute_checksum(data: bytes) -> bytes:
 
 
 class KeyIndexer:
-    """key_indexer.rs: key_hash -> (tag16 << 48 | offset48)."""
+    """key_indexer.rs: key_hash -> (tag16 << 48 | offset48).  Array-backed
+    (the validate pass's index arrays, sorted by key_hash for lookups), so
+    that adopting a million-key index costs a sort, not a Python dict."""
 
-    def __init__(self, index: dict[int, int]):
-        self.index = index
+    def __init__(self, index: dict[int, int] | None = None, keys=None, packed=None):
+        if index is not None:
+            keys = np.fromiter(index.keys(), np.uint64, len(index))
+            packed = np.fromiter(index.values(), np.uint64, len(index))
+        keys = np.zeros(0, np.uint64) if keys is None else np.asarray(keys, np.uint64)
+        packed = np.zeros(0, np.uint64) if packed is None else np.asarray(packed, np.uint64)
+        o = np.argsort(keys, kind="stable")
+        self._keys, self._packed = keys[o], packed[o]
+
+    @classmethod
+    def from_arrays(cls, keys: np.ndarray, packed: np.ndarray) -> "KeyIndexer":
+        return cls(keys=keys, packed=packed)
+
+    @property
+    def index(self) -> dict[int, int]:
+        return {int(k): int(v) for k, v in zip(self._keys, self._packed)}
 
     @staticmethod
     def tag_from_hash(key_hash: int) -> int:
@@ -436,17 +457,20 @@ class KeyIndexer:
         v = np.zeros(cap, np.uint64)
         n = C.c_uint64()
         _check(lib().srd_key_indexer_build(ctx.h, _ptr(a), tail, _ptr(k), _ptr(v), cap, C.byref(n)))
-        return cls({int(k[i]): int(v[i]) for i in range(n.value)})
+        return cls(keys=k[: n.value], packed=v[: n.value])
 
     def get_packed(self, key_hash: int):
-        return self.index.get(key_hash)
+        i = int(np.searchsorted(self._keys, np.uint64(key_hash)))
+        if i < self._keys.size and int(self._keys[i]) == key_hash:
+            return int(self._packed[i])
+        return None
 
     def get_offset(self, key_hash: int):
-        p = self.index.get(key_hash)
+        p = self.get_packed(key_hash)
         return None if p is None else p & OFFSET_MASK
 
     def __len__(self):
-        return len(self.index)
+        return int(self._keys.size)
 
 
 class EntryHandle:
@@ -475,8 +499,7 @@ class DataStore:
     def __init__(self, path, mm, result: Result):
         self.path, self.mm, self.result = path, mm, result
         self.tail_offset = result.final_len
-        self.key_indexer = KeyIndexer(result.index())
-        self._pos = {int(m): i for i, m in enumerate(result.meta_off)}
+        self.key_indexer = KeyIndexer.from_arrays(result.index_key_hash, result.index_packed)
 
     @classmethod
     def open(cls, path, ctx: Context | None = None, ctxs=None, flags: int = 0) -> "DataStore":
@@ -513,7 +536,7 @@ class DataStore:
         tag, off = KeyIndexer.unpack(packed)
         if tag != KeyIndexer.tag_from_hash(key_hash):
             return None
-        i = self._pos[off]
+        i = int(np.searchsorted(self.result.meta_off, np.uint64(off)))  # the chain is in file order
         if int(self.result.payload_len[i]) == 1 and self.mm[int(self.result.payload_start[i])] == 0:
             return None  # tombstone
         return EntryHandle(self, i)

@@ -105,13 +105,14 @@ def test_multi_forged_cut_is_refuted(ctxs):
 def test_staging_modes_agree(ctxs):
     st = _mixed_store(600, seed=8)
     want = S.validate_index(st, 0, ctxs[0])
-    for flags, mode in ((S.SRD_FLAG_STAGE_PAGEABLE, "pageable copy"), (S.SRD_FLAG_STAGE_BOUNCE, "bounce buffers")):
+    assert ctxs[0].stage_mode() == "bounce buffers"  # the default for unpinned host memory
+    for flags, mode in ((S.SRD_FLAG_STAGE_PAGEABLE, "pageable copy"), (S.SRD_FLAG_STAGE_REGISTER, "registered mapping")):
         r = S.validate_index(st, flags, ctxs[0])
         assert ctxs[0].stage_mode() == mode
         assert (r.final_len, r.n_chain, r.n_index) == (want.final_len, want.n_chain, want.n_index)
         assert np.array_equal(r.crc_computed, want.crc_computed) and r.index() == want.index()
-    r = S.validate_index_multi(st, ctxs[:3], S.SRD_FLAG_STAGE_BOUNCE)
-    same_as_oracle(r, st, "bounce-multi")
+    r = S.validate_index_multi(st, ctxs[:3], S.SRD_FLAG_STAGE_REGISTER)
+    same_as_oracle(r, st, "register-multi")
 
 
 @pytest.mark.parametrize("nd", [1, 2, 3])
