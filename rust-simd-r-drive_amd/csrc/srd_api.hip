@@ -114,6 +114,7 @@ enum BufId {
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST, B_XPART,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
+  B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE,
   B_COUNT_
 };
 
@@ -356,6 +357,22 @@ static void fit_cap(Ctx* c, uint64_t n_spans, uint64_t bytes) {
   while (c->cap > 64 && (uint64_t)c->cap * 40 * n_spans > 2 * bytes + (64ull << 20)) c->cap /= 4;
 }
 
+// the scan kernel's per-wave results and last-block reduction (ScanArgs)
+static int scan_wave_args(Ctx* c, ScanArgs* a) {
+  const uint64_t W = (uint64_t)c->scan_blocks * SCAN_WAVES_V2;
+  TRY(ensure(c, B_WTOT, W * 8));
+  TRY(ensure(c, B_WROOT, W * 8));
+  TRY(ensure(c, B_WBASE, W * 8));
+  TRY(ensure(c, B_KTOT, 64));
+  TRY(ensure_z(c, B_DONE, 64));  // zero once; the scan's last block resets it
+  a->wave_total = P<uint64_t>(c, B_WTOT);
+  a->wave_root = P<uint64_t>(c, B_WROOT);
+  a->wave_base = P<uint64_t>(c, B_WBASE);
+  a->k_total = P<uint64_t>(c, B_KTOT);
+  a->done = P<uint32_t>(c, B_DONE);
+  return 0;
+}
+
 static int alloc_scan(Ctx* c, uint64_t n_tiles, uint64_t n_spans) {
   const uint64_t slots = n_spans * c->cap;
   TRY(ensure(c, B_TILE, n_tiles * 16));
@@ -553,6 +570,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.c_rec = P<u32x4>(c, B_CREC);
     a.counters = (unsigned long long*)cnt;
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
+    TRY(scan_wave_args(c, &a));
     if (n_spans) {
       unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
@@ -638,9 +656,11 @@ static uint32_t index_log2_buckets(uint64_t n_est) {
   while (log2_nbk < 14 && ((uint64_t)IDX_BUCKET_AVG << log2_nbk) < n_est) log2_nbk++;
   return log2_nbk;
 }
+// cpart: the histogram is already in B_HIST, built by chain_finalize_kernel
+// over its chain partition (cpart = check_kernel's per-chunk core counts)
 static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
                                  const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
-                                 Plan* pl) {
+                                 Plan* pl, const uint32_t* cpart = nullptr, uint32_t coff = 0) {
   IdxArgs ia{};
   ia.kh = kh;
   ia.mo = mo;
@@ -656,10 +676,14 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   ia.okey = okey;
   ia.opacked = opacked;
   ia.plan = pl;
+  ia.cpart = cpart;
+  ia.coff = coff;
   const uint32_t nbk = 1u << log2_nbk;
   const int nh = (int)((uint64_t)nbk * IDX_HBLOCKS + 1);
-  idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
-  KCHK(c, "idx_hist_kernel");
+  if (!cpart) {
+    idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+    KCHK(c, "idx_hist_kernel");
+  }
   TRY(xscan(c, ia.histT, ia.hoff, (uint64_t)nh));
   idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
   KCHK(c, "idx_scatter_kernel");
@@ -729,9 +753,8 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     ++c->gen;
     Plan* pl = P<Plan>(c, B_PLAN);
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
-    HIPCHK(hipMemsetAsync(cnt, 0, 64, c->stream));
-    // the scan writes every span's count; only the scan sentinel needs a zero
-    // the scan-count sentinel and the plan are zeroed by the scan kernel
+    // the scan writes every span's count and (its last block) the counters,
+    // the wave bases and K; block 0 zeroes the plan
     // per-tile / per-span arrays hold the resident range only: their base
     // pointers are shifted so kernels index them by absolute tile / span
     ScanArgs a{};
@@ -750,14 +773,15 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.m_lo = lo;
     a.zero_words = (uint32_t*)pl;
     a.n_zero_words = (uint32_t)(sizeof(Plan) / 4);
-    a.sentinel = P<uint32_t>(c, B_SPAN_COUNT) + ns_rel;
+    a.sentinel = nullptr;
+    TRY(scan_wave_args(c, &a));
     const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
+    const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     launch_scan<false>(g, a, c->stream);
     KCHK(c, "scan_kernel");
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    TRY(xscan(c, P<uint32_t>(c, B_SPAN_COUNT), P<uint64_t>(c, B_SPAN_BASE), ns_rel + 1));
     Link2Args l{};
     l.file = d_file;
     l.flen = flen;
@@ -766,7 +790,8 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.cap = c->cap;
     l.gen = c->gen;
     l.span_count = a.span_count;
-    l.span_base = P<uint64_t>(c, B_SPAN_BASE) - s_lo;
+    l.wave_base = a.wave_base;
+    l.spw = (ns_rel + total_waves - 1) / total_waves;
     l.c_m = a.c_m;
     l.c_rec = a.c_rec;
     l.d_m = P<uint64_t>(c, B_DM);
@@ -775,7 +800,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.has_child = P<uint32_t>(c, B_HASCHILD);
     l.s_lo = s_lo;
     l.span_lo = lo;
-    link2_kernel<<<blocks(ns_rel, 64), 256, 0, c->stream>>>(l);
+    link2_kernel<<<(unsigned)total_waves, 256, 0, c->stream>>>(l);
     KCHK(c, "link2_kernel");
     // ---- shape check, chain, finalize, index; retried on device with more
     //      prune rounds when false candidates chained onto each other ----
@@ -790,7 +815,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       sa.file = d_file;
       sa.flen = flen;
       sa.capK = capK;
-      sa.Kp = P<uint64_t>(c, B_SPAN_BASE) + ns_rel;
+      sa.Kp = a.k_total;
       sa.coff = coff;
       sa.d_m = l.d_m;
       sa.d_par = l.d_par;
@@ -816,27 +841,17 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       sa.gen = mgen;
       child2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
       KCHK(c, "child2_kernel");
-      check_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
+      check_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, 0, c->stream>>>(sa);
       KCHK(c, "check_kernel");
-      scatter_plan_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
-      KCHK(c, "scatter_plan_kernel");
       HIPCHK(hipGetLastError());
-      // ---- finalize (per chain entry outputs + CRC) ----
+      // ---- plan + chain ranks + per-entry outputs / CRC + index histogram ----
       FinArgs f{};
       f.file = d_file;
       f.flen = flen;
-      f.n_chain = 0;
-      f.chain_g = sa.chain_g;
-      f.slot = l.d_slot;
-      f.par = l.d_par;
-      f.ws = nullptr;
       f.c_m = l.c_m;
       f.c_rec = l.c_rec;
       f.tile = a.tile;
       f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
-      f.d_n_chain = &pl->n_chain;
-      f.d_root_t = &pl->root_t;
-      f.d_status = &pl->status;
       f.coff = coff;
       f.o_mo = P<uint64_t>(c, B_O_MO);
       f.o_kh = P<uint64_t>(c, B_O_KH);
@@ -850,18 +865,15 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.o_sxm = P<uint32_t>(c, B_O_SXM);
       f.o_tail = P<uint32_t>(c, B_O_TAIL);
       f.o_ok = P<uint8_t>(c, B_O_OK);
-      f.slow_list = P<uint64_t>(c, B_SLOW);
-      f.n_slow = (unsigned long long*)&pl->n_slow;
       f.n_bad = (unsigned long long*)&pl->n_bad;
-      finalize_kernel<<<2048, 256, 0, c->stream>>>(f);
-      KCHK(c, "finalize_kernel");
-      if (!f.no_crc) slow_kernel<<<2048 / SLOW_WAVES, SLOW_WAVES * 64, 0, c->stream>>>(f);
-      KCHK(c, "slow_kernel");
+      chain_finalize_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, (1u << log2_nbk) * 4, c->stream>>>(
+          sa, f, P<uint32_t>(c, B_HIST), log2_nbk);
+      KCHK(c, "chain_finalize_kernel");
       HIPCHK(hipGetLastError());
       // ---- KeyIndexer::build (bucketed; SRD_INDEX_GLOBAL=1: one global table, timing experiments) ----
       if (!index_global_env())
         TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
-                                  P<uint64_t>(c, B_IPACKED), pl));
+                                  P<uint64_t>(c, B_IPACKED), pl, sa.part, coff));
       HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       hp = *c->h_plan;

@@ -76,6 +76,44 @@ __device__ __forceinline__ uint32_t block_rank256(bool f, uint32_t* wsum, uint32
   return off + pre;
 }
 
+// the same for NW-wave blocks (wsum: LDS[NW])
+template <int NW>
+__device__ __forceinline__ uint32_t block_rank_n(bool f, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t bal = __ballot(f);
+  const uint32_t pre = (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+  if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; i++) {
+    const uint32_t v = wsum[i];
+    off += i < w ? v : 0u;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + pre;
+}
+template <int NW>
+__device__ __forceinline__ uint32_t block_sum_n(uint32_t v, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+  if (lane == 0) wsum[w] = v;
+  __syncthreads();
+  uint32_t t = 0;
+#pragma unroll
+  for (int i = 0; i < NW; i++) t += wsum[i];
+  __syncthreads();
+  return t;
+}
+// chunked grid of the shape check and the fused chain finalize (the index
+// histogram / scatter partition too: IDX_HBLOCKS == CHAIN_BLOCKS)
+constexpr int CHAIN_BLOCKS = 256;
+constexpr int CHAIN_THREADS = 1024;
+constexpr int CHAIN_WAVES = CHAIN_THREADS / 64;
+
 __device__ __forceinline__ uint32_t block_sum256(uint32_t v, uint32_t* wsum) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -197,7 +235,8 @@ struct Link2Args {
   uint64_t flen, n_spans, capK;
   uint32_t cap, gen;
   const uint32_t* span_count;
-  const uint64_t* span_base;
+  const uint64_t* wave_base;  // scan_kernel's last block: dense base of each scan wave's records
+  uint64_t spw;               // spans per scan wave (the scan's partition)
   const uint64_t* c_m;
   u32x4* c_rec;  // tombstone flags are set in place
   uint64_t* d_m;
@@ -208,62 +247,115 @@ struct Link2Args {
   uint64_t span_lo;  // span mode: the shard's lower tail (a node with p == span_lo is the shard's first entry); 0 = whole file
 };
 
+// dense base of span sp: its scan wave's base + the counts of the wave's
+// earlier spans (the rare binary-search path into another wave's span)
+__device__ __forceinline__ uint64_t span_base_of(const Link2Args& a, uint64_t sp) {
+  const uint64_t w = (sp - a.s_lo) / a.spw, s0 = a.s_lo + w * a.spw;
+  uint64_t b = a.wave_base[w];
+  for (uint64_t s = s0; s < sp; s++) b += a.span_count[s];
+  return b;
+}
+
+// One block per scan wave, 4 lanes per span: every load a lane needs for its
+// first record (the record, the previous record's m, the span counts, the
+// wave base) is issued at once -- the span bases (a 64-span block scan in
+// LDS) are needed only for the dense indices written at the end.
+__device__ __forceinline__ void link_one(const Link2Args& a, uint64_t sp, uint32_t i, uint64_t gb, uint64_t m,
+                                         u32x4 r0, u32x4 r1, uint64_t m_prev, bool have_prev, const uint64_t* base,
+                                         uint64_t g0, uint64_t gend) {
+  const uint64_t gi = sp * a.cap + i, g = gb + i;
+  if (g >= a.capK) return;  // scatter_plan reports ST_CAPK
+  const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+  bool node = true;
+  if (r1[3] & F_NT) {
+    // single-candidate record, deferred node test (data_store.rs:404-470);
+    // F_ZB is the byte at m - 1, the tombstone byte when p == m - 1
+    const uint64_t dp = m - p;
+    const bool tomb = dp == 1 && (r1[3] & F_ZB);
+    node = p >= 20 && p < m && (tomb || dp > prepad64(p));
+    if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
+  }
+  const uint64_t mp = p - 20;  // p >= 20 for nodes
+  const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
+  // In a store without garbage the parent is the previous record in file
+  // order (the same span's slot i-1, else the previous span's last slot):
+  // one load instead of a binary search.
+  int64_t par = have_prev && m_prev == mp ? (int64_t)(g - 1) : PAR_MISS;
+  if (par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
+    const uint32_t n2 = min(a.span_count[sp2], a.cap);
+    uint32_t lo = 0, hi = n2;
+    const uint64_t* cm = a.c_m + sp2 * a.cap;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (cm[mid] < mp) lo = mid + 1; else hi = mid;
+    }
+    if (lo < n2 && cm[lo] == mp)
+      par = (int64_t)((sp2 >= g0 && sp2 < gend ? base[sp2 - g0] : span_base_of(a, sp2)) + lo);
+  }
+  if (!node) par = PAR_MISS;  // no parent, no root
+  else if (par == PAR_MISS) {
+    if (a.span_lo) {
+      if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
+    } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {
+      par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
+    }
+  }
+  a.d_m[g] = m;
+  a.d_par[g] = par;
+  a.d_slot[g] = gi;
+  if (par >= 0 && (uint64_t)par < a.capK) a.has_child[par] = a.gen;
+}
+
 __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
-  const uint64_t sp = a.s_lo + (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
-  if (sp >= a.n_spans) return;
-  const uint32_t n = min(a.span_count[sp], a.cap);
-  const uint64_t gb = a.span_base[sp];
-  for (uint32_t i = threadIdx.x & 3; i < n; i += 4) {
-    const uint64_t gi = sp * a.cap + i, g = gb + i;
-    if (g >= a.capK) return;  // plan_kernel reports ST_CAPK
-    const uint64_t m = a.c_m[gi];
-    const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
-    const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-    bool node = true;
-    if (r1[3] & F_NT) {
-      // single-candidate record, deferred node test (data_store.rs:404-470);
-      // F_ZB is the byte at m - 1, the tombstone byte when p == m - 1
-      const uint64_t dp = m - p;
-      const bool tomb = dp == 1 && (r1[3] & F_ZB);
-      node = p >= 20 && p < m && (tomb || dp > prepad64(p));
-      if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
-    }
-    const uint64_t mp = p - 20;  // p >= 20 for nodes
-    const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
-    int64_t par = PAR_MISS;
-    // In a store without garbage the parent is the previous record in file
-    // order (the same span's slot i-1, else the previous span's last slot):
-    // one load instead of a binary search.  Otherwise the search below.
-    if (i > 0) {
-      if (a.c_m[gi - 1] == mp) par = (int64_t)(g - 1);
-    } else if (sp > a.s_lo) {
-      const uint32_t np = min(a.span_count[sp - 1], a.cap);
-      if (np && a.c_m[(sp - 1) * a.cap + np - 1] == mp) par = (int64_t)(gb - 1);
-    }
-    // the lookup does not wait for the node test (its loads overlap the
-    // lean record's file reads); a failed test discards it below
-    if (par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
-      const uint32_t n2 = min(a.span_count[sp2], a.cap);
-      uint32_t lo = 0, hi = n2;
-      const uint64_t* cm = a.c_m + sp2 * a.cap;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (cm[mid] < mp) lo = mid + 1; else hi = mid;
+  __shared__ uint64_t base[65];
+  const uint64_t sA = a.s_lo + (uint64_t)blockIdx.x * a.spw, sB = min(sA + a.spw, a.n_spans);
+  uint64_t run = a.wave_base[blockIdx.x];
+  for (uint64_t g0 = sA; g0 < sB; g0 += 64) {
+    const uint64_t sp = g0 + (threadIdx.x >> 2);
+    const uint32_t i0 = threadIdx.x & 3;
+    const bool in = sp < sB;
+    const uint64_t spc = in ? sp : sA;
+    // speculative loads of slot i0 (the slots exist; unused ones are ignored)
+    const uint32_t cnt = in ? a.span_count[sp] : 0u;
+    const uint32_t cnt_prev = (i0 == 0 && sp > a.s_lo && in) ? a.span_count[sp - 1] : 0u;
+    const uint64_t gi0 = spc * a.cap + i0;
+    const uint64_t m0 = a.c_m[gi0];
+    const u32x4 r00 = a.c_rec[2 * gi0], r01 = a.c_rec[2 * gi0 + 1];
+    const uint64_t mprev0 = i0 ? a.c_m[gi0 - 1] : 0;
+    if (threadIdx.x < 64) {  // bases of the group's spans (wave 0; counts of spans g0 + lane)
+      const uint64_t s2 = g0 + threadIdx.x;
+      const uint64_t c = s2 < sB ? a.span_count[s2] : 0;
+      uint64_t x = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if ((int)threadIdx.x >= o) x += y;
       }
-      if (lo < n2 && cm[lo] == mp) par = (int64_t)(a.span_base[sp2] + lo);
+      base[threadIdx.x] = run + x - c;
+      if (threadIdx.x == 63) base[64] = run + x;
     }
-    if (!node) par = PAR_MISS;  // no parent, no root
-    else if (par == PAR_MISS) {
-      if (a.span_lo) {
-        if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
-      } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {
-        par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
+    __syncthreads();
+    if (in) {
+      const uint32_t n = min(cnt, a.cap);
+      const uint64_t gb = base[threadIdx.x >> 2];
+      if (i0 < n) {
+        uint64_t mp0 = mprev0;
+        bool hp = i0 > 0;
+        if (i0 == 0) {
+          const uint32_t np = min(cnt_prev, a.cap);
+          hp = np > 0;
+          if (hp) mp0 = a.c_m[(sp - 1) * a.cap + np - 1];
+        }
+        link_one(a, sp, i0, gb, m0, r00, r01, mp0, hp, base, g0, min(g0 + 64, sB));
+      }
+      for (uint32_t i = i0 + 4; i < n; i += 4) {  // spans with more than 4 records
+        const uint64_t gi = sp * a.cap + i;
+        link_one(a, sp, i, gb, a.c_m[gi], a.c_rec[2 * gi], a.c_rec[2 * gi + 1], a.c_m[gi - 1], true, base, g0,
+                 min(g0 + 64, sB));
       }
     }
-    a.d_m[g] = m;
-    a.d_par[g] = par;
-    a.d_slot[g] = gi;
-    if (par >= 0 && (uint64_t)par < a.capK) a.has_child[par] = a.gen;
+    run = base[64];
+    __syncthreads();
   }
 }
 
@@ -324,8 +416,8 @@ __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void check_kernel(ShapeArgs a) {
-  __shared__ uint32_t wsum[4];
+__global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
+  __shared__ uint32_t wsum[CHAIN_WAVES];
   const uint64_t K = *a.Kp;
   if (K > a.capK) return;
   const uint64_t start = start_node(a, K);
@@ -363,30 +455,60 @@ __global__ __launch_bounds__(256) void check_kernel(ShapeArgs a) {
       atomicAdd(&a.plan->why[2], 1u);
     }
   }
-  const uint32_t tot = block_sum256(cnt, wsum);
+  const uint32_t tot = block_sum_n<CHAIN_WAVES>(cnt, wsum);
   if (__syncthreads_or(fail) && threadIdx.x == 0) atomicOr(&a.plan->status, ST_SHAPE);
   if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
 }
 
+// ---------------------------------------------------------------------------
 // The plan (every block decides it from the same inputs; block 0 publishes
-// it) fused with the chain scatter: chain_g[coff + rank] = record slot of
-// core node g, in file order.
-__global__ __launch_bounds__(256) void scatter_plan_kernel(ShapeArgs a) {
-  __shared__ uint32_t wsum[4];
+// it) fused with the whole per-entry stage: chain rank of every core node
+// (block prefix of check_kernel's per-chunk core counts + a block rank), the
+// outputs and the CRC of each chain entry (finalize_core), the entries whose
+// CRC needs a wave (long entries, missing pieces: slow_one, run by this
+// block's 16 waves after each round), and the index histogram of the
+// bucketed KeyIndexer::build over this block's chain positions.  Replaces
+// the plan/scatter, finalize, slow and histogram launches.
+template <int NW>
+__device__ __forceinline__ void block_prefix_n(const uint32_t* part, uint32_t np, uint32_t* wsum, uint64_t* before,
+                                               uint64_t* total) {
+  uint32_t b = 0, t = 0;
+  for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+    const uint32_t v = part[i];
+    t += v;
+    b += i < blockIdx.x ? v : 0u;
+  }
+  *before = block_sum_n<NW>(b, wsum);
+  *total = block_sum_n<NW>(t, wsum);
+}
+
+__device__ __forceinline__ uint32_t idx_bucket(uint64_t key, uint32_t log2_nbk) {
+  return (uint32_t)(xxh3_64_u64(key) >> (64 - log2_nbk));
+}
+
+__global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs a, FinArgs f, uint32_t* histT,
+                                                                      uint32_t log2_nbk) {
+  __shared__ uint32_t wsum[CHAIN_WAVES];
+  __shared__ uint32_t tab[1024], mx[1024];
+  __shared__ uint32_t slowq[CHAIN_THREADS];
+  __shared__ uint32_t nslow;
+  extern __shared__ uint32_t hist[];
   const uint64_t K = *a.Kp;
   const bool capk = K > a.capK;
   uint64_t before = 0, total = 0;
-  block_prefix(a.part, capk ? 0u : (uint32_t)GLUE_BLOCKS, wsum, &before, &total);
+  block_prefix_n<CHAIN_WAVES>(a.part, capk ? 0u : (uint32_t)CHAIN_BLOCKS, wsum, &before, &total);
   Plan* pl = a.plan;
   uint32_t st = pl->status;  // check_kernel's shape bits
   // whole file only: file_len is itself a root tail (prev 0); flen >= 21 here
   const bool troot = a.coff && ld_u64_unaligned(a.file, a.flen - 12) == 0;
+  const uint64_t root_t = troot ? a.flen : pl->root_t;
   if (capk) st |= ST_CAPK;
   if (a.counters[2]) st |= ST_OVERFLOW;
   const uint64_t start = capk ? NO_NODE : start_node(a, K);
   if (start == NO_NODE) st |= ST_NOSTART;
   if (pl->nroot != 1) st |= ST_ROOTS;
-  __syncthreads();  // every block has read pl->status / nroot before block 0 rewrites them
+  __syncthreads();  // this block has read pl->status / nroot / root_t before block 0 rewrites them
+  const uint32_t nbk = 1u << log2_nbk;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     pl->K = K;
     pl->max_root = a.counters[0];
@@ -405,28 +527,66 @@ __global__ __launch_bounds__(256) void scatter_plan_kernel(ShapeArgs a) {
       pl->chain_core = total;
       pl->n_chain = st ? 0 : a.coff + total;
     }
+    histT[(uint64_t)nbk * CHAIN_BLOCKS] = 0;  // the histogram scan's total slot
   }
-  if (st || troot) return;
-  uint64_t lo, hi;
-  chunk_of(K, &lo, &hi);
-  uint64_t run = a.coff + before;
-  for (uint64_t base = lo; base < hi; base += blockDim.x) {
-    const uint64_t g = base + threadIdx.x;
-    const bool f = g < hi && a.flag[g];
-    uint32_t tot;
-    const uint32_t r = block_rank256(f, wsum, &tot);
-    if (f) a.chain_g[run + r] = a.d_slot[g];  // chain entry -> candidate record slot
-    run += tot;
+  if (st && !troot) return;
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
+  for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
+    tab[i] = g_tabs.tab[i >> 8][i & 255];
+    mx[i] = (&g_tabs.mx64[0][0])[i];
   }
+  if (threadIdx.x == 0) nslow = 0;
+  __syncthreads();
+  // the root entry (whole file: chain entry 0, no candidate record)
+  if (blockIdx.x == 0 && a.coff) {
+    if (threadIdx.x == 0) {
+      uint64_t kh;
+      nslow = finalize_core(f, 0, NO_REC, -1, root_t, &kh) ? 1u : 0u;
+      atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
+    }
+    __syncthreads();
+    if (nslow && threadIdx.x < 64) slow_one(f, 0, tab, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) nslow = 0;
+    __syncthreads();
+  }
+  if (!troot) {
+    uint64_t lo, hi;
+    chunk_of(K, &lo, &hi);
+    uint64_t run = a.coff + before;
+    for (uint64_t base = lo; base < hi; base += CHAIN_THREADS) {
+      const uint64_t g = base + threadIdx.x;
+      const bool fl = g < hi && a.flag[g];
+      uint32_t tot;
+      const uint32_t r = block_rank_n<CHAIN_WAVES>(fl, wsum, &tot);
+      if (fl) {
+        const uint64_t c = run + r;
+        const int64_t p = a.d_par[g];
+        uint64_t kh;
+        if (finalize_core(f, c, a.d_slot[g], p >= 0 ? (int64_t)a.d_slot[p] : -1, root_t, &kh))
+          slowq[atomicAdd(&nslow, 1u)] = (uint32_t)(c - run);
+        atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
+      }
+      __syncthreads();
+      const uint32_t ns = nslow;
+      if (ns) {  // this round's slow entries, one wave each
+        for (uint32_t q = threadIdx.x >> 6; q < ns; q += CHAIN_WAVES) slow_one(f, run + slowq[q], tab, mx);
+        __syncthreads();
+        if (threadIdx.x == 0) nslow = 0;
+        __syncthreads();
+      }
+      run += tot;
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) histT[(uint64_t)k * CHAIN_BLOCKS + blockIdx.x] = hist[k];
 }
 
 // --------------------------------------------------------------------------
 // KeyIndexer::build, bucketed
 // --------------------------------------------------------------------------
-#ifndef SRD_IDX_HBLOCKS
-#define SRD_IDX_HBLOCKS 256
-#endif
-constexpr int IDX_HBLOCKS = SRD_IDX_HBLOCKS;  // histogram / scatter blocks
+constexpr int IDX_HBLOCKS = 256;  // histogram / scatter blocks
+static_assert(IDX_HBLOCKS == CHAIN_BLOCKS, "chain_finalize_kernel builds the index histogram per chain block");
 constexpr int IDX_TSLOTS = 4096;     // LDS open-addressing slots per bucket block (max)
 constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
 constexpr int IDX_BUCKET_AVG = 1024; // host sizes the bucket count for this average
@@ -447,6 +607,11 @@ struct IdxArgs {
   uint64_t* okey;
   uint64_t* opacked;
   Plan* plan;
+  // chain_finalize_kernel's partition (its histogram's): block b's chain
+  // positions are [coff + before_b, coff + before_b + cpart[b]) (block 0
+  // from 0: the root entry); null = chunk_of over n
+  const uint32_t* cpart;
+  uint32_t coff;
 };
 
 __device__ __forceinline__ uint64_t idx_n(const IdxArgs& a) { return *a.status ? 0 : *a.n_dev; }
@@ -471,7 +636,17 @@ __global__ __launch_bounds__(256) void idx_scatter_kernel(IdxArgs a) {
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = a.hoff[(uint64_t)k * IDX_HBLOCKS + blockIdx.x];
   __syncthreads();
   uint64_t lo, hi;
-  chunk_of(idx_n(a), &lo, &hi);
+  if (a.cpart) {
+    __shared__ uint32_t wsum[4];
+    uint64_t before, total;
+    block_prefix(a.cpart, IDX_HBLOCKS, wsum, &before, &total);
+    if (*a.status) return;
+    const uint64_t n = *a.n_dev;  // 1 when file_len itself is a root tail (the chain is that entry)
+    lo = min(n, blockIdx.x ? a.coff + before : 0);
+    hi = min(n, a.coff + before + a.cpart[blockIdx.x]);
+  } else {
+    chunk_of(idx_n(a), &lo, &hi);
+  }
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) {
     const uint64_t k = a.kh[c];
     const uint32_t pos = atomicAdd(&lds_u32[xxh3_64_u64(k) >> (64 - a.log2_nbk)], 1u);

@@ -91,6 +91,17 @@ struct ScanArgs {
   uint32_t* zero_words;
   uint32_t n_zero_words;
   uint32_t* sentinel;
+  // per-wave results, reduced by the last block to finish (no atomics on the
+  // counters, no memset, no span-base scan launch): wave w's record count
+  // (bit 63: a span overflowed its slots), its largest root tail; the last
+  // block writes wave_base[w] = exclusive prefix of the counts, *k_total,
+  // counters[0] (max root tail), [1] = 0, [2] (overflow); `done` counts the
+  // finished blocks (the last block resets it to 0)
+  uint64_t* wave_total;
+  uint64_t* wave_root;
+  uint64_t* wave_base;
+  uint64_t* k_total;
+  uint32_t* done;
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -317,11 +328,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   const uint64_t s_lo = a.k_lo / SPAN_TILES;
   const uint64_t spw = (a.n_spans - s_lo + total_waves - 1) / total_waves;
   const uint64_t s0 = s_lo + w * spw;
-  const uint64_t k0 = s0 * SPAN_TILES;
-  const uint64_t k1 = min((s0 + spw) * SPAN_TILES, a.n_tiles);
-  if (k0 >= k1) return;
+  uint64_t k0 = s0 * SPAN_TILES;
+  uint64_t k1 = min((s0 + spw) * SPAN_TILES, a.n_tiles);
+  if (k0 >= k1) k0 = k1 = a.k_lo;  // no tiles (the loops below do nothing): the wave joins the epilogue
 
   uint32_t count = 0;
+  uint64_t wtotal = 0;  // wave-uniform: records of the wave's spans
+  bool ovf = false;     // wave-uniform: a span had more candidates than slots
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
   uint32_t tacc = 0, scnt = 0;
@@ -561,8 +574,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
               a.c_rec[2 * gi] = u32x4{s2, s3, s0, s1};
               a.c_rec[2 * gi + 1] = u32x4{s4, hm, hs, fl};
             }
-          } else if (lane == 0) {
-            atomicOr((unsigned int*)(a.counters + 2), 1u);
+          } else {
+            ovf = true;
           }
           count++;
           continue;
@@ -589,6 +602,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const int lm = r >> 6;                             // m's line (-1: previous tile's line 63)
       const uint32_t hm0 = __shfl(hx, lm & 63);
       const uint32_t hm = lm < 0 ? hxp : hm0;
+      if (count + __popcll(cm) > a.cap) ovf = true;
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
         if (idx < a.cap) {
@@ -599,8 +613,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           a.c_m[gi] = m;
           a.c_rec[2 * gi] = u32x4{f2, f3, f0, f1};
           a.c_rec[2 * gi + 1] = u32x4{f4, hm, hs, fl};
-        } else {
-          atomicOr((unsigned int*)(a.counters + 2), 1u);
         }
       }
       count += __popcll(cm);
@@ -634,6 +646,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
                                             0, 0);
       if (span_end) {
         rvalid = 0;
+        wtotal += count;
         count = 0;
       }
     }
@@ -689,8 +702,63 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     process(k, A, std::true_type{});
   }
 
-  // rootmax is wave-uniform already
-  if (lane == 0 && rootmax) atomicMax(a.counters + 0, (unsigned long long)rootmax);
+  // ---- epilogue: per-wave results; the last block to finish reduces them
+  // (cdna guide: plain stores, vmcnt(0), barrier, lane-0 agent release, add;
+  // the last block acquires before reading) ----
+  if (lane == 0) {
+    a.wave_total[w] = wtotal | (ovf ? (1ull << 63) : 0ull);
+    a.wave_root[w] = rootmax;  // wave-uniform already
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ uint32_t s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = atomicAdd(a.done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // exclusive prefix of the wave counts: thread t owns waves [t*q, (t+1)*q)
+  uint64_t* s_part = (uint64_t*)lds.tab;  // the CRC tables are dead now: 1024 partials
+  __shared__ uint64_t s_root[SCAN_WAVES_V2], s_ovf[SCAN_WAVES_V2];
+  const uint32_t T = blockDim.x, t = threadIdx.x;
+  const uint64_t q = (total_waves + T - 1) / T;
+  uint64_t sum = 0, rmax = 0, o = 0;
+  for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
+    const uint64_t v = a.wave_total[i];
+    sum += v & ~(1ull << 63);
+    o |= v >> 63;
+    rmax = max(rmax, a.wave_root[i]);
+  }
+  s_part[t] = sum;
+  rmax = wave_max_u64(rmax);
+  for (int d = 32; d > 0; d >>= 1) o |= __shfl_xor(o, d);
+  if (lane == 0) { s_root[wv] = rmax; s_ovf[wv] = o; }
+  __syncthreads();
+  for (uint32_t d = 1; d < T; d <<= 1) {  // inclusive Hillis-Steele scan of the T partials
+    const uint64_t x = t >= d ? s_part[t - d] : 0;
+    __syncthreads();
+    s_part[t] += x;
+    __syncthreads();
+  }
+  uint64_t run = t ? s_part[t - 1] : 0;
+  for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
+    a.wave_base[i] = run;
+    run += a.wave_total[i] & ~(1ull << 63);
+  }
+  if (t == 0) {
+    uint64_t mr = 0, oo = 0;
+    for (int i = 0; i < SCAN_WAVES_V2; i++) { mr = max(mr, s_root[i]); oo |= s_ovf[i]; }
+    *a.k_total = s_part[T - 1];
+    a.counters[0] = mr;
+    a.counters[1] = 0;
+    a.counters[2] = oo;
+    *a.done = 0;  // for the next launch on this context
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -951,7 +1019,9 @@ __device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint
 }
 
 constexpr uint64_t LONG_TILES = 4;  // whole tiles a finalize thread combines serially
+constexpr uint64_t NO_REC = ~0ull;
 __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t);
+__device__ bool finalize_core(const FinArgs& a, uint64_t c, uint64_t gi, int64_t pgi, uint64_t root_t, uint64_t* kh_out);
 __global__ void finalize_kernel(FinArgs a) {
   uint64_t n = a.n_chain, root_t = 0;
   if (a.d_status) {
@@ -965,10 +1035,33 @@ __global__ void finalize_kernel(FinArgs a) {
     finalize_one(a, c, root_t);
 }
 __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
+  uint64_t gi = NO_REC;
+  int64_t pgi = -1;
+  if (c >= a.coff) {
+    const uint64_t g = a.chain_g[c];
+    gi = a.d_status ? g : a.slot[g];
+    // plan mode: chain_g holds record slots and the parent of entry c > coff
+    // is entry c - 1; otherwise the dense parent of g
+    const int64_t pg = a.d_status ? (c >= a.coff + 1 ? 0 : PAR_ROOT) : a.par[g];
+    if (pg >= 0) pgi = (int64_t)(a.d_status ? a.chain_g[c - 1] : a.slot[pg]);
+  }
+  uint64_t kh;
+  if (finalize_core(a, c, gi, pgi, root_t, &kh)) {
+    const unsigned long long w = atomicAdd(a.n_slow, 1ull);
+    a.slow_list[w] = c;
+  }
+}
+
+// Chain entry c: its candidate record gi (NO_REC: the root entry, from
+// root_t) and its parent's record pgi (< 0: the parent is the root entry or
+// lies outside the span).  Writes every output; returns true when the CRC
+// needs slow_one (o_pieces / o_suf / o_sxm / o_tail hold its inputs then).
+__device__ bool finalize_core(const FinArgs& a, uint64_t c, uint64_t gi, int64_t pgi, uint64_t root_t,
+                              uint64_t* kh_out) {
   uint64_t mo, kh, p, start, len;
   uint32_t crc_st, suf = 0, sxm = 0, tail = 0, pieces = 0;
   bool tomb;
-  if (c < a.coff) {
+  if (gi == NO_REC) {
     const uint64_t t = root_t;
     mo = t - 20;
     kh = ld_u64_unaligned(a.file, mo);
@@ -979,8 +1072,6 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
     suf = tile_T(a.tile, 0);
     pieces = 1;
   } else {
-    const uint64_t g = a.chain_g[c];
-    const uint64_t gi = a.d_status ? g : a.slot[g];
     mo = a.c_m[gi];
     const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
     p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
@@ -994,9 +1085,7 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
       pieces |= 2;
     }
     if (fl & F_TAIL) { tail = 0; pieces |= 4; }
-    const int64_t pg = a.d_status ? (c >= a.coff + 1 ? 0 : PAR_ROOT) : a.par[g];
-    if (pg >= 0) {
-      const uint64_t pgi = a.d_status ? a.chain_g[c - 1] : a.slot[pg];
+    if (pgi >= 0) {
       const u32x4 pr1 = a.c_rec[2 * pgi + 1];
       const uint32_t kind = (pr1[3] >> F_SUF_SHIFT) & 3;
       const uint64_t k0 = start / TILE;  // kind 0: the parent's tile; 1, 2: the next one
@@ -1008,6 +1097,7 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
       pieces |= 1;
     }
   }
+  *kh_out = kh;
   // A piece no record holds (the root entry's metadata-line suffix, its
   // child's start-line suffix: the root has no candidate record) comes from
   // the per-tile values when its line is 0, 1 or 32 of the tile (C1/C2/C5:
@@ -1034,13 +1124,13 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
   a.o_start[c] = start;
   a.o_len[c] = len;
   a.o_crc_st[c] = crc_st;
-  if (a.no_crc) { a.o_crc[c] = 0; a.o_ok[c] = 0; return; }
+  if (a.no_crc) { a.o_crc[c] = 0; a.o_ok[c] = 0; return false; }
   if (tomb) {
     const uint32_t crc = 0xD202EF8Du;  // CRC32(b"\0"): the tombstone byte is 0 by the rule
     a.o_crc[c] = crc;
     a.o_ok[c] = crc == crc_st;
     if (crc != crc_st) atomicAdd(a.n_bad, 1ull);
-    return;
+    return false;
   }
   if (!(pieces & 4)) tail = tail_crc(a.file, mo);  // re-read the partial last line
   const bool need_long = len >= 64;
@@ -1051,15 +1141,16 @@ __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t) {
     a.o_crc[c] = crc;
     a.o_ok[c] = crc == crc_st;
     if (crc != crc_st) atomicAdd(a.n_bad, 1ull);
-  } else {
-    a.o_pieces[c] = pieces;
-    a.o_suf[c] = suf;
-    a.o_sxm[c] = sxm;
-    a.o_tail[c] = tail;
-    const unsigned long long w = atomicAdd(a.n_slow, 1ull);
-    a.slow_list[w] = c;
+    return false;
   }
+  a.o_pieces[c] = pieces;
+  a.o_suf[c] = suf;
+  a.o_sxm[c] = sxm;
+  a.o_tail[c] = tail;
+  return true;
 }
+
+
 
 // Recompute, with one wave, SX at line j of tile k (bytes past flen read as 0;
 // the buffer is readable to srd_padded_size).  tab = the 4x256 CRC table in LDS.
@@ -1138,6 +1229,22 @@ __device__ uint32_t crc_from_pieces_wave(uint64_t s, uint64_t m, uint32_t suf, u
 // (SLOW_WAVES waves per block share the LDS tables; few blocks keep the
 // launch cheap when the list is empty, the common case)
 constexpr int SLOW_WAVES = 4;
+// one wave: chain entry c's CRC from its recorded inputs (o_start / o_mo /
+// o_pieces / o_suf / o_sxm / o_tail), recomputing missing pieces from the
+// file.  tab, mx: the CRC and X^64 byte tables in LDS.
+__device__ void slow_one(const FinArgs& a, uint64_t c, const uint32_t* tab, const uint32_t* mx) {
+  const uint64_t s = a.o_start[c], m = a.o_mo[c];
+  const uint32_t pieces = a.o_pieces[c], tail = a.o_tail[c];
+  uint32_t suf = a.o_suf[c], sxm = a.o_sxm[c];
+  if (!(pieces & 1)) suf = tile_probe_sx(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64), tab);
+  if (!(pieces & 2)) sxm = tile_probe_sx(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64), tab);
+  const uint32_t crc = crc_from_pieces_wave(s, m, suf, sxm, tail, a.tile, mx);
+  if ((threadIdx.x & 63) == 0) {
+    a.o_crc[c] = crc;
+    a.o_ok[c] = crc == a.o_crc_st[c];
+    if (crc != a.o_crc_st[c]) atomicAdd(a.n_bad, 1ull);
+  }
+}
 __global__ __launch_bounds__(SLOW_WAVES * 64) void slow_kernel(FinArgs a) {
   __shared__ uint32_t tab[1024];
   __shared__ uint32_t mx[1024];
@@ -1149,19 +1256,8 @@ __global__ __launch_bounds__(SLOW_WAVES * 64) void slow_kernel(FinArgs a) {
   }
   __syncthreads();
   for (uint64_t w = (uint64_t)blockIdx.x * SLOW_WAVES + (threadIdx.x >> 6); w < ns;
-       w += (uint64_t)gridDim.x * SLOW_WAVES) {
-    const uint64_t c = a.slow_list[w];
-    const uint64_t s = a.o_start[c], m = a.o_mo[c];
-    uint32_t pieces = a.o_pieces[c], suf = a.o_suf[c], sxm = a.o_sxm[c], tail = a.o_tail[c];
-    if (!(pieces & 1)) suf = tile_probe_sx(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64), tab);
-    if (!(pieces & 2)) sxm = tile_probe_sx(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64), tab);
-    const uint32_t crc = crc_from_pieces_wave(s, m, suf, sxm, tail, a.tile, mx);
-    if ((threadIdx.x & 63) == 0) {
-      a.o_crc[c] = crc;
-      a.o_ok[c] = crc == a.o_crc_st[c];
-      if (crc != a.o_crc_st[c]) atomicAdd(a.n_bad, 1ull);
-    }
-  }
+       w += (uint64_t)gridDim.x * SLOW_WAVES)
+    slow_one(a, a.slow_list[w], tab, mx);
 }
 
 // --------------------------------------------------------------------------

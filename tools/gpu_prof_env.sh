@@ -11,4 +11,4 @@ python3 -c "
 import csv
 for r in csv.DictReader(open('$f')):
     print(f\"{r['Name'][:58]:58s} {r['Calls']:>5s} avg {float(r['AverageNs'])/1e3:9.1f} us\")
-" | head -30
+" | head -40
