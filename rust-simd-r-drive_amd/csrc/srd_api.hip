@@ -93,6 +93,7 @@ struct Ctx {
   int stage_workers = 8;
   int stage_mode = -1;  // last call: 0 pinned input, 1 registered, 2 bounce buffers, 3 pageable
   double stage_ms = 0;  // host wall time of the last staging
+  bool ev3_recorded = false;  // the optimistic pass recorded ev[3] before its final sync
   std::vector<void*> stage_pin;
   std::vector<hipStream_t> stage_streams;
   std::vector<hipEvent_t> stage_ev;
@@ -114,7 +115,7 @@ enum BufId {
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST, B_XPART,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
-  B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE,
+  B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
   B_COUNT_
 };
 
@@ -241,6 +242,19 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s) {
 static bool debug_env() {
   static const bool v = [] { const char* e = getenv("SRD_DEBUG"); return e && *e && *e != '0'; }();
   return v;
+}
+
+// Wait for the stream by polling (the call's result is on the host's
+// critical path: a blocking wait's wake-up adds tens of us per call)
+static hipError_t spin_sync(hipStream_t s) {
+#ifdef SRD_NO_SPIN
+  return hipStreamSynchronize(s);
+#else
+  hipError_t e;
+  while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+  }
+  return e;
+#endif
 }
 
 int read_counters(Ctx* c, uint64_t* h) {
@@ -570,6 +584,9 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.c_rec = P<u32x4>(c, B_CREC);
     a.counters = (unsigned long long*)cnt;
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
+    TRY(ensure(c, B_SPAN_FIRST, (n_spans + 1) * 4));
+    a.span_first = P<uint32_t>(c, B_SPAN_FIRST);
+    a.wcap = 0;  // the full pass stores records at span * cap + slot
     TRY(scan_wave_args(c, &a));
     if (n_spans) {
       unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
@@ -741,8 +758,14 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     // index buckets: ~IDX_BUCKET_AVG chain entries per bucket
     const uint64_t n_est = std::max<uint64_t>(std::max<uint64_t>(c->last_n, (flen - span_off) / 4096), 1);
     const uint32_t log2_nbk = index_log2_buckets(n_est);
-    TRY(alloc_scan(c, nt_rel, ns_rel));
-    TRY(ensure_cub(c, ns_rel + 1));
+    // the scan's partition: total_waves waves of spw spans; each wave's
+    // records are dense in its region of wcap = spw * cap slots
+    const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
+    const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
+    const uint64_t spw = (ns_rel + total_waves - 1) / total_waves;
+    const uint64_t wcap = spw * c->cap;
+    TRY(alloc_scan(c, nt_rel, std::max<uint64_t>(ns_rel, total_waves * spw)));
+    TRY(ensure(c, B_SPAN_FIRST, (ns_rel + 1) * 4));
     TRY(alloc_fast(c, capK, log2_nbk));
     if (c->gen >= 0xFFFFFFF0u || c->gen == 0) {  // tag wrap: clear the marks once
       c->gen = 0;
@@ -765,8 +788,10 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.cap = c->cap;
     a.tile = P<uint32_t>(c, B_TILE) - 4 * k_lo;
     a.span_count = P<uint32_t>(c, B_SPAN_COUNT) - s_lo;
-    a.c_m = P<uint64_t>(c, B_CM) - s_lo * c->cap;
-    a.c_rec = P<u32x4>(c, B_CREC) - 2 * s_lo * c->cap;
+    a.c_m = P<uint64_t>(c, B_CM);  // wave regions, indexed by the wave of this launch
+    a.c_rec = P<u32x4>(c, B_CREC);
+    a.span_first = P<uint32_t>(c, B_SPAN_FIRST) - s_lo;
+    a.wcap = wcap;
     a.counters = (unsigned long long*)cnt;
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
     a.k_lo = k_lo;
@@ -775,8 +800,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.n_zero_words = (uint32_t)(sizeof(Plan) / 4);
     a.sentinel = nullptr;
     TRY(scan_wave_args(c, &a));
-    const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
-    const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     launch_scan<false>(g, a, c->stream);
     KCHK(c, "scan_kernel");
@@ -787,11 +810,13 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.flen = flen;
     l.n_spans = n_spans;
     l.capK = capK;
-    l.cap = c->cap;
     l.gen = c->gen;
     l.span_count = a.span_count;
+    l.span_first = a.span_first;
     l.wave_base = a.wave_base;
-    l.spw = (ns_rel + total_waves - 1) / total_waves;
+    l.wave_total = a.wave_total;
+    l.spw = spw;
+    l.wcap = wcap;
     l.c_m = a.c_m;
     l.c_rec = a.c_rec;
     l.d_m = P<uint64_t>(c, B_DM);
@@ -800,7 +825,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.has_child = P<uint32_t>(c, B_HASCHILD);
     l.s_lo = s_lo;
     l.span_lo = lo;
-    link2_kernel<<<(unsigned)total_waves, 256, 0, c->stream>>>(l);
+    link2_kernel<<<blocks(ns_rel, 64), 256, 0, c->stream>>>(l);
     KCHK(c, "link2_kernel");
     // ---- shape check, chain, finalize, index; retried on device with more
     //      prune rounds when false candidates chained onto each other ----
@@ -874,8 +899,10 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       if (!index_global_env())
         TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
                                   P<uint64_t>(c, B_IPACKED), pl, sa.part, coff));
+      HIPCHK(hipEventRecord(c->ev[3], c->stream));  // end of the device work (srd_ctx_timings)
+      c->ev3_recorded = true;
       HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
+      HIPCHK(spin_sync(c->stream));
       hp = *c->h_plan;
       if (debug_env()) {
         fprintf(stderr, "plan K=%lu n_chain=%lu root_t=%lu start=%lu n_index=%lu bad=%lu slow=%lu st=%u nroot=%u "
@@ -916,7 +943,10 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     out->n_crc_bad = hp.n_bad;
     out->n_index = hp.n_index;
     c->last_n = hp.n_chain;
-    if (hp.idx_overflow || index_global_env()) TRY(index_global(c, hp.n_chain, &out->n_index));
+    if (hp.idx_overflow || index_global_env()) {
+      c->ev3_recorded = false;
+      TRY(index_global(c, hp.n_chain, &out->n_index));
+    }
     set_out_ptrs(c, out);
     *done = true;
     return 0;
@@ -933,10 +963,13 @@ extern "C" int srd_validate_index_device(srd_ctx* c, const uint8_t* d_file, uint
   HIPCHK(hipSetDevice(c->device));
   c->scan_ms = 0;
   c->scan_launches = 0;
+  c->ev3_recorded = false;
   HIPCHK(hipEventRecord(c->ev[2], c->stream));
   int r = validate_device_impl(c, d_file, flen, flags, out);
-  HIPCHK(hipEventRecord(c->ev[3], c->stream));
-  HIPCHK(hipEventSynchronize(c->ev[3]));
+  if (!(r == 0 && out->mode == SRD_MODE_OPTIMISTIC && c->ev3_recorded)) {
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[3]));
+  }
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
   c->total_ms = ms;

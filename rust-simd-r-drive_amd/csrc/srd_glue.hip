@@ -233,10 +233,13 @@ __device__ uint64_t block_scan_partials(const uint32_t* part, uint32_t np, uint3
 struct Link2Args {
   const uint8_t* file;
   uint64_t flen, n_spans, capK;
-  uint32_t cap, gen;
+  uint32_t gen;
   const uint32_t* span_count;
-  const uint64_t* wave_base;  // scan_kernel's last block: dense base of each scan wave's records
-  uint64_t spw;               // spans per scan wave (the scan's partition)
+  const uint32_t* span_first;  // scan_kernel: span's first record inside its wave's region
+  const uint64_t* wave_base;   // scan_kernel's last block: dense index of each scan wave's first record
+  const uint64_t* wave_total;  // records per scan wave (bit 63: overflow)
+  uint64_t spw;                // spans per scan wave (the scan's partition)
+  uint64_t wcap;               // record slots per scan wave
   const uint64_t* c_m;
   u32x4* c_rec;  // tombstone flags are set in place
   uint64_t* d_m;
@@ -247,115 +250,71 @@ struct Link2Args {
   uint64_t span_lo;  // span mode: the shard's lower tail (a node with p == span_lo is the shard's first entry); 0 = whole file
 };
 
-// dense base of span sp: its scan wave's base + the counts of the wave's
-// earlier spans (the rare binary-search path into another wave's span)
-__device__ __forceinline__ uint64_t span_base_of(const Link2Args& a, uint64_t sp) {
-  const uint64_t w = (sp - a.s_lo) / a.spw, s0 = a.s_lo + w * a.spw;
-  uint64_t b = a.wave_base[w];
-  for (uint64_t s = s0; s < sp; s++) b += a.span_count[s];
-  return b;
-}
-
-// One block per scan wave, 4 lanes per span: every load a lane needs for its
-// first record (the record, the previous record's m, the span counts, the
-// wave base) is issued at once -- the span bases (a 64-span block scan in
-// LDS) are needed only for the dense indices written at the end.
-__device__ __forceinline__ void link_one(const Link2Args& a, uint64_t sp, uint32_t i, uint64_t gb, uint64_t m,
-                                         u32x4 r0, u32x4 r1, uint64_t m_prev, bool have_prev, const uint64_t* base,
-                                         uint64_t g0, uint64_t gend) {
-  const uint64_t gi = sp * a.cap + i, g = gb + i;
-  if (g >= a.capK) return;  // scatter_plan reports ST_CAPK
-  const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-  bool node = true;
-  if (r1[3] & F_NT) {
-    // single-candidate record, deferred node test (data_store.rs:404-470);
-    // F_ZB is the byte at m - 1, the tombstone byte when p == m - 1
-    const uint64_t dp = m - p;
-    const bool tomb = dp == 1 && (r1[3] & F_ZB);
-    node = p >= 20 && p < m && (tomb || dp > prepad64(p));
-    if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
-  }
-  const uint64_t mp = p - 20;  // p >= 20 for nodes
-  const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
-  // In a store without garbage the parent is the previous record in file
-  // order (the same span's slot i-1, else the previous span's last slot):
-  // one load instead of a binary search.
-  int64_t par = have_prev && m_prev == mp ? (int64_t)(g - 1) : PAR_MISS;
-  if (par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
-    const uint32_t n2 = min(a.span_count[sp2], a.cap);
-    uint32_t lo = 0, hi = n2;
-    const uint64_t* cm = a.c_m + sp2 * a.cap;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (cm[mid] < mp) lo = mid + 1; else hi = mid;
-    }
-    if (lo < n2 && cm[lo] == mp)
-      par = (int64_t)((sp2 >= g0 && sp2 < gend ? base[sp2 - g0] : span_base_of(a, sp2)) + lo);
-  }
-  if (!node) par = PAR_MISS;  // no parent, no root
-  else if (par == PAR_MISS) {
-    if (a.span_lo) {
-      if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
-    } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {
-      par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
-    }
-  }
-  a.d_m[g] = m;
-  a.d_par[g] = par;
-  a.d_slot[g] = gi;
-  if (par >= 0 && (uint64_t)par < a.capK) a.has_child[par] = a.gen;
-}
-
+// 4 lanes per span.  The scan wrote each wave's records densely in file
+// order: record i of span sp lives at slot w*wcap + span_first[sp] + i and
+// has the dense index wave_base[w] + span_first[sp] + i.
 __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
-  __shared__ uint64_t base[65];
-  const uint64_t sA = a.s_lo + (uint64_t)blockIdx.x * a.spw, sB = min(sA + a.spw, a.n_spans);
-  uint64_t run = a.wave_base[blockIdx.x];
-  for (uint64_t g0 = sA; g0 < sB; g0 += 64) {
-    const uint64_t sp = g0 + (threadIdx.x >> 2);
-    const uint32_t i0 = threadIdx.x & 3;
-    const bool in = sp < sB;
-    const uint64_t spc = in ? sp : sA;
-    // speculative loads of slot i0 (the slots exist; unused ones are ignored)
-    const uint32_t cnt = in ? a.span_count[sp] : 0u;
-    const uint32_t cnt_prev = (i0 == 0 && sp > a.s_lo && in) ? a.span_count[sp - 1] : 0u;
-    const uint64_t gi0 = spc * a.cap + i0;
-    const uint64_t m0 = a.c_m[gi0];
-    const u32x4 r00 = a.c_rec[2 * gi0], r01 = a.c_rec[2 * gi0 + 1];
-    const uint64_t mprev0 = i0 ? a.c_m[gi0 - 1] : 0;
-    if (threadIdx.x < 64) {  // bases of the group's spans (wave 0; counts of spans g0 + lane)
-      const uint64_t s2 = g0 + threadIdx.x;
-      const uint64_t c = s2 < sB ? a.span_count[s2] : 0;
-      uint64_t x = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o);
-        if ((int)threadIdx.x >= o) x += y;
-      }
-      base[threadIdx.x] = run + x - c;
-      if (threadIdx.x == 63) base[64] = run + x;
+  const uint64_t sp = a.s_lo + (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  if (sp >= a.n_spans) return;
+  const uint64_t w = (sp - a.s_lo) / a.spw;
+  const uint32_t n = a.span_count[sp], first = a.span_first[sp];
+  const uint64_t gw = w * a.wcap, gb = a.wave_base[w] + first;
+  for (uint32_t i = threadIdx.x & 3; i < n; i += 4) {
+    if ((uint64_t)first + i >= a.wcap) return;  // wave overflow: scatter_plan reports ST_OVERFLOW
+    const uint64_t gi = gw + first + i, g = gb + i;
+    if (g >= a.capK) return;  // chain_finalize reports ST_CAPK
+    const uint64_t m = a.c_m[gi];
+    const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
+    // the previous record in file order: the slot before (same wave), else
+    // the previous wave's last record
+    uint64_t mprev = 0;
+    bool hp = true;
+    if (first + i > 0) {
+      mprev = a.c_m[gi - 1];
+    } else {
+      const uint64_t wt = w ? (a.wave_total[w - 1] & ~(1ull << 63)) : 0;
+      hp = wt > 0 && wt <= a.wcap;
+      if (hp) mprev = a.c_m[(w - 1) * a.wcap + wt - 1];
     }
-    __syncthreads();
-    if (in) {
-      const uint32_t n = min(cnt, a.cap);
-      const uint64_t gb = base[threadIdx.x >> 2];
-      if (i0 < n) {
-        uint64_t mp0 = mprev0;
-        bool hp = i0 > 0;
-        if (i0 == 0) {
-          const uint32_t np = min(cnt_prev, a.cap);
-          hp = np > 0;
-          if (hp) mp0 = a.c_m[(sp - 1) * a.cap + np - 1];
-        }
-        link_one(a, sp, i0, gb, m0, r00, r01, mp0, hp, base, g0, min(g0 + 64, sB));
+    const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+    bool node = true;
+    if (r1[3] & F_NT) {
+      // single-candidate record, deferred node test (data_store.rs:404-470);
+      // F_ZB is the byte at m - 1, the tombstone byte when p == m - 1
+      const uint64_t dp = m - p;
+      const bool tomb = dp == 1 && (r1[3] & F_ZB);
+      node = p >= 20 && p < m && (tomb || dp > prepad64(p));
+      if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
+    }
+    const uint64_t mp = p - 20;  // p >= 20 for nodes
+    const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
+    // In a store without garbage the parent is the previous record in file
+    // order: one load instead of a binary search.
+    int64_t par = hp && mprev == mp ? (int64_t)(g - 1) : PAR_MISS;
+    if (par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
+      const uint64_t w2 = (sp2 - a.s_lo) / a.spw;
+      const uint32_t f2 = a.span_first[sp2];
+      const uint32_t n2 = (uint32_t)min<uint64_t>(a.span_count[sp2], a.wcap - min<uint64_t>(f2, a.wcap));
+      uint32_t lo = 0, hi = n2;
+      const uint64_t* cm = a.c_m + w2 * a.wcap + f2;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cm[mid] < mp) lo = mid + 1; else hi = mid;
       }
-      for (uint32_t i = i0 + 4; i < n; i += 4) {  // spans with more than 4 records
-        const uint64_t gi = sp * a.cap + i;
-        link_one(a, sp, i, gb, a.c_m[gi], a.c_rec[2 * gi], a.c_rec[2 * gi + 1], a.c_m[gi - 1], true, base, g0,
-                 min(g0 + 64, sB));
+      if (lo < n2 && cm[lo] == mp) par = (int64_t)(a.wave_base[w2] + f2 + lo);
+    }
+    if (!node) par = PAR_MISS;  // no parent, no root
+    else if (par == PAR_MISS) {
+      if (a.span_lo) {
+        if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
+      } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {
+        par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
       }
     }
-    run = base[64];
-    __syncthreads();
+    a.d_m[g] = m;
+    a.d_par[g] = par;
+    a.d_slot[g] = gi;
+    if (par >= 0 && (uint64_t)par < a.capK) a.has_child[par] = a.gen;
   }
 }
 

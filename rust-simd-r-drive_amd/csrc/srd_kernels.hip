@@ -102,6 +102,13 @@ struct ScanArgs {
   uint64_t* wave_base;
   uint64_t* k_total;
   uint32_t* done;
+  // optimistic pass: the records of scan wave w are DENSE in file order at
+  // [w*wcap, (w+1)*wcap) (consecutive span flushes fill whole cache lines;
+  // per-span slots left most lines partial: +0.11 ms of HBM writes at C2);
+  // span_first[s] = index of span s's first record inside its wave's region
+  // (the full pass keeps span*cap + slot)
+  uint32_t* span_first;
+  uint64_t wcap;
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -337,11 +344,17 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   bool ovf = false;     // wave-uniform: a span had more candidates than slots
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
-  uint32_t tacc = 0, scnt = 0;
+  uint32_t tacc = 0, scnt = 0, sfirst = 0;
   uint32_t rq[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) rq[i] = 0;
-  uint64_t rvalid = 0;  // wave-uniform: record slots buffered in rq
+  // records buffered in rq: the wave's records [flushed, wtotal + count) sit
+  // in lanes [0, wtotal + count - flushed) (< 64); they are written out with
+  // whole-line stores once >= FLUSH_AT are pending (and at the wave's end):
+  // a real store holds the prefetch ring's vmcnt waits until it completes,
+  // so few large flushes beat one per span
+  uint64_t flushed = 0;  // wave-uniform
+  uint64_t rvalid = 0;   // wave-uniform: bit j = record flushed + j is in lane j (multi-candidate lines store directly)
 
   // Unconditional loads: the buffer is readable to srd_padded_size(flen)
   // (no loads under divergent/uniform branches, so the compiler's vmcnt
@@ -548,15 +561,15 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
           const int lm = rs >> 6;
           const uint32_t hm = lm < 0 ? __builtin_amdgcn_readfirstlane(hxp) : __builtin_amdgcn_readlane(hx, lm & 63);
-          if (count < a.cap) {
+          const uint64_t r = wtotal + count;  // the record's index in the wave's region
+          if (r < a.wcap) {
             const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
             const uint32_t fl = REC_KIND | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
                                 (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
                                 ((js & 63) < 32 ? F_SUF_LO : 0u);
-            if (count < 64) {
-              // slot `count` of the span -> lane `count` of the record
-              // registers (flushed at the span's end)
-              const bool mine = lane == (int)count;
+            if (r - flushed < 64) {
+              // record r -> lane r - flushed of the record registers
+              const bool mine = lane == (int)(r - flushed);
               rq[0] = mine ? (uint32_t)m : rq[0];
               rq[1] = mine ? (uint32_t)(m >> 32) : rq[1];
               rq[2] = mine ? hm : rq[2];
@@ -567,9 +580,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
               rq[7] = mine ? s0 : rq[7];
               rq[8] = mine ? s1 : rq[8];
               rq[9] = mine ? s4 : rq[9];
-              rvalid |= 1ull << count;
+              rvalid |= 1ull << (r - flushed);
             } else if (lane == 0) {
-              const uint64_t gi = span * a.cap + count;
+              const uint64_t gi = w * a.wcap + r;
               a.c_m[gi] = m;
               a.c_rec[2 * gi] = u32x4{s2, s3, s0, s1};
               a.c_rec[2 * gi + 1] = u32x4{s4, hm, hs, fl};
@@ -602,11 +615,11 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const int lm = r >> 6;                             // m's line (-1: previous tile's line 63)
       const uint32_t hm0 = __shfl(hx, lm & 63);
       const uint32_t hm = lm < 0 ? hxp : hm0;
-      if (count + __popcll(cm) > a.cap) ovf = true;
+      if (FULL ? count + __popcll(cm) > a.cap : wtotal + count + __popcll(cm) > a.wcap) ovf = true;
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
-        if (idx < a.cap) {
-          const uint64_t gi = span * a.cap + idx;
+        if (FULL ? idx < a.cap : wtotal + idx < a.wcap) {
+          const uint64_t gi = FULL ? span * a.cap + idx : w * a.wcap + wtotal + idx;
           const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
           const uint32_t fl = (tomb ? F_TOMB : 0u) | ((r & 63) == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT) |
                               (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) | ((js & 63) < 32 ? F_SUF_LO : 0u);
@@ -627,27 +640,35 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     // (lane span%64 of scnt, one store per 64 spans) -- unconditional stores
     const bool span_end = (k + 1) % SPAN_TILES == 0 || k + 1 == k1;  // uniform
     {
-      const bool w = span_end && ((rvalid >> lane) & 1);
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + span * a.cap, 64 * 8),
-                                            w ? 8u * lane : OOB_OFF, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]},
-                                             out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
-                                             w ? 32u * lane : OOB_OFF, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]},
-                                             out_rsrc(a.c_rec + 2 * span * a.cap, 64 * 32),
-                                             w ? 32u * lane + 16u : OOB_OFF, 0, 0);
+      // (optimistic pass only; the full pass stores its records directly)
+      constexpr uint64_t FLUSH_AT = 40;
+      const uint64_t pend = wtotal + count - flushed;  // records pending (lanes [0, min(pend, 64)))
+      const bool fl = span_end && (pend >= FLUSH_AT || k + 1 == k1);  // uniform
+      const bool wr = fl && ((rvalid >> lane) & 1);
+      const uint64_t rb = w * a.wcap + flushed;  // lane 0's record
+      const uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + rb, rn * 8),
+                                            wr ? 8u * lane : OOB_OFF, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
+                                             wr ? 32u * lane : OOB_OFF, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
+                                             wr ? 32u * lane + 16u : OOB_OFF, 0, 0);
       const uint32_t sp = (uint32_t)(span & 63);
       scnt = (span_end && (uint32_t)lane == sp) ? count : scnt;
+      sfirst = (span_end && (uint32_t)lane == sp) ? (uint32_t)wtotal : sfirst;
       const bool sfl = span_end && (sp == 63 || k + 1 == k1);
       const uint64_t sg = span & ~63ull;
       const uint32_t slo = (uint32_t)(max(sg, k0 / SPAN_TILES) - sg);
-      __builtin_amdgcn_raw_buffer_store_b32(scnt, out_rsrc(a.span_count + sg, 256),
-                                            (sfl && (uint32_t)lane >= slo && (uint32_t)lane <= sp) ? 4u * lane : OOB_OFF,
-                                            0, 0);
+      const uint32_t soff = (sfl && (uint32_t)lane >= slo && (uint32_t)lane <= sp) ? 4u * lane : OOB_OFF;
+      __builtin_amdgcn_raw_buffer_store_b32(scnt, out_rsrc(a.span_count + sg, 256), soff, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(sfirst, out_rsrc(a.span_first + sg, 256), soff, 0, 0);
       if (span_end) {
-        rvalid = 0;
         wtotal += count;
         count = 0;
+        if (fl) {
+          flushed = wtotal;
+          rvalid = 0;
+        }
       }
     }
   };
@@ -664,14 +685,14 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   uint32_t A[16], Bv[16], Cv[16];
   // vmcnt counts loads and stores in issue order, and the compiler's wait
   // counts at the loop header are the minimum over its entries.  In the
-  // steady state every tile's loads are followed by process()'s 5
-  // unconditional stores (tile values, span records, span count); without
+  // steady state every tile's loads are followed by process()'s 6
+  // unconditional stores (tile values, span records, span count / first); without
   // them on the entry path the first iteration's shorter queue sets every
   // wait of the loop, which then waits for part of the next tile early.
   // Dummy stores (out-of-range offsets: dropped by the hardware; distinct,
   // or the compiler merges them as dead stores) give the entry the same queue.
   auto pad_stores = [&](uint32_t g) {
-    constexpr uint32_t NST = 5u;  // process()'s unconditional stores
+    constexpr uint32_t NST = 6u;  // process()'s unconditional stores
 #pragma unroll
     for (uint32_t i = 0; i < NST; i++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, out_rsrc(a.tile, 256), OOB_OFF - 64u * (NST * g + i), 0, 0);
