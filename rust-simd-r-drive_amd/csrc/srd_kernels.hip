@@ -485,32 +485,25 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     while (slow) {
       const int f = __builtin_ctzll(slow);
       slow &= slow - 1;
-      // stage [L-16, L+72): lane f-1 (or the saved tail for f == 0), f, f+1
-      // (or the prefetched next tile's lane 0 for f == 63)
-      if (f > 0 && lane == f - 1) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) win[j] = d[12 + j];
-      }
-      if (lane == f) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) win[4 + j] = d[j];
-      }
-      if (f < 63) {
-        if (lane == f + 1) {
-          win[20] = d[0];
-          win[21] = d[1];
-        }
-      } else {
-        uint32_t n0, n1;
+      // stage [L-16, L+72) from lane f alone: its line, the previous line's
+      // tail and the next line's head moved into every lane by DPP (one exec
+      // group, 16-byte LDS stores); f == 0: the previous tile's tail is
+      // already in win[0..3]; f == 63: the next tile's head by a scalar load
+      const uint32_t p12 = dpp<DPP_WAVE_SHR1>(d[12]), p13 = dpp<DPP_WAVE_SHR1>(d[13]),
+                     p14 = dpp<DPP_WAVE_SHR1>(d[14]), p15 = dpp<DPP_WAVE_SHR1>(d[15]);
+      uint32_t n0 = dpp<DPP_WAVE_SHL1>(d[0]), n1 = dpp<DPP_WAVE_SHL1>(d[1]);
+      if (f == 63) {
         next_head(k, &n0, &n1);
         if (tail_tile) {
           n0 = mask_past_end32(n0, TILE, remu);
           n1 = mask_past_end32(n1, TILE + 4, remu);
         }
-        if (lane == 0) {
-          win[20] = n0;
-          win[21] = n1;
-        }
+      }
+      if (lane == f) {
+        if (f > 0) *(u32x4*)&win[0] = u32x4{p12, p13, p14, p15};
+#pragma unroll
+        for (int j = 0; j < 4; j++) *(u32x4*)&win[4 + 4 * j] = u32x4{d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]};
+        *(u32x2*)&win[20] = u32x2{n0, n1};
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
