@@ -80,7 +80,13 @@ class HipBackend:
     def __init__(self, ctx: S.Context, device: int):
         self.ctx, self.device = ctx, device
 
+    def _after_torch(self, t: torch.Tensor):
+        # inputs written on torch's stream (copies, the RCCL collectives):
+        # the library's own stream waits for them (an event, no host sync)
+        torch.cuda.ExternalStream(self.ctx.stream, device=t.device).wait_stream(torch.cuda.current_stream(t.device))
+
     def validate_span(self, buf: torch.Tensor, span_off: int, lo: int, hi: int, flags: int = 0):
+        self._after_torch(buf)
         r = S.validate_span_device(buf.data_ptr(), span_off, lo, hi, flags, self.ctx)
         proven = r.mode == S.SRD_MODE_OPTIMISTIC or (lo == 0 and r.final_len == hi)
         st = ShardStatus(bool(proven), lo, hi, int(r.n_chain), int(r.n_crc_bad))
@@ -98,6 +104,7 @@ class HipBackend:
         n = pairs.numel() // 2
         ok = torch.empty(max(n, 1), dtype=torch.int64, device=pairs.device)
         op = torch.empty(max(n, 1), dtype=torch.int64, device=pairs.device)
+        self._after_torch(pairs)  # the RCCL all_to_all wrote `pairs` on torch's stream
         ni = S.index_build_device(pairs.data_ptr(), n, ok.data_ptr(), op.data_ptr(), self.ctx)
         return ok[:ni], op[:ni]
 

@@ -158,3 +158,24 @@ def test_synth_span_matches_whole_store(ctx):
         assert torch.equal(t[: hi - span_off], whole[span_off:hi]), (first, cnt)
         r = S.validate_span_device(t.data_ptr(), span_off, lo, hi, 0, ctx)
         assert (r.mode, r.final_len, r.n_chain, r.n_crc_bad, r.n_index) == (0, hi, cnt, 0, cnt), (first, r.mode)
+
+
+def test_backend_build_waits_for_torch_stream(ctx):
+    """The index exchange hands the library pairs produced on torch's stream
+    (the RCCL all_to_all); HipBackend.build must order its own stream after
+    it.  torch's stream is held back by a sleep kernel before the copy that
+    produces the pairs: a build that does not wait reads zeros."""
+    import torch
+    import srd_shard as SH
+    store = O.synth_store(300)
+    ch = O.chain(store, store.size)
+    host = np.array([[e["key_hash"], ((e["key_hash"] >> 48) << 48) | e["meta_off"]] for e in ch],
+                    np.uint64).reshape(-1)
+    src = torch.from_numpy(host.view(np.int64)).cuda()
+    dst = torch.zeros_like(src)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)  # ~0.1 s of GPU time on torch's current stream
+    dst.copy_(src)
+    ok, op = SH.HipBackend(ctx, 0).build(dst)
+    got = dict(zip(ok.cpu().numpy().view(np.uint64).tolist(), op.cpu().numpy().view(np.uint64).tolist()))
+    assert got == O.key_indexer_build(store, store.size)
