@@ -113,7 +113,7 @@ enum BufId {
   B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
   B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
-  B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST, B_XPART,
+  B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
   B_COUNT_
@@ -213,19 +213,6 @@ int ensure_cub(Ctx* c, uint64_t n) {
                                 (uint64_t*)nullptr, (uint64_t*)nullptr, nn);
   t5 = std::max(std::max(t1, t2), std::max(t3, t4));
   return ensure(c, B_CUB_TMP, t5 + 256);
-}
-
-// exclusive scan of n u32 counts into u32 / u64 offsets on the call's stream
-// (xscan_* kernels: chunk sums, then per-block prefix + scan)
-template <class OUT>
-static int xscan(Ctx* c, const uint32_t* in, OUT* out, uint64_t n) {
-  TRY(ensure(c, B_XPART, GLUE_BLOCKS * 8));
-  xscan_sum_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(in, n, P<uint64_t>(c, B_XPART));
-  KCHK(c, "xscan_sum_kernel");
-  xscan_apply_kernel<OUT><<<GLUE_BLOCKS, 256, 0, c->stream>>>(in, n, P<uint64_t>(c, B_XPART), out);
-  KCHK(c, "xscan_apply_kernel");
-  HIPCHK(hipGetLastError());
-  return 0;
 }
 
 // stores above 2^40 bytes take the WIDE scan (48-bit prev offsets)
@@ -655,53 +642,62 @@ static int set_single_root(Ctx* c, uint64_t t) {
 
 // KeyIndexer::build (key_indexer.rs:98-124) as a bucketed build over the
 // pairs (kh[i], mo[i]), i < *n_dev, in file order (latest = last position);
-// *status != 0 disables it.  Scratch: B_HIST/B_HOFF/B_SKEY/B_SIDX/B_LATEST8,
-// B_PART/B_PARTEX (alloc_index).  pl->n_index / pl->idx_overflow are written.
+// *status != 0 disables it.  Scratch (alloc_index): B_HIST = the claimed
+// bucket bases [IDX_HBLOCKS][nbk], B_HOFF = the bucket fills [nbk] (zero
+// before the claims) followed by the chunk counts [GLUE_BLOCKS], B_SKEY = nbk
+// buckets of IDX_TCAP records, B_LATEST8.  pl->n_index / pl->idx_overflow are
+// written.
 static int alloc_index(Ctx* c, uint64_t n_cap, uint32_t log2_nbk) {
-  const uint64_t nh = ((uint64_t)1 << log2_nbk) * IDX_HBLOCKS + 1;
-  TRY(ensure(c, B_HIST, nh * 4));
-  TRY(ensure(c, B_HOFF, nh * 4));
-  TRY(ensure(c, B_SKEY, (n_cap + 1) * 16));
+  const uint64_t nbk = (uint64_t)1 << log2_nbk;
+  TRY(ensure(c, B_HIST, nbk * IDX_HBLOCKS * 4));
+  TRY(ensure(c, B_HOFF, (nbk + GLUE_BLOCKS) * 4));
+  TRY(ensure(c, B_SKEY, nbk * IDX_TCAP * 16));
   TRY(ensure(c, B_LATEST8, n_cap + 1));
-  TRY(ensure(c, B_PART, GLUE_BLOCKS * 4));
-  TRY(ensure(c, B_PARTEX, GLUE_BLOCKS * 4));
-  TRY(ensure_cub(c, nh));
   return 0;
+}
+static uint32_t* index_zero_words(Ctx* c, uint32_t log2_nbk, uint32_t* n) {
+  *n = 1u << log2_nbk;
+  return P<uint32_t>(c, B_HOFF);
 }
 static uint32_t index_log2_buckets(uint64_t n_est) {
   uint32_t log2_nbk = 1;  // >= 1: the bucket is the hash's top log2_nbk bits
   while (log2_nbk < 14 && ((uint64_t)IDX_BUCKET_AVG << log2_nbk) < n_est) log2_nbk++;
   return log2_nbk;
 }
-// cpart: the histogram is already in B_HIST, built by chain_finalize_kernel
-// over its chain partition (cpart = check_kernel's per-chunk core counts)
+static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
+  IdxArgs ia{};
+  ia.log2_nbk = log2_nbk;
+  ia.bbase = P<uint32_t>(c, B_HIST);
+  ia.bfill = P<uint32_t>(c, B_HOFF);
+  ia.ccount = ia.bfill + ((size_t)1 << log2_nbk);
+  ia.srec = P<u64x2>(c, B_SKEY);
+  ia.latest = P<uint8_t>(c, B_LATEST8);
+  return ia;
+}
+// cpart: the bucket ranges are already claimed by chain_finalize_kernel over
+// its chain partition (cpart = check_kernel's per-chunk core counts), and
+// child2_kernel zeroed the fills; otherwise the fills are zeroed here and
+// idx_hist_kernel claims them
 static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
                                  const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
                                  Plan* pl, const uint32_t* cpart = nullptr, uint32_t coff = 0) {
-  IdxArgs ia{};
+  IdxArgs ia = index_args(c, log2_nbk);
   ia.kh = kh;
   ia.mo = mo;
   ia.n_dev = n_dev;
   ia.status = status;
-  ia.log2_nbk = log2_nbk;
-  ia.histT = P<uint32_t>(c, B_HIST);
-  ia.hoff = P<uint32_t>(c, B_HOFF);
-  ia.srec = P<u64x2>(c, B_SKEY);
-  ia.latest = P<uint8_t>(c, B_LATEST8);
-  ia.part = P<uint32_t>(c, B_PART);
-  ia.part_ex = P<uint32_t>(c, B_PARTEX);
   ia.okey = okey;
   ia.opacked = opacked;
   ia.plan = pl;
   ia.cpart = cpart;
   ia.coff = coff;
   const uint32_t nbk = 1u << log2_nbk;
-  const int nh = (int)((uint64_t)nbk * IDX_HBLOCKS + 1);
   if (!cpart) {
+    uint32_t nz = 0;
+    HIPCHK(hipMemsetAsync(index_zero_words(c, log2_nbk, &nz), 0, (size_t)nz * 4, c->stream));
     idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
     KCHK(c, "idx_hist_kernel");
   }
-  TRY(xscan(c, ia.histT, ia.hoff, (uint64_t)nh));
   idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
   KCHK(c, "idx_scatter_kernel");
   idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
@@ -853,6 +849,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       sa.chain_g = P<uint64_t>(c, B_CHAIN_G);
       sa.counters = (const unsigned long long*)cnt;
       sa.plan = pl;
+      sa.zero = index_zero_words(c, log2_nbk, &sa.n_zero);  // child2 zeroes the index's bucket fills
       for (int r = 0; r < (rounds ? 2 : 0); r++) {  // two more prune rounds per retry
         sa.has_child = marks;
         sa.gen = mgen;
@@ -892,7 +889,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.o_ok = P<uint8_t>(c, B_O_OK);
       f.n_bad = (unsigned long long*)&pl->n_bad;
       chain_finalize_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, (1u << log2_nbk) * 4, c->stream>>>(
-          sa, f, P<uint32_t>(c, B_HIST), log2_nbk);
+          sa, f, index_args(c, log2_nbk), log2_nbk);
       KCHK(c, "chain_finalize_kernel");
       HIPCHK(hipGetLastError());
       // ---- KeyIndexer::build (bucketed; SRD_INDEX_GLOBAL=1: one global table, timing experiments) ----

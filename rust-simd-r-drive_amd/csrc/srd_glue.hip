@@ -145,70 +145,7 @@ __device__ __forceinline__ void block_prefix(const uint32_t* part, uint32_t np, 
   *total = block_sum256(t, wsum);
 }
 
-__device__ __forceinline__ uint64_t block_sum256_u64(uint64_t v, uint64_t* wsum) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
-  if (lane == 0) wsum[w] = v;
-  __syncthreads();
-  const uint64_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  __syncthreads();
-  return t;
-}
 
-// Device exclusive scan of n u32 values in two launches (replaces hipCUB's
-// lookback-state init + scan pair on the per-call path): per-block chunk sums
-// (u64), then every block derives its own prefix and scans its chunk 256
-// values at a time.  Sums are u64 (a u64 output never wraps); a u32 output
-// holds counts of one call that fit in u32 by construction.
-__global__ __launch_bounds__(256) void xscan_sum_kernel(const uint32_t* in, uint64_t n, uint64_t* part) {
-  __shared__ uint64_t wsum[4];
-  uint64_t lo, hi;
-  chunk_of(n, &lo, &hi);
-  uint64_t s = 0;
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) s += in[i];
-  const uint64_t t = block_sum256_u64(s, wsum);
-  if (threadIdx.x == 0) part[blockIdx.x] = t;
-}
-
-template <class OUT>
-__global__ __launch_bounds__(256) void xscan_apply_kernel(const uint32_t* in, uint64_t n, const uint64_t* part,
-                                                          OUT* out) {
-  __shared__ uint64_t wsum[4];
-  __shared__ uint64_t wpre[4];
-  uint64_t before = 0;
-  {
-    uint64_t b = 0;
-    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) b += i < blockIdx.x ? part[i] : 0ull;
-    before = block_sum256_u64(b, wsum);
-  }
-  uint64_t lo, hi;
-  chunk_of(n, &lo, &hi);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint64_t run = before;
-  for (uint64_t base = lo; base < hi; base += blockDim.x) {
-    const uint64_t i = base + threadIdx.x;
-    const uint64_t v = i < hi ? in[i] : 0u;
-    uint64_t x = v;  // inclusive wave scan
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wpre[w] = x;
-    __syncthreads();
-    uint64_t wb = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint64_t q = wpre[k];
-      wb += k < w ? q : 0u;
-      tot += q;
-    }
-    __syncthreads();
-    if (i < hi) out[i] = (OUT)(run + wb + x - v);
-    run += tot;
-  }
-}
 
 // exclusive scan of up to 1024 partials with one 1024-thread block
 __device__ uint64_t block_scan_partials(const uint32_t* part, uint32_t np, uint32_t* part_ex) {
@@ -336,6 +273,8 @@ struct ShapeArgs {
   const unsigned long long* counters;
   Plan* plan;
   uint32_t coff;     // chain entries before the first candidate (1 whole file, 0 span mode)
+  uint32_t* zero;    // child2_kernel zeroes [zero, zero + n_zero): the index's bucket fills and chunk counts
+  uint32_t n_zero;
 };
 
 __device__ __forceinline__ uint64_t start_node(const ShapeArgs& a, uint64_t K) {
@@ -366,6 +305,7 @@ __global__ __launch_bounds__(256) void prune_kernel(ShapeArgs a, uint32_t* marks
 }
 
 __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_zero; i += gridDim.x * blockDim.x) a.zero[i] = 0;
   const uint64_t K = *a.Kp;
   if (K > a.capK) return;
   const uint64_t start = start_node(a, K);
@@ -419,6 +359,52 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
   if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
 }
 
+// KeyIndexer::build's bucket layout (shared with chain_finalize_kernel, which
+// builds the histogram and claims the bucket ranges)
+constexpr int IDX_HBLOCKS = 256;  // histogram / scatter blocks
+static_assert(IDX_HBLOCKS == CHAIN_BLOCKS, "chain_finalize_kernel builds the index histogram per chain block");
+constexpr int IDX_TSLOTS = 4096;     // LDS open-addressing slots per bucket block (max)
+constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
+// the host picks the fewest buckets with <= IDX_BUCKET_AVG expected entries
+// each (fewer buckets, fewer range claims; a bucket of Poisson(1280) stays far
+// below IDX_TCAP, and an overflowing one sends the build to the global table)
+constexpr int IDX_BUCKET_AVG = 1280;
+constexpr uint64_t IDX_EMPTY = ~0ull;
+
+struct IdxArgs {
+  const uint64_t* kh;    // chain key hashes (o_kh)
+  const uint64_t* mo;    // chain meta offsets (o_mo)
+  const uint64_t* n_dev; // &plan->n_chain
+  const uint32_t* status;
+  uint32_t log2_nbk;
+  // Buckets of fixed capacity IDX_TCAP: bucket k owns srec[k*IDX_TCAP, ...).
+  // Each histogram block claims a range per bucket with one atomicAdd on
+  // bfill[k] (no histogram scan); bbase[b*nbk + k] = block b's first slot.
+  // bfill (nbk) is zero before the claims.
+  uint32_t* bfill;
+  uint32_t* bbase;       // [IDX_HBLOCKS * nbk]
+  u64x2* srec;           // (key, chain index) per entry, in its bucket's range
+  uint8_t* latest;       // [n] 1 = latest entry of its key
+  uint32_t* ccount;      // [GLUE_BLOCKS] latest entries per chain chunk (idx_count -> idx_emit)
+  uint64_t* okey;
+  uint64_t* opacked;
+  Plan* plan;
+  // chain_finalize_kernel's partition (its histogram's): block b's chain
+  // positions are [coff + before_b, coff + before_b + cpart[b]) (block 0
+  // from 0: the root entry); null = chunk_of over n
+  const uint32_t* cpart;
+  uint32_t coff;
+};
+
+__device__ __forceinline__ uint64_t idx_n(const IdxArgs& a) { return *a.status ? 0 : *a.n_dev; }
+
+// block b's per-bucket counts (LDS) -> claimed ranges of the buckets
+__device__ __forceinline__ void idx_claim(const IdxArgs& a, const uint32_t* hist, uint32_t nbk, uint32_t b) {
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) {
+    const uint32_t n = hist[k];
+    a.bbase[(uint64_t)b * nbk + k] = n ? atomicAdd(&a.bfill[k], n) : 0u;
+  }
+}
 // ---------------------------------------------------------------------------
 // The plan (every block decides it from the same inputs; block 0 publishes
 // it) fused with the whole per-entry stage: chain rank of every core node
@@ -445,7 +431,7 @@ __device__ __forceinline__ uint32_t idx_bucket(uint64_t key, uint32_t log2_nbk) 
   return (uint32_t)(xxh3_64_u64(key) >> (64 - log2_nbk));
 }
 
-__global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs a, FinArgs f, uint32_t* histT,
+__global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs a, FinArgs f, IdxArgs ia,
                                                                       uint32_t log2_nbk) {
   __shared__ uint32_t wsum[CHAIN_WAVES];
   __shared__ uint32_t tab[1024], mx[1024];
@@ -486,7 +472,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       pl->chain_core = total;
       pl->n_chain = st ? 0 : a.coff + total;
     }
-    histT[(uint64_t)nbk * CHAIN_BLOCKS] = 0;  // the histogram scan's total slot
   }
   if (st && !troot) return;
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
@@ -538,61 +523,29 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     }
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) histT[(uint64_t)k * CHAIN_BLOCKS + blockIdx.x] = hist[k];
+  idx_claim(ia, hist, nbk, blockIdx.x);
 }
 
 // --------------------------------------------------------------------------
 // KeyIndexer::build, bucketed
 // --------------------------------------------------------------------------
-constexpr int IDX_HBLOCKS = 256;  // histogram / scatter blocks
-static_assert(IDX_HBLOCKS == CHAIN_BLOCKS, "chain_finalize_kernel builds the index histogram per chain block");
-constexpr int IDX_TSLOTS = 4096;     // LDS open-addressing slots per bucket block (max)
-constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
-constexpr int IDX_BUCKET_AVG = 1024; // host sizes the bucket count for this average
-constexpr uint64_t IDX_EMPTY = ~0ull;
-
-struct IdxArgs {
-  const uint64_t* kh;    // chain key hashes (o_kh)
-  const uint64_t* mo;    // chain meta offsets (o_mo)
-  const uint64_t* n_dev; // &plan->n_chain
-  const uint32_t* status;
-  uint32_t log2_nbk;
-  uint32_t* histT;       // [nbk * IDX_HBLOCKS + 1]
-  uint32_t* hoff;        // exclusive scan of histT
-  u64x2* srec;           // bucket-ordered (key, chain index): one 16-B store per entry
-  uint8_t* latest;       // [n] 1 = latest entry of its key
-  uint32_t* part;
-  uint32_t* part_ex;
-  uint64_t* okey;
-  uint64_t* opacked;
-  Plan* plan;
-  // chain_finalize_kernel's partition (its histogram's): block b's chain
-  // positions are [coff + before_b, coff + before_b + cpart[b]) (block 0
-  // from 0: the root entry); null = chunk_of over n
-  const uint32_t* cpart;
-  uint32_t coff;
-};
-
-__device__ __forceinline__ uint64_t idx_n(const IdxArgs& a) { return *a.status ? 0 : *a.n_dev; }
-
 __global__ __launch_bounds__(256) void idx_hist_kernel(IdxArgs a) {
   extern __shared__ uint32_t lds_u32[];
   const uint32_t nbk = 1u << a.log2_nbk;
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.histT[(uint64_t)nbk * IDX_HBLOCKS] = 0;  // scan -> total
   __syncthreads();
   uint64_t lo, hi;
   chunk_of(idx_n(a), &lo, &hi);
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x)
     atomicAdd(&lds_u32[xxh3_64_u64(a.kh[c]) >> (64 - a.log2_nbk)], 1u);
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) a.histT[(uint64_t)k * IDX_HBLOCKS + blockIdx.x] = lds_u32[k];
+  idx_claim(a, lds_u32, nbk, blockIdx.x);
 }
 
 __global__ __launch_bounds__(256) void idx_scatter_kernel(IdxArgs a) {
   extern __shared__ uint32_t lds_u32[];
   const uint32_t nbk = 1u << a.log2_nbk;
-  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = a.hoff[(uint64_t)k * IDX_HBLOCKS + blockIdx.x];
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = a.bbase[(uint64_t)blockIdx.x * nbk + k];
   __syncthreads();
   uint64_t lo, hi;
   if (a.cpart) {
@@ -608,8 +561,9 @@ __global__ __launch_bounds__(256) void idx_scatter_kernel(IdxArgs a) {
   }
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) {
     const uint64_t k = a.kh[c];
-    const uint32_t pos = atomicAdd(&lds_u32[xxh3_64_u64(k) >> (64 - a.log2_nbk)], 1u);
-    a.srec[pos] = u64x2{k, c};
+    const uint32_t bk = (uint32_t)(xxh3_64_u64(k) >> (64 - a.log2_nbk));
+    const uint32_t pos = atomicAdd(&lds_u32[bk], 1u);
+    if (pos < IDX_TCAP) a.srec[(uint64_t)bk * IDX_TCAP + pos] = u64x2{k, c};  // else: idx_dedup flags the bucket
   }
 }
 
@@ -620,14 +574,14 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
   __shared__ uint32_t special;
   if (*a.status) return;
   const uint32_t k = blockIdx.x;
-  const uint64_t lo = a.hoff[(uint64_t)k * IDX_HBLOCKS], hi = a.hoff[(uint64_t)(k + 1) * IDX_HBLOCKS];
-  if (hi == lo) return;
-  if (hi - lo > IDX_TCAP) {  // skewed bucket: the host reruns the global-table build
-    if (threadIdx.x == 0) a.plan->idx_overflow = 1;
-    // keep count/emit in bounds: this bucket contributes nothing
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.latest[a.srec[i][1]] = 0;
+  const uint32_t fill = a.bfill[k];
+  if (fill == 0) return;
+  if (fill > IDX_TCAP) {  // skewed bucket (entries beyond the capacity were dropped): the host
+    if (threadIdx.x == 0) a.plan->idx_overflow = 1;  // reruns the global-table build
     return;
   }
+  const uint64_t lo = (uint64_t)k * IDX_TCAP, hi = lo + fill;
+
   uint32_t slots = 64;
   while (slots < 2 * (hi - lo)) slots <<= 1;  // load <= 1/2
   const uint32_t M = slots - 1;
@@ -661,7 +615,6 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
     a.latest[c] = best == c + 1;
   }
 }
-
 __global__ __launch_bounds__(256) void idx_count_kernel(IdxArgs a) {
   __shared__ uint32_t wsum[4];
   uint64_t lo, hi;
@@ -669,14 +622,15 @@ __global__ __launch_bounds__(256) void idx_count_kernel(IdxArgs a) {
   uint32_t cnt = 0;
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) cnt += a.latest[c];
   const uint32_t t = block_sum256(cnt, wsum);
-  if (threadIdx.x == 0) a.part[blockIdx.x] = t;
+  if (threadIdx.x == 0) a.ccount[blockIdx.x] = t;
 }
+
 
 
 __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
   __shared__ uint32_t wsum[4];
   uint64_t before = 0, total = 0;
-  block_prefix(a.part, GLUE_BLOCKS, wsum, &before, &total);
+  block_prefix(a.ccount, GLUE_BLOCKS, wsum, &before, &total);
   if (blockIdx.x == 0 && threadIdx.x == 0) a.plan->n_index = total;
   uint64_t lo, hi;
   chunk_of(idx_n(a), &lo, &hi);
