@@ -314,7 +314,10 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   }
   int r = upload_tables();
   if (r) { delete c; return r; }
-  for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+  // timing events (srd_ctx_timings) with a device-scope release: a default
+  // event's system-scope release (an L2 write-back) put ~5 us into the
+  // timeline at each record (four per call)
+  for (auto& e : c->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventReleaseToDevice));
   HIPCHK(hipHostMalloc((void**)&c->h_plan, sizeof(Plan), hipHostMallocDefault));
   c->stage_workers = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   int ncu = 0;

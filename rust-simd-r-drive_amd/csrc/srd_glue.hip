@@ -431,11 +431,152 @@ __device__ __forceinline__ uint32_t idx_bucket(uint64_t key, uint32_t log2_nbk) 
   return (uint32_t)(xxh3_64_u64(key) >> (64 - log2_nbk));
 }
 
+// block ranks of R rounds of flags at once (one LDS exchange): round r's
+// flags rank after every flag of rounds < r; wsum is LDS[R * NW]
+template <int NW, int R>
+__device__ __forceinline__ uint32_t block_rank_rounds(const bool* f, uint32_t* wsum, uint32_t* rank) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t pre[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint64_t bal = __ballot(f[r]);
+    pre[r] = (uint32_t)__popcll(bal & lt);
+    if (lane == 0) wsum[r * NW + w] = (uint32_t)__popcll(bal);
+  }
+  __syncthreads();
+  uint32_t acc = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    uint32_t off = 0, t = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      const uint32_t v = wsum[r * NW + i];
+      off += i < w ? v : 0u;
+      t += v;
+    }
+    rank[r] = acc + off + pre[r];
+    acc += t;
+  }
+  __syncthreads();
+  return acc;
+}
+
+// chain entries per thread per pass of chain_finalize_kernel: the per-entry
+// work is a chain of four dependent loads (flag -> parent/slot -> records ->
+// parent record, tile values, table words); the R entries' loads of each level
+// are issued together
+constexpr int FIN_R = 2;  // 3 and 4 spill at 128 VGPRs
+
+// one chain entry's inputs (finalize_core's, loaded level by level)
+struct FinIn {
+  uint64_t mo, p;
+  uint32_t crc_st, fl, sxv;   // record: r1[0], r1[3], r1[1]
+  uint32_t pfl, psuf;         // parent record: r1[3], r1[2] (pfl = 3 << F_SUF_SHIFT: no parent record)
+  u32x4 t0, t1;               // per-tile values of the start tile k0 and the metadata tile k1
+};
+// the tables finalize_in reads, in LDS
+struct FinLds {
+  uint32_t tab[1024];         // CRC slice-by-4
+  uint32_t m16k[1024];        // v -> v * x^16384
+  uint32_t winit[64], zero_crc[64];
+  uint32_t invpow[4097];
+};
+
+__device__ __forceinline__ uint32_t mul16k_lds(const uint32_t* m16k, uint32_t v) {
+  return m16k[v & 0xff] ^ m16k[256 + ((v >> 8) & 0xff)] ^ m16k[512 + ((v >> 16) & 0xff)] ^ m16k[768 + (v >> 24)];
+}
+
+// crc_raw of bytes [floor64(m), m) (tail_crc) with the CRC table in LDS
+__device__ __forceinline__ uint32_t tail_crc_lds(const uint8_t* file, uint64_t m, const uint32_t* tab) {
+  const uint64_t L = m & ~63ull;
+  const uint32_t r = (uint32_t)(m - L);
+  uint32_t s = 0, q = 0;
+  for (; q + 4 <= r; q += 4) {
+    s ^= *(const uint32_t*)(file + L + q);
+    s = tab[768 + (s & 0xff)] ^ tab[512 + ((s >> 8) & 0xff)] ^ tab[256 + ((s >> 16) & 0xff)] ^ tab[s >> 24];
+  }
+  for (; q < r; q++) s = tab[(s ^ file[L + q]) & 0xff] ^ (s >> 8);
+  return s;
+}
+
+// finalize_core (srd_kernels.hip) for a candidate chain entry from its
+// preloaded inputs: the same outputs, bit for bit; true = slow_one needed
+__device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const FinIn& e, const FinLds& t) {
+  const uint32_t* m16k = t.m16k;
+  const uint64_t mo = e.mo, p = e.p;
+  const uint32_t fl = e.fl;
+  const bool tomb = fl & F_TOMB;
+  const uint64_t start = tomb ? p : p + prepad64(p);
+  const uint64_t k0 = start / TILE, k1 = mo / TILE;
+  uint32_t suf = 0, sxm = 0, tail = 0, pieces = 0;
+  if (fl & F_SXM) {
+    sxm = (fl & F_SXM_LO) ? mul16k_lds(m16k, e.sxv) ^ e.t1[2] : e.sxv;
+    pieces |= 2;
+  }
+  if (fl & F_TAIL) pieces |= 4;
+  const uint32_t kind = (e.pfl >> F_SUF_SHIFT) & 3;
+  if (kind == 0) { suf = (e.pfl & F_SUF_LO) ? mul16k_lds(m16k, e.psuf) ^ e.t0[2] : e.psuf; pieces |= 1; }
+  else if (kind == 1) { suf = mul16k_lds(m16k, e.t0[0]) ^ e.t0[2]; pieces |= 1; }
+  else if (kind == 2) { suf = mul16k_lds(m16k, e.t0[1]) ^ e.t0[2]; pieces |= 1; }
+  if (!(pieces & 1)) {  // the start line's suffix from the per-tile values (line 0, 1 or 32)
+    const uint32_t j = (uint32_t)((start % TILE) / 64);
+    if (j == 0) { suf = mul16k_lds(m16k, e.t0[0]) ^ e.t0[2]; pieces |= 1; }
+    else if (j == 1) { suf = mul16k_lds(m16k, e.t0[1]) ^ e.t0[2]; pieces |= 1; }
+    else if (j == 32) { suf = e.t0[2]; pieces |= 1; }
+  }
+  if (!(pieces & 2)) {
+    const uint32_t j = (uint32_t)((mo % TILE) / 64);
+    if (j == 0) { sxm = mul16k_lds(m16k, e.t1[0]) ^ e.t1[2]; pieces |= 2; }
+    else if (j == 1) { sxm = mul16k_lds(m16k, e.t1[1]) ^ e.t1[2]; pieces |= 2; }
+    else if (j == 32) { sxm = e.t1[2]; pieces |= 2; }
+  }
+  const uint64_t len = mo - start;
+  a.o_start[c] = start;  // o_mo / o_kh / o_prev / o_crc_st: stored by the caller
+  a.o_len[c] = len;
+  if (a.no_crc) { a.o_crc[c] = 0; a.o_ok[c] = 0; return false; }
+  uint32_t crc;
+  if (tomb) {
+    crc = 0xD202EF8Du;  // CRC32(b"\0"): the tombstone byte is 0 by the rule
+  } else {
+    if (!(pieces & 4)) tail = tail_crc_lds(a.file, mo, t.tab);
+    const bool need_long = len >= 64;
+    const bool many_tiles = need_long && k1 > k0 + 1 + LONG_TILES;
+    if (need_long && !((pieces & 1) && (pieces & 2) && !many_tiles)) {
+      a.o_pieces[c] = pieces;
+      a.o_suf[c] = suf;
+      a.o_sxm[c] = sxm;
+      a.o_tail[c] = tail;
+      return true;
+    }
+    if (!need_long) {
+      crc = tail ^ t.zero_crc[len];
+    } else {  // crc_from_pieces
+      uint32_t acc = suf ^ t.winit[(start % TILE) / 64], y;
+      if (k0 == k1) {
+        y = acc ^ sxm;
+      } else {
+        // one tile step: v * x^32768 = (v * x^16384) * x^16384, two table multiplies
+        for (uint64_t k = k0 + 1; k < k1; k++)
+          acc = mul16k_lds(m16k, mul16k_lds(m16k, acc)) ^ tile_T(a.tile, k);
+        y = mul16k_lds(m16k, mul16k_lds(m16k, acc)) ^ (mul16k_lds(m16k, e.t1[0]) ^ e.t1[2]) ^ sxm;
+      }
+      crc = ~(mulp(t.invpow[(k1 + 1) * TILE - mo], y) ^ tail);
+    }
+  }
+  a.o_crc[c] = crc;
+  a.o_ok[c] = crc == e.crc_st;
+  if (crc != e.crc_st) atomicAdd(a.n_bad, 1ull);
+  return false;
+}
+
 __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs a, FinArgs f, IdxArgs ia,
                                                                       uint32_t log2_nbk) {
-  __shared__ uint32_t wsum[CHAIN_WAVES];
-  __shared__ uint32_t tab[1024], mx[1024];
-  __shared__ uint32_t slowq[CHAIN_THREADS];
+  __shared__ uint32_t wsum[CHAIN_WAVES * FIN_R];
+  __shared__ FinLds lt;
+  __shared__ uint32_t mx[1024];
+  uint32_t* const tab = lt.tab;
+  __shared__ uint32_t slowq[CHAIN_THREADS * FIN_R];
   __shared__ uint32_t nslow;
   extern __shared__ uint32_t hist[];
   const uint64_t K = *a.Kp;
@@ -478,42 +619,95 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
     tab[i] = g_tabs.tab[i >> 8][i & 255];
     mx[i] = (&g_tabs.mx64[0][0])[i];
+    lt.m16k[i] = (&g_tabs.m16k[0][0])[i];
+  }
+  for (uint32_t i = threadIdx.x; i < 4097; i += blockDim.x) lt.invpow[i] = g_tabs.invpow[i];
+  if (threadIdx.x < 64) {
+    lt.winit[threadIdx.x] = g_tabs.winit[threadIdx.x];
+    lt.zero_crc[threadIdx.x] = g_tabs.zero_crc[threadIdx.x];
   }
   if (threadIdx.x == 0) nslow = 0;
   __syncthreads();
-  // the root entry (whole file: chain entry 0, no candidate record)
-  if (blockIdx.x == 0 && a.coff) {
-    if (threadIdx.x == 0) {
-      uint64_t kh;
-      nslow = finalize_core(f, 0, NO_REC, -1, root_t, &kh) ? 1u : 0u;
-      atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
-    }
-    __syncthreads();
-    if (nslow && threadIdx.x < 64) slow_one(f, 0, tab, mx);
-    __syncthreads();
-    if (threadIdx.x == 0) nslow = 0;
-    __syncthreads();
+  // the root entry (whole file: chain entry 0, no candidate record); its
+  // CRC's slow path, if any, runs after the candidates
+  bool root_slow = false;
+  if (blockIdx.x == 0 && a.coff && threadIdx.x == 0) {
+    uint64_t kh;
+    root_slow = finalize_core(f, 0, NO_REC, -1, root_t, &kh);
+    atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
   }
   if (!troot) {
     uint64_t lo, hi;
     chunk_of(K, &lo, &hi);
     uint64_t run = a.coff + before;
-    for (uint64_t base = lo; base < hi; base += CHAIN_THREADS) {
-      const uint64_t g = base + threadIdx.x;
-      const bool fl = g < hi && a.flag[g];
-      uint32_t tot;
-      const uint32_t r = block_rank_n<CHAIN_WAVES>(fl, wsum, &tot);
-      if (fl) {
-        const uint64_t c = run + r;
-        const int64_t p = a.d_par[g];
-        uint64_t kh;
-        if (finalize_core(f, c, a.d_slot[g], p >= 0 ? (int64_t)a.d_slot[p] : -1, root_t, &kh))
-          slowq[atomicAdd(&nslow, 1u)] = (uint32_t)(c - run);
-        atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
+    const u32x4* t4 = (const u32x4*)f.tile;
+    for (uint64_t base = lo; base < hi; base += CHAIN_THREADS * FIN_R) {
+      bool fl[FIN_R];
+      uint64_t g[FIN_R], gi[FIN_R];
+      int64_t par[FIN_R];
+      FinIn e[FIN_R];
+      // level 1-2: core flag, parent, record slot (indices of idle lanes: 0)
+#pragma unroll
+      for (int r = 0; r < FIN_R; r++) {
+        g[r] = base + (uint64_t)r * CHAIN_THREADS + threadIdx.x;
+        fl[r] = g[r] < hi && a.flag[g[r] < hi ? g[r] : lo];
+        if (!fl[r]) g[r] = 0;
+      }
+#pragma unroll
+      for (int r = 0; r < FIN_R; r++) {
+        par[r] = a.d_par[g[r]];
+        gi[r] = a.d_slot[g[r]];
+      }
+      // level 3: the records and the parent's record slot
+      uint64_t pgi[FIN_R], kh[FIN_R];
+#pragma unroll
+      for (int r = 0; r < FIN_R; r++) {
+        pgi[r] = a.d_slot[par[r] >= 0 ? (uint64_t)par[r] : 0];
+        e[r].mo = f.c_m[gi[r]];
+        const u32x4 r0 = f.c_rec[2 * gi[r]], r1 = f.c_rec[2 * gi[r] + 1];
+        e[r].p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+        kh[r] = (uint64_t)r0[2] | ((uint64_t)r0[3] << 32);
+        e[r].crc_st = r1[0];
+        e[r].sxv = r1[1];
+        e[r].fl = r1[3];
+      }
+      uint32_t rank[FIN_R];
+      const uint32_t tot = block_rank_rounds<CHAIN_WAVES, FIN_R>(fl, wsum, rank);
+      // level 4: the parent's record, the tile values and table words.  k0
+      // (the entry's start tile) is resident: start >= p >= the span's lower
+      // tail in span mode.  A root-linked candidate (par == PAR_ROOT) has no
+      // parent record: its suffix comes from the per-tile values (start 0)
+#pragma unroll
+      for (int r = 0; r < FIN_R; r++) {
+        const u32x4 pr1 = f.c_rec[2 * (par[r] >= 0 ? pgi[r] : 0) + 1];
+        e[r].pfl = par[r] >= 0 ? pr1[3] : (3u << F_SUF_SHIFT);
+        e[r].psuf = pr1[2];
+        // idle lanes read the last tile's values (resident in span mode too)
+        const uint64_t mo = fl[r] ? e[r].mo : f.flen - 1;
+        const uint64_t st0 = !fl[r] ? mo : (e[r].fl & F_TOMB) ? e[r].p : e[r].p + prepad64(e[r].p);
+        e[r].t0 = t4[st0 / TILE];
+        e[r].t1 = t4[mo / TILE];
+      }
+      // the record's own outputs and the index histogram while those loads fly
+#pragma unroll
+      for (int r = 0; r < FIN_R; r++) {
+        if (!fl[r]) continue;
+        const uint64_t c = run + rank[r];
+        f.o_mo[c] = e[r].mo;
+        f.o_kh[c] = kh[r];
+        f.o_prev[c] = e[r].p;
+        f.o_crc_st[c] = e[r].crc_st;
+        atomicAdd(&hist[idx_bucket(kh[r], log2_nbk)], 1u);
+      }
+#pragma unroll
+      for (int r = 0; r < FIN_R; r++) {
+        if (!fl[r]) continue;
+        const uint64_t c = run + rank[r];
+        if (finalize_in(f, c, e[r], lt)) slowq[atomicAdd(&nslow, 1u)] = (uint32_t)(c - run);
       }
       __syncthreads();
       const uint32_t ns = nslow;
-      if (ns) {  // this round's slow entries, one wave each
+      if (ns) {  // this pass's slow entries, one wave each
         for (uint32_t q = threadIdx.x >> 6; q < ns; q += CHAIN_WAVES) slow_one(f, run + slowq[q], tab, mx);
         __syncthreads();
         if (threadIdx.x == 0) nslow = 0;
@@ -522,6 +716,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       run += tot;
     }
   }
+  if (__syncthreads_or(root_slow) && threadIdx.x < 64) slow_one(f, 0, tab, mx);
   __syncthreads();
   idx_claim(ia, hist, nbk, blockIdx.x);
 }
