@@ -677,13 +677,12 @@ static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
   ia.latest = P<uint8_t>(c, B_LATEST8);
   return ia;
 }
-// cpart: the bucket ranges are already claimed by chain_finalize_kernel over
-// its chain partition (cpart = check_kernel's per-chunk core counts), and
-// child2_kernel zeroed the fills; otherwise the fills are zeroed here and
-// idx_hist_kernel claims them
+// fused: chain_finalize_kernel already claimed the bucket ranges and wrote
+// the records (child2_kernel zeroed the fills); otherwise the fills are
+// zeroed here, idx_hist_kernel claims the ranges and idx_scatter_kernel fills them
 static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
                                  const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
-                                 Plan* pl, const uint32_t* cpart = nullptr, uint32_t coff = 0) {
+                                 Plan* pl, bool fused = false) {
   IdxArgs ia = index_args(c, log2_nbk);
   ia.kh = kh;
   ia.mo = mo;
@@ -692,17 +691,15 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   ia.okey = okey;
   ia.opacked = opacked;
   ia.plan = pl;
-  ia.cpart = cpart;
-  ia.coff = coff;
   const uint32_t nbk = 1u << log2_nbk;
-  if (!cpart) {
+  if (!fused) {
     uint32_t nz = 0;
     HIPCHK(hipMemsetAsync(index_zero_words(c, log2_nbk, &nz), 0, (size_t)nz * 4, c->stream));
     idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
     KCHK(c, "idx_hist_kernel");
+    idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+    KCHK(c, "idx_scatter_kernel");
   }
-  idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
-  KCHK(c, "idx_scatter_kernel");
   idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
   KCHK(c, "idx_dedup_kernel");
   idx_count_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
@@ -898,7 +895,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       // ---- KeyIndexer::build (bucketed; SRD_INDEX_GLOBAL=1: one global table, timing experiments) ----
       if (!index_global_env())
         TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
-                                  P<uint64_t>(c, B_IPACKED), pl, sa.part, coff));
+                                  P<uint64_t>(c, B_IPACKED), pl, true));
       HIPCHK(hipEventRecord(c->ev[3], c->stream));  // end of the device work (srd_ctx_timings)
       c->ev3_recorded = true;
       HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));

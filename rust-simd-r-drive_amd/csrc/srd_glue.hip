@@ -108,8 +108,8 @@ __device__ __forceinline__ uint32_t block_sum_n(uint32_t v, uint32_t* wsum) {
   __syncthreads();
   return t;
 }
-// chunked grid of the shape check and the fused chain finalize (the index
-// histogram / scatter partition too: IDX_HBLOCKS == CHAIN_BLOCKS)
+// chunked grid of the shape check and the fused chain finalize (which also
+// builds the index histogram and scatter of its chain positions)
 constexpr int CHAIN_BLOCKS = 256;
 constexpr int CHAIN_THREADS = 1024;
 constexpr int CHAIN_WAVES = CHAIN_THREADS / 64;
@@ -309,9 +309,25 @@ __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
   const uint64_t K = *a.Kp;
   if (K > a.capK) return;
   const uint64_t start = start_node(a, K);
-  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x) {
-    const int64_t p = a.d_par[g];
-    if (p >= 0 && is_core(a, g, start)) a.childof[p] = ((uint64_t)a.gen << 32) | g;
+  // CR nodes per thread per pass: loads first (no store in between)
+  constexpr int CR = 4;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g0 < K; g0 += CR * stride) {
+    int64_t par[CR];
+    uint32_t hc[CR];
+#pragma unroll
+    for (int r = 0; r < CR; r++) {
+      const uint64_t g = g0 + r * stride, gg = g < K ? g : g0;
+      par[r] = a.d_par[gg];
+      hc[r] = a.has_child[gg];
+    }
+#pragma unroll
+    for (int r = 0; r < CR; r++) {
+      const uint64_t g = g0 + r * stride;
+      if (g >= K) break;
+      const int64_t p = par[r];
+      if (p >= 0 && (g == start || hc[r] == a.gen)) a.childof[p] = ((uint64_t)a.gen << 32) | g;  // is_core(g)
+    }
   }
 }
 
@@ -325,33 +341,58 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
   chunk_of(K, &lo, &hi);
   uint32_t cnt = 0;
   bool fail = false;
-  for (uint64_t g = lo + threadIdx.x; g < hi; g += blockDim.x) {
-    const bool core = is_core(a, g, start);
-    a.flag[g] = core;
-    if (!core) continue;
-    cnt++;
-    const int64_t p = a.d_par[g];
-    if (p == PAR_ROOT) {
-      atomicAdd(&a.plan->nroot, 1u);
-      const u32x4 r0 = a.c_rec[2 * a.d_slot[g]];
-      a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-    } else if (p < 0 || !is_core(a, (uint64_t)p, start)) {
-      fail = true;  // dangling: the chain through g is broken (only the start node can get here)
-      atomicAdd(&a.plan->why[0], 1u);
-      const uint32_t w = atomicAdd(&a.plan->ndbg, 1u);
-      if (w < 8) {
-        const u32x4 r0 = a.c_rec[2 * a.d_slot[g]];
-        a.plan->dbg[2 * w] = a.d_m[g];
-        a.plan->dbg[2 * w + 1] = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-        a.plan->dbg_g[w] = g;
-      }
-    } else if (a.childof[p] != (tag | g)) {
-      fail = true;  // branch: another core node claims the same parent
-      atomicAdd(&a.plan->why[1], 1u);
+  // CR nodes per thread per pass, their loads issued level by level: the
+  // node's own words (marks, parent, child claim), then its parent's
+  constexpr int CR = 4;
+  for (uint64_t base = lo; base < hi; base += CR * CHAIN_THREADS) {
+    uint64_t g[CR], cg[CR], cp[CR];
+    int64_t par[CR], pp[CR];
+    uint32_t hc[CR], hp[CR];
+#pragma unroll
+    for (int r = 0; r < CR; r++) {
+      g[r] = base + (uint64_t)r * CHAIN_THREADS + threadIdx.x;
+      const uint64_t gg = g[r] < hi ? g[r] : lo;
+      hc[r] = a.has_child[gg];
+      par[r] = a.d_par[gg];
+      cg[r] = a.childof[gg];
     }
-    if (g != start && (a.childof[g] & ~0xffffffffull) != tag) {  // core node without a core child
-      fail = true;
-      atomicAdd(&a.plan->why[2], 1u);
+#pragma unroll
+    for (int r = 0; r < CR; r++) {
+      const uint64_t q = par[r] >= 0 ? (uint64_t)par[r] : lo;
+      hp[r] = a.has_child[q];
+      pp[r] = a.d_par[q];
+      cp[r] = a.childof[q];
+    }
+#pragma unroll
+    for (int r = 0; r < CR; r++) {
+      if (g[r] >= hi) break;
+      const int64_t p = par[r];
+      const bool core = g[r] == start || (hc[r] == a.gen && (p >= 0 || p == PAR_ROOT));  // is_core(g)
+      a.flag[g[r]] = core;
+      if (!core) continue;
+      cnt++;
+      if (p == PAR_ROOT) {
+        atomicAdd(&a.plan->nroot, 1u);
+        const u32x4 r0 = a.c_rec[2 * a.d_slot[g[r]]];
+        a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+      } else if (p < 0 || !((uint64_t)p == start || (hp[r] == a.gen && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
+        fail = true;  // dangling: the chain through g is broken (only the start node can get here)
+        atomicAdd(&a.plan->why[0], 1u);
+        const uint32_t w = atomicAdd(&a.plan->ndbg, 1u);
+        if (w < 8) {
+          const u32x4 r0 = a.c_rec[2 * a.d_slot[g[r]]];
+          a.plan->dbg[2 * w] = a.d_m[g[r]];
+          a.plan->dbg[2 * w + 1] = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+          a.plan->dbg_g[w] = g[r];
+        }
+      } else if (cp[r] != (tag | g[r])) {
+        fail = true;  // branch: another core node claims the same parent
+        atomicAdd(&a.plan->why[1], 1u);
+      }
+      if (g[r] != start && (cg[r] & ~0xffffffffull) != tag) {  // core node without a core child
+        fail = true;
+        atomicAdd(&a.plan->why[2], 1u);
+      }
     }
   }
   const uint32_t tot = block_sum_n<CHAIN_WAVES>(cnt, wsum);
@@ -360,9 +401,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
 }
 
 // KeyIndexer::build's bucket layout (shared with chain_finalize_kernel, which
-// builds the histogram and claims the bucket ranges)
-constexpr int IDX_HBLOCKS = 256;  // histogram / scatter blocks
-static_assert(IDX_HBLOCKS == CHAIN_BLOCKS, "chain_finalize_kernel builds the index histogram per chain block");
+// builds the histogram, claims the bucket ranges and scatters its chain
+// positions itself)
+constexpr int IDX_HBLOCKS = 256;  // histogram / scatter blocks of the stand-alone build
 constexpr int IDX_TSLOTS = 4096;     // LDS open-addressing slots per bucket block (max)
 constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
 // the host picks the fewest buckets with <= IDX_BUCKET_AVG expected entries
@@ -389,11 +430,6 @@ struct IdxArgs {
   uint64_t* okey;
   uint64_t* opacked;
   Plan* plan;
-  // chain_finalize_kernel's partition (its histogram's): block b's chain
-  // positions are [coff + before_b, coff + before_b + cpart[b]) (block 0
-  // from 0: the root entry); null = chunk_of over n
-  const uint32_t* cpart;
-  uint32_t coff;
 };
 
 __device__ __forceinline__ uint64_t idx_n(const IdxArgs& a) { return *a.status ? 0 : *a.n_dev; }
@@ -411,9 +447,9 @@ __device__ __forceinline__ void idx_claim(const IdxArgs& a, const uint32_t* hist
 // (block prefix of check_kernel's per-chunk core counts + a block rank), the
 // outputs and the CRC of each chain entry (finalize_core), the entries whose
 // CRC needs a wave (long entries, missing pieces: slow_one, run by this
-// block's 16 waves after each round), and the index histogram of the
-// bucketed KeyIndexer::build over this block's chain positions.  Replaces
-// the plan/scatter, finalize, slow and histogram launches.
+// block's 16 waves after each round), and the index histogram and scatter
+// of the bucketed KeyIndexer::build over this block's chain positions.
+// Replaces the plan/scatter, finalize, slow, histogram and scatter launches.
 template <int NW>
 __device__ __forceinline__ void block_prefix_n(const uint32_t* part, uint32_t np, uint32_t* wsum, uint64_t* before,
                                                uint64_t* total) {
@@ -636,10 +672,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     root_slow = finalize_core(f, 0, NO_REC, -1, root_t, &kh);
     atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
   }
+  uint64_t run = a.coff + before;  // this block's next chain position
   if (!troot) {
     uint64_t lo, hi;
     chunk_of(K, &lo, &hi);
-    uint64_t run = a.coff + before;
     const u32x4* t4 = (const u32x4*)f.tile;
     for (uint64_t base = lo; base < hi; base += CHAIN_THREADS * FIN_R) {
       bool fl[FIN_R];
@@ -718,7 +754,34 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   }
   if (__syncthreads_or(root_slow) && threadIdx.x < 64) slow_one(f, 0, tab, mx);
   __syncthreads();
-  idx_claim(ia, hist, nbk, blockIdx.x);
+  // KeyIndexer::build's scatter for this block's chain positions [clo, run)
+  // (block 0 from 0: the root entry): claim the block's range of every
+  // bucket, then one (key, position) record per entry into it; the keys are
+  // re-read from o_kh (written above by this block: L2-hot)
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) {
+    const uint32_t n = hist[k];
+    hist[k] = n ? atomicAdd(&ia.bfill[k], n) : 0u;
+  }
+  __syncthreads();
+  const uint64_t n_chain = troot ? 1 : a.coff + total;
+  const uint64_t clo = min(n_chain, blockIdx.x ? a.coff + before : 0), chi = min(n_chain, run);
+  constexpr int SR = 4;  // keys loaded together per pass
+  for (uint64_t base = clo; base < chi; base += SR * CHAIN_THREADS) {
+    uint64_t k[SR];
+#pragma unroll
+    for (int r = 0; r < SR; r++) {
+      const uint64_t c = base + (uint64_t)r * CHAIN_THREADS + threadIdx.x;
+      k[r] = f.o_kh[c < chi ? c : clo];
+    }
+#pragma unroll
+    for (int r = 0; r < SR; r++) {
+      const uint64_t c = base + (uint64_t)r * CHAIN_THREADS + threadIdx.x;
+      if (c >= chi) break;
+      const uint32_t bk = idx_bucket(k[r], log2_nbk);
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      if (pos < IDX_TCAP) ia.srec[(uint64_t)bk * IDX_TCAP + pos] = u64x2{k[r], c};  // else: idx_dedup flags the bucket
+    }
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -743,17 +806,7 @@ __global__ __launch_bounds__(256) void idx_scatter_kernel(IdxArgs a) {
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = a.bbase[(uint64_t)blockIdx.x * nbk + k];
   __syncthreads();
   uint64_t lo, hi;
-  if (a.cpart) {
-    __shared__ uint32_t wsum[4];
-    uint64_t before, total;
-    block_prefix(a.cpart, IDX_HBLOCKS, wsum, &before, &total);
-    if (*a.status) return;
-    const uint64_t n = *a.n_dev;  // 1 when file_len itself is a root tail (the chain is that entry)
-    lo = min(n, blockIdx.x ? a.coff + before : 0);
-    hi = min(n, a.coff + before + a.cpart[blockIdx.x]);
-  } else {
-    chunk_of(idx_n(a), &lo, &hi);
-  }
+  chunk_of(idx_n(a), &lo, &hi);
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) {
     const uint64_t k = a.kh[c];
     const uint32_t bk = (uint32_t)(xxh3_64_u64(k) >> (64 - a.log2_nbk));
@@ -776,17 +829,28 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
     return;
   }
   const uint64_t lo = (uint64_t)k * IDX_TCAP, hi = lo + fill;
-
+  // each thread's <= IDX_TCAP / 512 records (loaded before the table is
+  // cleared) and their slots stay in registers between the insert and the
+  // lookup pass
+  constexpr int DR = IDX_TCAP / 512;
+  u64x2 rec[DR];
+  uint32_t slot[DR];
+#pragma unroll
+  for (int r = 0; r < DR; r++) {
+    const uint64_t i = lo + (uint64_t)r * 512 + threadIdx.x;
+    rec[r] = a.srec[i < hi ? i : lo];
+  }
   uint32_t slots = 64;
   while (slots < 2 * (hi - lo)) slots <<= 1;  // load <= 1/2
   const uint32_t M = slots - 1;
   for (uint32_t i = threadIdx.x; i < slots; i += blockDim.x) { keys[i] = IDX_EMPTY; vals[i] = 0; }
   if (threadIdx.x == 0) special = 0;
   __syncthreads();
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const u64x2 rec = a.srec[i];
-    const uint64_t key = rec[0];
-    const uint32_t v = (uint32_t)rec[1] + 1;
+#pragma unroll
+  for (int r = 0; r < DR; r++) {
+    if (lo + (uint64_t)r * 512 + threadIdx.x >= hi) break;
+    const uint64_t key = rec[r][0];
+    const uint32_t v = (uint32_t)rec[r][1] + 1;
     if (key == IDX_EMPTY) { atomicMax(&special, v); continue; }
     uint32_t s = (uint32_t)xxh3_64_u64(key) & M;
     while (true) {
@@ -794,19 +858,14 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
       if (old == IDX_EMPTY || old == key) { atomicMax(&vals[s], v); break; }
       s = (s + 1) & M;
     }
+    slot[r] = s;
   }
   __syncthreads();
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const u64x2 rec = a.srec[i];
-    const uint64_t key = rec[0];
-    const uint32_t c = (uint32_t)rec[1];
-    uint32_t best;
-    if (key == IDX_EMPTY) best = special;
-    else {
-      uint32_t s = (uint32_t)xxh3_64_u64(key) & M;
-      while (keys[s] != key) s = (s + 1) & M;
-      best = vals[s];
-    }
+#pragma unroll
+  for (int r = 0; r < DR; r++) {
+    if (lo + (uint64_t)r * 512 + threadIdx.x >= hi) break;
+    const uint32_t c = (uint32_t)rec[r][1];
+    const uint32_t best = rec[r][0] == IDX_EMPTY ? special : vals[slot[r]];
     a.latest[c] = best == c + 1;
   }
 }
@@ -830,15 +889,27 @@ __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
   uint64_t lo, hi;
   chunk_of(idx_n(a), &lo, &hi);
   uint64_t run = before;
-  for (uint64_t base = lo; base < hi; base += blockDim.x) {
-    const uint64_t c = base + threadIdx.x;
-    const bool f = c < hi && a.latest[c];
-    uint32_t tot;
-    const uint32_t r = block_rank256(f, wsum, &tot);
-    if (f) {
-      const uint64_t key = a.kh[c];
-      a.okey[run + r] = key;
-      a.opacked[run + r] = ((key >> 48) << 48) | (a.mo[c] & 0xFFFFFFFFFFFFull);  // key_indexer.rs:79-85
+  // ER rounds of 256 positions per pass: their flags and keys are loaded
+  // together and ranked with one LDS exchange
+  constexpr int ER = 4;
+  __shared__ uint32_t wsum_r[4 * ER];
+  for (uint64_t base = lo; base < hi; base += ER * 256) {
+    bool f[ER];
+    uint64_t key[ER], mo[ER];
+#pragma unroll
+    for (int r = 0; r < ER; r++) {
+      const uint64_t c = base + (uint64_t)r * 256 + threadIdx.x, cc = c < hi ? c : lo;
+      f[r] = c < hi && a.latest[cc];
+      key[r] = a.kh[cc];
+      mo[r] = a.mo[cc];
+    }
+    uint32_t rank[ER];
+    const uint32_t tot = block_rank_rounds<4, ER>(f, wsum_r, rank);
+#pragma unroll
+    for (int r = 0; r < ER; r++) {
+      if (!f[r]) continue;
+      a.okey[run + rank[r]] = key[r];
+      a.opacked[run + rank[r]] = ((key[r] >> 48) << 48) | (mo[r] & 0xFFFFFFFFFFFFull);  // key_indexer.rs:79-85
     }
     run += tot;
   }
