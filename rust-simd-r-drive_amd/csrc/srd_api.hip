@@ -179,13 +179,12 @@ int upload_tables() {
       for (int l = 0; l < 32; l++)  // x^(512*(31-l)) = lw[l + 32]
         t.nib[((pos * 16 + nb) << 5) + l] = mulp(g_host_tabs.lw[l + 32], (uint32_t)nb << (4 * pos));
   {
-    const uint32_t x16k = host_xpow8(g_host_tabs, 2048), x128 = host_xpow8(g_host_tabs, 16),
-                   x256 = host_xpow8(g_host_tabs, 32);
+    const uint32_t x16k = host_xpow8(g_host_tabs, 2048);
     for (int tb = 0; tb < 4; tb++)
       for (int b = 0; b < 256; b++) {
         t.m16k[tb][b] = mulp(x16k, (uint32_t)b << (8 * tb));
-        t.m128[tb][b] = mulp(x128, (uint32_t)b << (8 * tb));
-        t.m256[tb][b] = mulp(x256, (uint32_t)b << (8 * tb));
+        for (int q = 0; q < 3; q++)
+          t.last[q][tb][b] = mulp(host_xpow8(g_host_tabs, 4 + 16 * (3 - q)), (uint32_t)b << (8 * tb));
       }
   }
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_tabs), &t, sizeof t));

@@ -62,8 +62,7 @@ struct DevTables {
   uint32_t invpow[4097];
   uint32_t nib[8 * 16 * 32];       // half-tile lane-weight nibble tables
   uint32_t m16k[4][256];           // v -> v * x^16384 byte tables
-  uint32_t m128[4][256];
-  uint32_t m256[4][256];
+  uint32_t last[3][4][256];        // chain q's last slice-by-4 step, shifted: v -> v * x^(32 + 128 (3 - q))
   uint32_t xtile[65];              // X^e, X = x^32768 (one tile), e = 0..64
   uint32_t xt64[65];               // X^(64 q), q = 0..64 (with xtile: X^n for n < 4160 in one multiply)
   uint32_t mx64[4][256];           // v -> v * X^64 byte tables (the long-entry Horner step)
@@ -187,8 +186,10 @@ constexpr int SCAN_WAVES_V2 = 16;
 struct ScanLds {
   uint32_t tab[4 * 256 * 32];      // 128 KiB slice-by-4 tables, conflict-free (layout: tab_lookup)
   uint32_t nib[8 * 16 * 32];       // 16 KiB: c -> c * x^(512*(31 - l%32)), bank = l%32
-  uint32_t m128[4 * 256];          // v -> v * x^128  (join 16-byte chains)
-  uint32_t m256[4 * 256];          // v -> v * x^256  (join 32-byte halves)
+  // the last slice-by-4 step of 16-byte chain q (q < 3) with the chain's
+  // join shift folded in: byte i of s -> (b << 8i) * x^(32 + 128 (3 - q)),
+  // so the line CRC is the XOR of the four chains' last steps (crc_line4)
+  uint32_t last[3 * 4 * 256];      // 12 KiB, not replicated
   uint32_t win[SCAN_WAVES_V2][24];
 };
 
@@ -220,22 +221,31 @@ __device__ __forceinline__ uint32_t mulfix(uint32_t v, const uint32_t* __restric
   return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
 }
 // Same CRC as crc_line1 with 4 independent 16-byte chains (4 dependent LDS
-// round trips instead of 16), joined by c = (a*x^128 ^ b)*x^256 ^ (c*x^128 ^ d).
+// round trips instead of 16): raw(line) = a x^384 ^ b x^256 ^ c x^128 ^ d for
+// the chains' raw CRCs a..d, and chain q's last step looks its bytes up in
+// tables that already carry the x^(128 (3 - q)) shift (ScanLds::last), so the
+// joins cost no lookups of their own.
 __device__ __forceinline__ uint32_t crc_line4(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
   constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
   uint32_t s[4] = {d[0], d[4], d[8], d[12]};
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < 3; j++) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const uint32_t t3 = tab_lookup(L, s[q], R[3], SEL0), t2 = tab_lookup(L, s[q], R[2], SEL1);
       const uint32_t t1 = tab_lookup(L, s[q], R[1], SEL2), t0 = tab_lookup(L, s[q], R[0], SEL3);
-      s[q] = xor3(xor3(t3, t2, j < 3 ? d[4 * q + (j < 3 ? j + 1 : 3)] : 0u), t1, t0);
+      s[q] = xor3(xor3(t3, t2, d[4 * q + j + 1]), t1, t0);
     }
   }
-  const uint32_t ab = mulfix(s[0], L.m128) ^ s[1];
-  const uint32_t cd = mulfix(s[2], L.m128) ^ s[3];
-  return mulfix(ab, L.m256) ^ cd;
+  uint32_t v[4];
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    const uint32_t* m = L.last + 1024 * q;
+    v[q] = xor3(m[s[q] & 0xff], m[256 + ((s[q] >> 8) & 0xff)], m[512 + ((s[q] >> 16) & 0xff)]) ^ m[768 + (s[q] >> 24)];
+  }
+  v[3] = xor3(tab_lookup(L, s[3], R[3], SEL0), tab_lookup(L, s[3], R[2], SEL1), tab_lookup(L, s[3], R[1], SEL2)) ^
+         tab_lookup(L, s[3], R[0], SEL3);
+  return xor3(v[0], v[1], v[2]) ^ v[3];
 }
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -295,10 +305,7 @@ __device__ __forceinline__ void load_crc_lds(ScanLds& lds) {
     lds.tab[i] = g_tabs.tab[t][b];
   }
   for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) lds.nib[i] = g_tabs.nib[i];
-  for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) {
-    lds.m128[i] = (&g_tabs.m128[0][0])[i];
-    lds.m256[i] = (&g_tabs.m256[0][0])[i];
-  }
+  for (int i = threadIdx.x; i < 3 * 4 * 256; i += blockDim.x) lds.last[i] = (&g_tabs.last[0][0][0])[i];
   __syncthreads();
 }
 // lane l's slice-by-4 lookup bases (tab_lookup)
