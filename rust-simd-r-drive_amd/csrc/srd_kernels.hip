@@ -463,10 +463,18 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     //      zero bytes, the last one possibly the next line's first ----
     uint64_t slow;
     if (!WIDE) {
-      u16x2 zmin = __builtin_bit_cast(u16x2, d[0]);
+      // a tree, not a chain: back-to-back dependent v_pk_min_u16 need an
+      // s_nop between them on gfx950 (15 per tile as a chain)
+      u16x2 zm[8];
 #pragma unroll
-      for (int i = 1; i < 16; i++) zmin = __builtin_elementwise_min(zmin, __builtin_bit_cast(u16x2, d[i]));
-      slow = __ballot(zmin.x == 0 || zmin.y == 0);
+      for (int i = 0; i < 8; i++)
+        zm[i] = __builtin_elementwise_min(__builtin_bit_cast(u16x2, d[i]), __builtin_bit_cast(u16x2, d[i + 8]));
+#pragma unroll
+      for (int w = 4; w > 0; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; i++) zm[i] = __builtin_elementwise_min(zm[i], zm[i + w]);
+      const uint32_t z = __builtin_bit_cast(uint32_t, zm[0]);
+      slow = __ballot(((z - 0x00010001u) & ~z & 0x80008000u) != 0);  // a zero halfword (exact)
     } else {
       uint32_t nx = __shfl_down(d[0], 1);
       if (lane == 63) {
@@ -486,8 +494,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     // that stores and uses a register last written by a pending VMEM load
     // makes the compiler flush vmcnt to 0 in the loop preheader, draining the
     // prefetch ring on every flagged tile.
-#pragma unroll
-    for (int j = 0; j < 16; j++) asm volatile("" : "+v"(d[j]));
+    // (one statement: an asm per register put an s_nop hazard guard after each)
+    asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7]),
+                 "+v"(d[8]), "+v"(d[9]), "+v"(d[10]), "+v"(d[11]), "+v"(d[12]), "+v"(d[13]), "+v"(d[14]), "+v"(d[15]));
 
     while (slow) {
       const int f = __builtin_ctzll(slow);
