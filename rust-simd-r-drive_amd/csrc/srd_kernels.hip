@@ -31,6 +31,7 @@
 
 namespace srd {
 
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -183,15 +184,20 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // ((pos*16+nib)*64 + l): every lane its own bank, conflict-free) and one
 // 24-dword window per wave for the cooperative candidate check.
 constexpr int SCAN_WAVES_V2 = 16;
-struct ScanLds {
-  uint32_t tab[4 * 256 * 32];      // 128 KiB slice-by-4 tables, conflict-free (layout: tab_lookup)
-  uint32_t nib[8 * 16 * 32];       // 16 KiB: c -> c * x^(512*(31 - l%32)), bank = l%32
+struct alignas(2048) ScanLds {
   // the last slice-by-4 step of 16-byte chain q (q < 3) with the chain's
   // join shift folded in: byte i of s -> (b << 8i) * x^(32 + 128 (3 - q)),
   // so the line CRC is the XOR of the four chains' last steps (crc_line4)
-  uint32_t last[3 * 4 * 256];      // 12 KiB, not replicated
+  uint32_t last[3 * 4 * 256];      // 12 KiB, not replicated; first, so its
+                                   // lookups carry the table base in the ds_read offset field (no base VGPRs)
+  uint32_t tab[4 * 256 * 32];      // 128 KiB slice-by-4 tables, conflict-free (layout: tab_lookup)
+  uint32_t nib[8 * 16 * 32];       // 16 KiB: c -> c * x^(512*(31 - l%32)), bank = l%32
   uint32_t win[SCAN_WAVES_V2][24];
+  // the epilogue's block reduction
+  uint64_t s_root[SCAN_WAVES_V2], s_ovf[SCAN_WAVES_V2];
+  uint32_t s_last;
 };
+static_assert(offsetof(ScanLds, nib) % 2048 == 0, "lane_weight_or ORs nibble bits 7-10 into the table base");
 
 // Slice-by-4 with v_perm addressing.  LDS layout of the 4 tables: word
 // b*64 + (t&1)*32 + c (+ 16384*(t>>1)), c = lane%32 -> byte address
@@ -282,6 +288,32 @@ __device__ __forceinline__ uint32_t lane_weight(uint32_t c, const uint32_t* __re
   }
   return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6] ^ v[7]);
 }
+// v_writelane_b32 (the LLVM intrinsic; this clang has no builtin for it):
+// lane `lane` (uniform) of `old` takes `val`
+__device__ int srd_llvm_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t writelane_u32(uint32_t val, int lane, uint32_t old) {
+  return (uint32_t)srd_llvm_writelane((int)val, lane, (int)old);
+}
+// LDS byte offsets (address space 3) for explicit address arithmetic
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint32_t lds_ld(uint32_t off) {
+  return *(const __attribute__((address_space(3))) uint32_t*)(uintptr_t)off;
+}
+// lane_weight for the scan, whose nib table sits at a 2 KiB-aligned LDS
+// offset: the nibble's address bits (7-10) are OR-ed into the lane's base
+// (one v_and_or_b32 after the shift instead of and + add)
+__device__ __forceinline__ uint32_t lane_weight_or(uint32_t c, uint32_t lbase) {
+  uint32_t v[8];
+#pragma unroll
+  for (int pos = 0; pos < 8; pos++) {
+    const int sh = 4 * pos - 7;  // nibble pos -> address bits 7-10
+    const uint32_t x = sh < 0 ? c << (-sh) : c >> sh;
+    v[pos] = lds_ld(((x & 0x780u) | lbase) + pos * 2048);
+  }
+  return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6] ^ v[7]);
+}
 __device__ __forceinline__ uint32_t mul16k(uint32_t v, const uint32_t* __restrict__ m) {
   return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
 }
@@ -335,6 +367,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   const uint8_t* __restrict__ file = a.file;
   const uint64_t flen = a.flen;
   uint32_t* win = lds.win[wv];
+  const uint32_t nib_lane = lds_off(lds.nib) + 4u * (lane & 31);  // 2 KiB-aligned table base + the lane's bank
 
   // balanced contiguous tile range per wave (whole spans)
   const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES_V2;
@@ -435,28 +468,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       for (int j = 0; j < 16; j++) d[j] = mask_past_end32(d[j], 64u * lane + 4 * j, remu);
     }
 
-    // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
-    const uint32_t c = crc_line4(d, lds, R);
-    const uint32_t hx = half_suffix_xor(lane_weight(c, lds.nib, lane), lane);
-    // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
-    // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
-    // tiles.  Every store of this loop is an UNCONDITIONAL buffer store whose
-    // unused lanes carry an out-of-range offset (dropped by the hardware): a
-    // store under a branch makes the count of memory ops between a prefetch
-    // load and its wait path-dependent, and the compiler then waits for the
-    // store's completion too (measured: ~10 % of the kernel).
-    {
-      const int t = (int)(k & 15);
-      const uint32_t v0 = __builtin_amdgcn_readlane(hx, 0), v1 = __builtin_amdgcn_readlane(hx, 1),
-                     v2 = __builtin_amdgcn_readlane(hx, 32);
-      tacc = lane == 4 * t ? v0 : lane == 4 * t + 1 ? v1 : lane == 4 * t + 2 ? v2 : tacc;
-      const bool flush = t == 15 || k + 1 == k1;  // uniform
-      const uint64_t g = k & ~15ull;
-      const uint32_t lo = (uint32_t)(max(g, k0) - g) * 4;
-      const uint32_t off = (flush && (uint32_t)lane >= lo && lane < 4 * t + 4) ? 4u * lane : OOB_OFF;
-      __builtin_amdgcn_raw_buffer_store_b32(tacc, out_rsrc(a.tile + 4 * g, 256), off, 0, 0);
-    }
-
+    // the filter first: its VALU fills the CRC's LDS waits and the suffix
+    // XOR's DPP hazard slots (same basic block)
     // ---- filter, level 1: any aligned zero halfword in the lane's line
     //      (packed 16-bit min over the 16 dwords: 1 VALU per dword); level 2
     //      (exact, per position) in the slow path.  WIDE: any two adjacent
@@ -490,6 +503,32 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       }
       slow = __ballot(hz != 0);
     }
+    // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
+    const uint32_t c = crc_line4(d, lds, R);
+    const uint32_t hx = half_suffix_xor(lane_weight_or(c, nib_lane), lane);
+    // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
+    // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
+    // tiles.  Every store of this loop is an UNCONDITIONAL buffer store whose
+    // unused lanes carry an out-of-range offset (dropped by the hardware): a
+    // store under a branch makes the count of memory ops between a prefetch
+    // load and its wait path-dependent, and the compiler then waits for the
+    // store's completion too (measured: ~10 % of the kernel).
+    {
+      const int t = (int)(k & 15);
+      const uint32_t v0 = __builtin_amdgcn_readlane(hx, 0), v1 = __builtin_amdgcn_readlane(hx, 1),
+                     v2 = __builtin_amdgcn_readlane(hx, 32);
+      tacc = writelane_u32(v0, 4 * t, tacc);
+      tacc = writelane_u32(v1, 4 * t + 1, tacc);
+      tacc = writelane_u32(v2, 4 * t + 2, tacc);
+      const bool flush = t == 15 || k + 1 == k1;  // uniform
+      const uint64_t g = k & ~15ull;
+      const uint32_t lo = (uint32_t)(max(g, k0) - g) * 4;
+      // branch-free (a uniform branch here split the tile's basic block)
+      const uint32_t lo2 = flush ? lo : 0u, n2 = flush ? 4u * t + 4u - lo : 0u;
+      const uint32_t off = (uint32_t)lane - lo2 < n2 ? 4u * lane : OOB_OFF;
+      __builtin_amdgcn_raw_buffer_store_b32(tacc, out_rsrc(a.tile + 4 * g, 256), off, 0, 0);
+    }
+
     // Re-define d by an empty asm once its loads have been consumed: a loop
     // that stores and uses a register last written by a pending VMEM load
     // makes the compiler flush vmcnt to 0 in the loop preheader, draining the
@@ -578,17 +617,17 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
                                 ((js & 63) < 32 ? F_SUF_LO : 0u);
             if (r - flushed < 64) {
               // record r -> lane r - flushed of the record registers
-              const bool mine = lane == (int)(r - flushed);
-              rq[0] = mine ? (uint32_t)m : rq[0];
-              rq[1] = mine ? (uint32_t)(m >> 32) : rq[1];
-              rq[2] = mine ? hm : rq[2];
-              rq[3] = mine ? hs : rq[3];
-              rq[4] = mine ? fl : rq[4];
-              rq[5] = mine ? s2 : rq[5];
-              rq[6] = mine ? s3 : rq[6];
-              rq[7] = mine ? s0 : rq[7];
-              rq[8] = mine ? s1 : rq[8];
-              rq[9] = mine ? s4 : rq[9];
+              const int li = (int)(r - flushed);
+              rq[0] = writelane_u32((uint32_t)m, li, rq[0]);
+              rq[1] = writelane_u32((uint32_t)(m >> 32), li, rq[1]);
+              rq[2] = writelane_u32(hm, li, rq[2]);
+              rq[3] = writelane_u32(hs, li, rq[3]);
+              rq[4] = writelane_u32(fl, li, rq[4]);
+              rq[5] = writelane_u32(s2, li, rq[5]);
+              rq[6] = writelane_u32(s3, li, rq[6]);
+              rq[7] = writelane_u32(s0, li, rq[7]);
+              rq[8] = writelane_u32(s1, li, rq[8]);
+              rq[9] = writelane_u32(s4, li, rq[9]);
               rvalid |= 1ull << (r - flushed);
             } else if (lane == 0) {
               const uint64_t gi = w * a.wcap + r;
@@ -740,7 +779,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     a.wave_root[w] = rootmax;  // wave-uniform already
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __shared__ uint32_t s_last;
+  uint32_t& s_last = lds.s_last;
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -754,7 +793,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   __syncthreads();
   // exclusive prefix of the wave counts: thread t owns waves [t*q, (t+1)*q)
   uint64_t* s_part = (uint64_t*)lds.tab;  // the CRC tables are dead now: 1024 partials
-  __shared__ uint64_t s_root[SCAN_WAVES_V2], s_ovf[SCAN_WAVES_V2];
+  uint64_t* s_root = lds.s_root;
+  uint64_t* s_ovf = lds.s_ovf;
   const uint32_t T = blockDim.x, t = threadIdx.x;
   const uint64_t q = (total_waves + T - 1) / T;
   uint64_t sum = 0, rmax = 0, o = 0;
