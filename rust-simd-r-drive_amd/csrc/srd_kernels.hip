@@ -324,9 +324,13 @@ __device__ __forceinline__ uint32_t half_suffix_xor(uint32_t v, int lane) {
   v ^= dpp<DPP_ROW_SHL + 2>(v);
   v ^= dpp<DPP_ROW_SHL + 4>(v);
   v ^= dpp<DPP_ROW_SHL + 8>(v);
-  const uint32_t t1 = __builtin_amdgcn_readlane(v, 16), t3 = __builtin_amdgcn_readlane(v, 48);
-  const int row = lane >> 4;
-  return v ^ (row == 0 ? t1 : row == 2 ? t3 : 0u);
+  // rows 0 and 2 add the totals of rows 1 and 3 (held by lanes 16, 48):
+  // row_newbcast:0 on rows 1 and 3 only ({0, T1, 0, T3}), then
+  // v_permlane16_swap against zero moves rows 1 / 3 down to rows 0 / 2
+  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150, 0xA, 0xF, false);
+  const auto sw = __builtin_amdgcn_permlane16_swap(t, 0u, false, false);
+  (void)lane;
+  return v ^ sw[1];
 }
 
 // the LDS tables of the line-CRC machinery (crc_line*, lane_weight); ends
