@@ -407,6 +407,10 @@ def main():
         dist.init_process_group(os.environ.get("SRD_DIST_BACKEND", "nccl"), init_method="env://")
     torch.cuda.set_device(local)
     ctx = S.Context(local)
+    # the roofline's kernel time: HIP events around each scan launch on the
+    # library's stream, inside the timed region (the product default is no
+    # events: each record costs ~10 us of a call)
+    ctx.set_timing(S.TIMING_SCAN)
 
     if args.config == "c5":
         return bench_c5(args, ctx, local)

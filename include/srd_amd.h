@@ -77,9 +77,20 @@ void srd_ctx_destroy(srd_ctx *ctx);
 /* The HIP stream the context launches on (hipStream_t as void*). */
 void *srd_ctx_stream(srd_ctx *ctx);
 const char *srd_last_error(void);
+/* HIP-event timing of the validate calls on ctx (each event record costs
+ * ~10 us of a call's wall time): SRD_TIMING_NONE (the default),
+ * SRD_TIMING_SCAN (the streaming scan's launches: bench.py's roofline),
+ * SRD_TIMING_CALL (+ the device span of the whole call).  Not part of the
+ * reference interface. */
+#define SRD_TIMING_NONE 0
+#define SRD_TIMING_SCAN 1
+#define SRD_TIMING_CALL 2
+int srd_ctx_set_timing(srd_ctx *ctx, int level);
+
 /* HIP-event timings of the last srd_validate_index(_device) call on ctx,
  * measured on the context stream: summed duration of the streaming scan
- * kernel launches (ms), their count, and the device span of the whole call. */
+ * kernel launches (ms), their count, and the device span of the whole call
+ * (0 unless the timing level includes them). */
 int srd_ctx_timings(srd_ctx *ctx, double *scan_ms, int *scan_launches,
                     double *total_ms);
 

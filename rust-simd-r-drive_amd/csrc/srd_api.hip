@@ -77,6 +77,10 @@ struct Ctx {
   Buf file;
   // timing (HIP events on `stream`)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // srd_ctx_set_timing: 0 none (default), 1 scan kernel (ev[0], ev[1]), 2 +
+  // whole call (ev[2], ev[3]); each event record costs ~11 us of the C2
+  // call's wall time (4 events: 1.104 ms, 2: 1.081, none: 1.070)
+  int timing = SRD_TIMING_NONE;
   double scan_ms = 0, total_ms = 0;
   int scan_launches = 0;
   // sync-free optimistic pass
@@ -579,21 +583,21 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     TRY(scan_wave_args(c, &a));
     if (n_spans) {
       unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
-      HIPCHK(hipEventRecord(c->ev[0], c->stream));
+      if (c->timing >= SRD_TIMING_SCAN) HIPCHK(hipEventRecord(c->ev[0], c->stream));
       if (full)
         launch_scan<true>(g, a, c->stream);
       else
         launch_scan<false>(g, a, c->stream);
       KCHK(c, "scan_kernel");
       HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(c->ev[1], c->stream));
+      if (c->timing >= SRD_TIMING_SCAN) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     }
     size_t tb = c->bufs[B_CUB_TMP].n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_SPAN_COUNT),
                                             P<uint64_t>(c, B_SPAN_BASE), (int)(n_spans + 1), c->stream));
     HIPCHK(hipMemcpyAsync(K, P<uint64_t>(c, B_SPAN_BASE) + n_spans, 8, hipMemcpyDeviceToHost, c->stream));
     TRY(read_counters(c, h));
-    if (n_spans) {
+    if (n_spans && c->timing >= SRD_TIMING_SCAN) {
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
       c->scan_ms += ms;
@@ -795,11 +799,11 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.n_zero_words = (uint32_t)(sizeof(Plan) / 4);
     a.sentinel = nullptr;
     TRY(scan_wave_args(c, &a));
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    if (c->timing >= SRD_TIMING_SCAN) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     launch_scan<false>(g, a, c->stream);
     KCHK(c, "scan_kernel");
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    if (c->timing >= SRD_TIMING_SCAN) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     Link2Args l{};
     l.file = d_file;
     l.flen = flen;
@@ -895,8 +899,10 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       if (!index_global_env())
         TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
                                   P<uint64_t>(c, B_IPACKED), pl, true));
-      HIPCHK(hipEventRecord(c->ev[3], c->stream));  // end of the device work (srd_ctx_timings)
-      c->ev3_recorded = true;
+      if (c->timing >= SRD_TIMING_CALL) {
+        HIPCHK(hipEventRecord(c->ev[3], c->stream));  // end of the device work (srd_ctx_timings)
+        c->ev3_recorded = true;
+      }
       HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(spin_sync(c->stream));
       hp = *c->h_plan;
@@ -911,7 +917,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
           fprintf(stderr, "  dangling g=%lu m=%lu p=%lu\n", (unsigned long)hp.dbg_g[w], (unsigned long)hp.dbg[2 * w],
                   (unsigned long)hp.dbg[2 * w + 1]);
       }
-      if (!timed) {
+      if (!timed && c->timing >= SRD_TIMING_SCAN) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
         c->scan_ms += ms;
@@ -959,16 +965,24 @@ extern "C" int srd_validate_index_device(srd_ctx* c, const uint8_t* d_file, uint
   HIPCHK(hipSetDevice(c->device));
   c->scan_ms = 0;
   c->scan_launches = 0;
+  c->total_ms = 0;
   c->ev3_recorded = false;
-  HIPCHK(hipEventRecord(c->ev[2], c->stream));
+  const bool tcall = c->timing >= SRD_TIMING_CALL;
+  if (tcall) HIPCHK(hipEventRecord(c->ev[2], c->stream));
   int r = validate_device_impl(c, d_file, flen, flags, out);
-  if (!(r == 0 && out->mode == SRD_MODE_OPTIMISTIC && c->ev3_recorded)) {
-    HIPCHK(hipEventRecord(c->ev[3], c->stream));
-    HIPCHK(hipEventSynchronize(c->ev[3]));
+  if (!(r == 0 && out->mode == SRD_MODE_OPTIMISTIC && (c->ev3_recorded || !tcall))) {
+    if (tcall) {
+      HIPCHK(hipEventRecord(c->ev[3], c->stream));
+      HIPCHK(hipEventSynchronize(c->ev[3]));
+    } else {
+      HIPCHK(hipStreamSynchronize(c->stream));
+    }
   }
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
-  c->total_ms = ms;
+  if (tcall) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+    c->total_ms = ms;
+  }
   return r;
 }
 
@@ -988,7 +1002,9 @@ extern "C" int srd_validate_span_device(srd_ctx* c, const uint8_t* d_span, uint6
   c->scan_launches = 0;
   memset(out, 0, sizeof *out);
   out->file_len = hi;
-  HIPCHK(hipEventRecord(c->ev[2], c->stream));
+  c->total_ms = 0;
+  const bool tcall = c->timing >= SRD_TIMING_CALL;
+  if (tcall) HIPCHK(hipEventRecord(c->ev[2], c->stream));
   bool done = false;
   int r = optimistic_pass(c, d_span, span_off, lo, hi, flags, out, &done);
   if (!r && !done) {
@@ -998,11 +1014,15 @@ extern "C" int srd_validate_span_device(srd_ctx* c, const uint8_t* d_span, uint6
     out->n_index = 0;
     out->n_crc_bad = 0;
   }
-  HIPCHK(hipEventRecord(c->ev[3], c->stream));
-  HIPCHK(hipEventSynchronize(c->ev[3]));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
-  c->total_ms = ms;
+  if (tcall) {
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[3]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+    c->total_ms = ms;
+  } else {
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
   return r;
 }
 
@@ -1078,6 +1098,12 @@ extern "C" int srd_index_build_device(srd_ctx* c, const uint64_t* d_pairs, uint6
   KCHK(c, "deinterleave_kernel");
   HIPCHK(hipGetLastError());
   return index_build_sep(c, P<uint64_t>(c, B_MKEY), P<uint64_t>(c, B_MVAL), n, d_out_keys, d_out_packed, n_index);
+}
+
+extern "C" int srd_ctx_set_timing(srd_ctx* c, int level) {
+  if (!c || level < SRD_TIMING_NONE || level > SRD_TIMING_CALL) { set_err("bad argument"); return SRD_ERR_ARG; }
+  c->timing = level;
+  return 0;
 }
 
 extern "C" int srd_ctx_timings(srd_ctx* c, double* scan_ms, int* scan_launches, double* total_ms) {

@@ -33,6 +33,7 @@ SRD_FLAG_NO_CRC = 2
 SRD_FLAG_STAGE_PAGEABLE = 4  # host input: one pageable hipMemcpy (measurement baseline)
 SRD_FLAG_STAGE_REGISTER = 8  # host input: hipHostRegister the range (default: pinned bounce buffers)
 STAGE_MODES = {0: "pinned input", 1: "registered mapping", 2: "bounce buffers", 3: "pageable copy"}
+TIMING_NONE, TIMING_SCAN, TIMING_CALL = 0, 1, 2  # srd_ctx_set_timing levels
 SRD_MODE_OPTIMISTIC = 0
 SRD_MODE_FULL = 1
 SRD_MODE_SPAN_UNPROVEN = 3
@@ -45,6 +46,7 @@ OFFSET_MASK = (1 << 48) - 1
 # symbols include/srd_amd.h declares
 EXPORTS = [
     "srd_ctx_create", "srd_ctx_destroy", "srd_ctx_stream", "srd_last_error", "srd_ctx_timings",
+    "srd_ctx_set_timing",
     "srd_validate_index_device", "srd_validate_index", "srd_result_free",
     "srd_recover_valid_chain", "srd_key_indexer_build", "srd_crc32_batch",
     "srd_crc32_batch_device", "srd_xxh3_64_batch", "srd_xxh3_64_batch_device",
@@ -100,6 +102,7 @@ def lib():
         L.srd_ctx_stream.restype = vp
         L.srd_last_error.restype = C.c_char_p
         L.srd_ctx_timings.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double)]
+        L.srd_ctx_set_timing.argtypes = [vp, C.c_int]
         L.srd_validate_index_device.argtypes = [vp, vp, u64, u32, C.POINTER(DeviceResult)]
         L.srd_validate_index.argtypes = [vp, vp, u64, u32, C.POINTER(DeviceResult)]
         L.srd_result_free.argtypes = [C.POINTER(DeviceResult)]
@@ -176,6 +179,10 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_timing(self, level: int):
+        """HIP-event timing level: TIMING_NONE (default), TIMING_SCAN, TIMING_CALL."""
+        _check(lib().srd_ctx_set_timing(self.h, level))
 
     def timings(self):
         """(scan_ms, scan_launches, total_ms) of the last validate call (HIP events)."""

@@ -1,5 +1,6 @@
 """A/B timing of scan-kernel variants in ONE process (timing tool only).
-usage: python tools/ab_scan.py lib1.so lib2.so ...   (interleaved rounds)"""
+usage: python tools/ab_scan.py lib1.so lib2.so[@level] ...   (interleaved rounds;
+@level = srd_ctx_set_timing level, default 2: scan + whole-call events)"""
 import ctypes as C, json, os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rust-simd-r-drive_amd"))
 import torch
@@ -8,12 +9,16 @@ import srd_amd as S
 libs = sys.argv[1:]
 handles = []
 for p in libs:
-    L = C.CDLL(os.path.abspath(p))
+    path, _, lvl = p.partition("@")
+    L = C.CDLL(os.path.abspath(path))
     L.srd_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     L.srd_validate_index_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(S.DeviceResult)]
     L.srd_ctx_timings.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double)]
     h = C.c_void_p()
     assert L.srd_ctx_create(0, C.byref(h)) == 0
+    if hasattr(L, "srd_ctx_set_timing"):
+        L.srd_ctx_set_timing.argtypes = [C.c_void_p, C.c_int]
+        assert L.srd_ctx_set_timing(h, int(lvl or 2)) == 0
     handles.append((L, h))
 ctx = S.Context(0)
 c3 = os.environ.get("CONFIG") == "c3"  # C3: 10M Zipf-sized entries
@@ -42,7 +47,7 @@ for rnd in range(int(os.environ.get('ROUNDS', 12))):
             res[p].append(a.value / max(k.value, 1))
             tot[p].append(b.value)
             wall[p].append(wl)
-out = {os.path.basename(p): {"scan_ms_min": round(min(v), 4), "scan_ms_med": round(sorted(v)[len(v) // 2], 4),
+out = {os.path.basename(p.partition("@")[0]) + (("@" + p.partition("@")[2]) if "@" in p else ""): {"scan_ms_min": round(min(v), 4), "scan_ms_med": round(sorted(v)[len(v) // 2], 4),
                              "total_ms_med": round(sorted(tot[p])[len(v) // 2], 4),
                              "wall_ms_med": round(sorted(wall[p])[len(v) // 2], 4),
                              "wall_ms_min": round(min(wall[p]), 4)} for p, v in res.items()}
