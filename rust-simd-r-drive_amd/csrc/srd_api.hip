@@ -818,7 +818,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.wcap = wcap;
     l.c_m = a.c_m;
     l.c_rec = a.c_rec;
-    l.d_m = P<uint64_t>(c, B_DM);
     l.d_par = P<int64_t>(c, B_DPAR);
     l.d_slot = P<uint64_t>(c, B_DSLOT);
     l.has_child = P<uint32_t>(c, B_HASCHILD);
@@ -841,7 +840,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       sa.capK = capK;
       sa.Kp = a.k_total;
       sa.coff = coff;
-      sa.d_m = l.d_m;
+      sa.c_m = l.c_m;
       sa.d_par = l.d_par;
       sa.d_slot = l.d_slot;
       sa.c_rec = l.c_rec;

@@ -179,7 +179,6 @@ struct Link2Args {
   uint64_t wcap;               // record slots per scan wave
   const uint64_t* c_m;
   u32x4* c_rec;  // tombstone flags are set in place
-  uint64_t* d_m;
   int64_t* d_par;
   uint64_t* d_slot;
   uint32_t* has_child;
@@ -248,7 +247,6 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
         par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
       }
     }
-    a.d_m[g] = m;
     a.d_par[g] = par;
     a.d_slot[g] = gi;
     if (par >= 0 && (uint64_t)par < a.capK) a.has_child[par] = a.gen;
@@ -260,7 +258,7 @@ struct ShapeArgs {
   uint64_t flen, capK;
   uint32_t gen;
   const uint64_t* Kp;  // span_base + n_spans
-  const uint64_t* d_m;
+  const uint64_t* c_m;  // the records' metadata offsets (slot d_slot[g])
   const int64_t* d_par;
   const uint64_t* d_slot;
   const u32x4* c_rec;
@@ -278,7 +276,7 @@ struct ShapeArgs {
 };
 
 __device__ __forceinline__ uint64_t start_node(const ShapeArgs& a, uint64_t K) {
-  return (K && a.d_m[K - 1] == a.flen - 20) ? K - 1 : NO_NODE;
+  return (K && a.c_m[a.d_slot[K - 1]] == a.flen - 20) ? K - 1 : NO_NODE;
 }
 
 // Core nodes of the current round: the start node, or a node some node of
@@ -381,7 +379,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
         const uint32_t w = atomicAdd(&a.plan->ndbg, 1u);
         if (w < 8) {
           const u32x4 r0 = a.c_rec[2 * a.d_slot[g[r]]];
-          a.plan->dbg[2 * w] = a.d_m[g[r]];
+          a.plan->dbg[2 * w] = a.c_m[a.d_slot[g[r]]];
           a.plan->dbg[2 * w + 1] = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
           a.plan->dbg_g[w] = g[r];
         }
