@@ -261,20 +261,6 @@ constexpr int DPP_WAVE_SHL1 = 0x130;  // lane i <- lane i+1 (0 past the end)
 constexpr int DPP_WAVE_SHR1 = 0x138;  // lane i <- lane i-1
 constexpr int DPP_ROW_SHL = 0x100;    // + n: lane i <- lane i+n inside a row of 16
 
-// XOR of u over lanes >= lane (64-lane suffix scan: DPP inside rows,
-// readlane for the row totals)
-__device__ __forceinline__ uint32_t suffix_xor(uint32_t v, int lane) {
-  v ^= dpp<DPP_ROW_SHL + 1>(v);
-  v ^= dpp<DPP_ROW_SHL + 2>(v);
-  v ^= dpp<DPP_ROW_SHL + 4>(v);
-  v ^= dpp<DPP_ROW_SHL + 8>(v);
-  const uint32_t t1 = __builtin_amdgcn_readlane(v, 16), t2 = __builtin_amdgcn_readlane(v, 32),
-                 t3 = __builtin_amdgcn_readlane(v, 48);
-  const int row = lane >> 4;
-  const uint32_t add = row == 0 ? (t1 ^ t2 ^ t3) : row == 1 ? (t2 ^ t3) : row == 2 ? t3 : 0u;
-  return v ^ add;
-}
-
 // c * x^(512*(31 - lane%32)) via 8 nibble lookups: the lane weight relative
 // to the end of the lane's HALF of the tile (lanes >= 32: relative to the
 // tile end, i.e. final; lanes < 32: relative to line 31, corrected on use).

@@ -320,3 +320,32 @@ def test_index_build_device_hot_key(ctx):
         want[k] = ((k >> 48) << 48) | (64 * i + 7)
     got = dict(zip(ok[:n].cpu().numpy().view(np.uint64).tolist(), op[:n].cpu().numpy().view(np.uint64).tolist()))
     assert n == len(want) and got == want
+
+
+def test_timing_levels_do_not_change_results():
+    """srd_ctx_set_timing: events are opt-in (none by default); every level
+    returns the same outputs, and srd_ctx_timings reports only what was timed."""
+    import torch
+    c = S.Context(0)
+    try:
+        n, L = 3000, 4096
+        size = S.synth_store_len(n, L)
+        t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
+        S.synth_store_device(t.data_ptr(), n, L, seed=0x5EED0001, ctx=c)
+        torch.cuda.synchronize()
+        outs = []
+        for level in (S.TIMING_NONE, S.TIMING_SCAN, S.TIMING_CALL, S.TIMING_NONE):
+            c.set_timing(level)
+            r = S.validate_index_device(t.data_ptr(), size, 0, c)
+            outs.append((r.final_len, r.n_chain, r.n_crc_bad, r.n_index, r.mode))
+            scan_ms, launches, total_ms = c.timings()
+            if level == S.TIMING_NONE:
+                assert (scan_ms, launches, total_ms) == (0.0, 0, 0.0)
+            else:
+                assert launches == 1 and scan_ms > 0
+                assert (total_ms > 0) == (level == S.TIMING_CALL)
+        assert all(o == (size, n, 0, n, S.SRD_MODE_OPTIMISTIC) for o in outs), outs
+        with pytest.raises(S.SrdError):
+            c.set_timing(3)
+    finally:
+        c.close()
