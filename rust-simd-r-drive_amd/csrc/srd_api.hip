@@ -1480,15 +1480,56 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
     run(0);
     for (auto& t : th) t.join();
   }
+  auto composes = [&] {
+    bool ok = true;
+    for (auto& x : sh) ok = ok && !x.rc && x.proven;
+    return ok;
+  };
+  bool composed = composes();
+  bool hard = false;
+  for (auto& x : sh) hard = hard || x.rc;
+  if (!composed && !hard) {
+    // A cut that is no chain tail (a forged metadata record in a payload)
+    // leaves the shard above it unproven (no node has prev == the cut).
+    // Each run [a, b] of unproven shards is re-validated once together with
+    // its lower neighbour, as the span [cuts[a-1], cuts[b+1]) whose ends are
+    // tails the neighbours proved: 2/nc of the store instead of all of it.
+    // Still unproven (a torn tail, corruption): the whole-file path decides.
+    std::vector<std::pair<uint32_t, uint32_t>> runs;
+    uint32_t floor = 0;  // the first shard the next run may take
+    for (uint32_t i = 0; i < nc; i++) {
+      if (sh[i].proven) continue;
+      uint32_t b = i;
+      while (b + 1 < nc && !sh[b + 1].proven) b++;
+      // the lower neighbour: the first non-empty shard below (an empty shard
+      // "proves" nothing; its cut may be the forged one)
+      uint32_t a = i ? i - 1 : 0;
+      while (a > floor && cuts[a] == cuts[a + 1]) a--;
+      runs.emplace_back(std::max(a, floor), b);
+      floor = b + 1;
+      i = b;
+    }
+    for (auto [a, b] : runs) {
+      for (uint32_t i = a + 1; i <= b; i++) {
+        cuts[i] = cuts[b + 1];  // shards a+1..b become empty; shard a spans the run
+        sh[i] = Shard{};
+        sh[i].proven = true;
+      }
+      sh[a] = Shard{};
+    }
+    std::vector<std::thread> th;
+    for (size_t j = 1; j < runs.size(); j++) th.emplace_back(run, runs[j].first);
+    run(runs[0].first);
+    for (auto& t : th) t.join();
+    composed = composes();
+  }
   if (reg_a) {
     (void)hipSetDevice(ctxs[0]->device);
     (void)hipHostUnregister((void*)reg_a);
   }
-  bool composed = true;
-  for (auto& x : sh) composed = composed && !x.rc && x.proven;
-  // a torn tail, corruption, a cut that is no chain tail, or a shard that
-  // failed (capacity, allocation): recover_valid_chain's byte-wise search is
-  // global, so the whole-file path decides
+  // a torn tail, corruption, or a shard that failed (capacity, allocation):
+  // recover_valid_chain's byte-wise search is global, so the whole-file path
+  // decides
   if (!composed) return srd_validate_index(ctxs[0], file, flen, flags, out);
 
   memset(out, 0, sizeof *out);

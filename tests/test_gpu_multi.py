@@ -132,3 +132,21 @@ def test_datastore_open_mmap(tmp_path, ctxs, nd):
     with pytest.warns(UserWarning):
         ds = S.DataStore.open(str(p), ctxs=ctxs[:nd])
     assert ds.tail_offset == st.size and p.stat().st_size == st.size
+
+
+@pytest.mark.parametrize("nd", [3, 4, 6])
+def test_multi_forged_cut_merges_with_lower_neighbour(nd):
+    """A forged cut inside the store (not the top shard's): the shard above it
+    is unproven and is re-validated together with its lower neighbour (the
+    first non-empty one below); the result is still the oracle's."""
+    from test_shard_gloo import fake_cut_store
+    store, fake = fake_cut_store()
+    cuts = list(S.shard_cuts(store, nd))
+    assert fake in cuts and cuts.index(fake) >= 1
+    cs = [S.Context(0) for _ in range(nd)]
+    try:
+        r = S.validate_index_multi(store, cs)
+        same_as_oracle(r, store, f"forged-{nd}")
+    finally:
+        for c in cs:
+            c.close()
