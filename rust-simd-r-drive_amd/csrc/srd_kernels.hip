@@ -494,7 +494,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       slow = __ballot(hz != 0);
     }
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
+    // Wave priority over the LDS-latency chains (the CRC's lookups here, the
+    // flagged-line window below): a wave in them wins the issue arbitration,
+    // so its next round of lookups goes out as soon as the last returns,
+    // while the other waves fill the gaps (same-box A/B: -4 %)
+    __builtin_amdgcn_s_setprio(3);
     const uint32_t c = crc_line4(d, lds, R);
+    __builtin_amdgcn_s_setprio(0);
     const uint32_t hx = half_suffix_xor(lane_weight_or(c, nib_lane), lane);
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
     // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
@@ -527,6 +533,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7]),
                  "+v"(d[8]), "+v"(d[9]), "+v"(d[10]), "+v"(d[11]), "+v"(d[12]), "+v"(d[13]), "+v"(d[14]), "+v"(d[15]));
 
+    if (slow) __builtin_amdgcn_s_setprio(3);
     while (slow) {
       const int f = __builtin_ctzll(slow);
       slow &= slow - 1;
@@ -668,6 +675,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       }
       count += __popcll(cm);
     }
+    __builtin_amdgcn_s_setprio(0);
     // carry the last line's tail and SX_63 into the next tile's window
     if (lane == 63) {
 #pragma unroll
