@@ -754,10 +754,16 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   pad_stores(1);
   for (uint32_t i = 0; i < nfull; i++) {
     const uint32_t j = 3 * i;
+    // priority from the tile's prefetch loads through its CRC (process()
+    // drops it after the lookups): -1.6 % same-box A/B over priority on the
+    // CRC alone
+    __builtin_amdgcn_s_setprio(3);
     load_tile(k0 + min(j + 2, nk), Cv);
     process(k0 + j, A, body);
+    __builtin_amdgcn_s_setprio(3);
     load_tile(k0 + min(j + 3, nk), A);
     process(k0 + j + 1, Bv, body);
+    __builtin_amdgcn_s_setprio(3);
     load_tile(k0 + min(j + 4, nk), Bv);
     process(k0 + j + 2, Cv, body);
   }
