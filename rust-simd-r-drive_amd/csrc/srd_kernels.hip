@@ -533,7 +533,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7]),
                  "+v"(d[8]), "+v"(d[9]), "+v"(d[10]), "+v"(d[11]), "+v"(d[12]), "+v"(d[13]), "+v"(d[14]), "+v"(d[15]));
 
-    if (slow) __builtin_amdgcn_s_setprio(3);
+    // (the flagged-line chain one level below the CRC's: -1.3 % vs equal)
+    if (slow) __builtin_amdgcn_s_setprio(2);
     while (slow) {
       const int f = __builtin_ctzll(slow);
       slow &= slow - 1;
