@@ -9,15 +9,16 @@ payload + compare (is_valid_checksum), and the latest-wins index rebuild
 (KeyIndexer::build).  value = algorithmic bytes sum(payload_len + 20) over all
 ranks / max-over-ranks wall time of K steps.
 
-N>1 (torchrun, one process per GPU): ONE global store of N x --entries-per-gpu
-entries (default 2^21: the C4 partition, so N=8 is exactly C4 -- 16M x 4 KiB,
-65 GiB -- and N=1/2/4 its prefixes), sharded by entry range:
-rank r holds entries [r*n, (r+1)*n) in its HBM and a step
-is srd_shard.sharded_validate_index -- its shard's validate+index
-(srd_validate_span_device), the boundary composition check (all_gather) and
-the owner-partitioned index exchange (all_to_all over RCCL, 16 B per key) +
-owner-side KeyIndexer build.  Weak scaling; the step time is the MAX over
-ranks.
+N>1 (`--gpus N`; under torchrun WORLD_SIZE must equal N): ONE global store of
+N x --entries-per-gpu entries (default 2^21: the C4 partition, so N=8 is
+exactly C4 -- 16M x 4 KiB, 65 GiB -- and N=2/4 its prefixes), sharded by entry
+range: GPU i holds entries [i*n, (i+1)*n) in its HBM.  The
+reference's open is one call, so ONE process (rank 0 under torchrun; the other
+ranks exit) drives all N GPUs: a step is one srd_validate_index_multi_device
+call -- per-GPU host threads run their shard's validate+index, the host
+composes the shards, and the index is exchanged by owner with xGMI peer
+copies (no RCCL).  Weak scaling; the call returns when every shard is done,
+so the step time is the max over shards by construction.
 
 Also prints: roofline of the dominant kernel (scan_kernel, HIP events on the
 library's stream) and a CPU baseline (oracle/, the C restatement of the
@@ -396,15 +397,24 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time host->HBM->result end to end (stderr)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if os.environ.get("SRD_BENCH_SAME_DEVICE"):  # rehearsal of N>1 on a 1-GPU box (gloo, all ranks on cuda:0)
+    world = args.gpus
+    if world_env > 1 and world_env != world:
+        sys.exit(f"bench.py: --gpus {world} but WORLD_SIZE={world_env}: launch one rank per GPU with --gpus N")
+    if world_env > 1:
+        # DataStore::open is ONE call (data_store.rs:84-117): rank 0 drives all
+        # N GPUs of the node in one process (srd_validate_index_multi_device,
+        # per-GPU host threads, index exchange over xGMI peer copies, no RCCL);
+        # the other ranks of a torchrun launch have nothing to do
+        if rank != 0:
+            return
         local = 0
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group(os.environ.get("SRD_DIST_BACKEND", "nccl"), init_method="env://")
+    same_dev = bool(os.environ.get("SRD_BENCH_SAME_DEVICE"))  # rehearsal of N>1 on a 1-GPU box: every shard on cuda:0
+    if world > 1 and not same_dev and torch.cuda.device_count() < local + world:
+        sys.exit(f"bench.py: --gpus {world} needs {world} visible GPUs (found {torch.cuda.device_count()})")
+    devs = [local if same_dev else local + i for i in range(world)]
     torch.cuda.set_device(local)
     ctx = S.Context(local)
     # the roofline's kernel time: HIP events around each scan launch on the
@@ -422,6 +432,7 @@ def main():
     lens, seed = None, 0x5EED0001
     if args.config == "c3":
         lens, seed = S.zipf_lens(n * world), 0x5EED0004
+    multi = None
     if world == 1:
         size = S.synth_store_len(n, L, lens)
         store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
@@ -433,35 +444,55 @@ def main():
             return r.final_len, r.n_chain, r.n_crc_bad, r.n_index
         expect = (size, n, 0, n)
     else:
+        import ctypes as C
         import srd_shard as SH
-        first, cnt = SH.plan_entry_shards(n * world, world)[rank]
-        lo, hi = S.synth_span(None, 0, first, cnt, L, lens)
-        file_len = S.synth_store_len(n * world, L, lens)
-        span_off = lo - lo % S.SPAN_ALIGN
-        size = hi - span_off
-        store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
-        S.synth_span(store.data_ptr(), span_off, first, cnt, L, lens, seed=seed, ctx=ctx)
-        span = (span_off, lo, hi)
-        backend = SH.HipBackend(ctx, local)
+        ctxs = [ctx] + [S.Context(d) for d in devs[1:]]
+        for c in ctxs:
+            c.set_timing(S.TIMING_SCAN)
+        spans, soffs, cuts, keep = [], [], [0], []
+        for i, (first, cnt) in enumerate(SH.plan_entry_shards(n * world, world)):
+            lo, hi = S.synth_span(None, 0, first, cnt, L, lens)
+            so = lo - lo % S.SPAN_ALIGN
+            t = torch.empty(S.padded_size(hi - so), dtype=torch.uint8, device=f"cuda:{devs[i]}")
+            S.synth_span(t.data_ptr(), so, first, cnt, L, lens, seed=seed, ctx=ctxs[i])
+            keep.append(t)
+            spans.append(t.data_ptr())
+            soffs.append(so)
+            cuts.append(hi)
+        for d in set(devs):
+            torch.cuda.synchronize(d)
+        file_len = cuts[-1]
+        store = keep[0]
+        size = cuts[1] - cuts[0]
+        span = (0, 0, size)
+        hs = (C.c_void_p * world)(*[c.h.value for c in ctxs])
+        sp = (C.c_void_p * world)(*spans)
+        so_a = np.array(soffs, np.uint64)
+        cu_a = np.array(cuts, np.uint64)
+        res = (S.DeviceResult * world)()
+        summ = S.MultiSummary()
+        multi = {"validate_ms": 0.0, "exchange_ms": 0.0, "total_ms": 0.0, "scan_ms": [0.0] * world, "n": 0}
 
         def step():
-            r = SH.sharded_validate_index(backend, store, span_off, lo, hi, file_len)
-            return r.final_len, r.n_chain, r.n_crc_bad, r.n_index
+            S._check(S.lib().srd_validate_index_multi_device(hs, world, sp, S._ptr(so_a), S._ptr(cu_a), 0, res,
+                                                             C.byref(summ)))
+            return summ.final_len, summ.n_chain, summ.n_crc_bad, summ.n_index
         expect = (file_len, n * world, 0, n * world)
-    torch.cuda.synchronize()
+    # algorithmic bytes, SURVEY.md 8(d): sum(L_i + 20) over every chain entry
+    # of the whole store (all N shards); bytes_alg = the first shard's share
     if lens is None:
+        bytes_total = algorithmic_bytes(n * world, L)
         bytes_alg = algorithmic_bytes(n, L)
-    else:  # this rank's entries: sum(L_i + 20)
-        f0 = rank * n if world > 1 else 0
-        bytes_alg = int(lens[f0:f0 + n].sum()) + 20 * n
+    else:
+        bytes_total = int(lens[: n * world].sum()) + 20 * n * world
+        bytes_alg = int(lens[:n].sum()) + 20 * n
 
     for _ in range(args.warmup):
         got = step()
     assert got == expect, (got, expect)
 
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    for d in set(devs):
+        torch.cuda.synchronize(d)
     scan_ms_sum, scan_n = 0.0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -469,18 +500,22 @@ def main():
         sm, sn, _ = ctx.timings()
         scan_ms_sum += sm
         scan_n += sn
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+        if multi is not None:
+            for i, c in enumerate(ctxs):
+                multi["scan_ms"][i] += c.timings()[0]
+            for k in ("validate_ms", "exchange_ms", "total_ms"):
+                multi[k] += getattr(summ, k)
+            multi["n"] += 1
+    for d in set(devs):
+        torch.cuda.synchronize(d)
     dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], device="cpu" if dist.get_backend() == "gloo" else f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
 
     ms_per_step = dt / args.steps * 1e3
-    value = bytes_alg * world / dt * args.steps / 2**30
+    value = bytes_total / dt * args.steps / 2**30
     scan_ms = scan_ms_sum / max(scan_n, 1)
+    if multi is not None:  # the slowest shard's scan bounds the step
+        shard_scan = [x / max(multi["n"], 1) for x in multi["scan_ms"]]
+        scan_ms = max(shard_scan)
     achieved = bytes_alg / (scan_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
@@ -521,8 +556,9 @@ def main():
             "store_bytes_per_gpu": span[2] - span[1],
             "algorithmic_bytes_per_gpu": bytes_alg,
             "parallelism": "1 GPU" if world == 1 else
-                           f"{world} entry-range shards, one per GPU; all_gather (boundaries) + "
-                           f"all_to_all (index owners) over RCCL",
+                           f"{world} entry-range shards, one per GPU, one process (srd_validate_index_multi_device): "
+                           f"per-GPU host threads, host composition, index by owner via xGMI peer copies; no RCCL"
+                           + (" [rehearsal: every shard on cuda:0]" if same_dev else ""),
         },
         "roofline": {
             "bound": "hbm",
@@ -535,19 +571,25 @@ def main():
             "traffic": traffic,
             "traffic_note": traffic_note,
             # the whole step (scan + glue + one host sync) against the same peak
-            "step_achieved": round(bytes_alg * world / (ms_per_step * 1e-3) / 1e9 / world, 1),
-            "step_frac": round(bytes_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "step_achieved": round(bytes_total / (ms_per_step * 1e-3) / 1e9 / world, 1),
+            "step_frac": round(bytes_total / world / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu and args.config == "c2":
+    if multi is not None:
+        k = max(multi["n"], 1)
+        out["multi"] = {"devices": devs, "shard_scan_ms": [round(x, 4) for x in shard_scan],
+                        "validate_ms": round(multi["validate_ms"] / k, 4),
+                        "exchange_ms": round(multi["exchange_ms"] / k, 4),
+                        "call_ms": round(multi["total_ms"] / k, 4),
+                        "note": "validate_ms = the slowest shard's validate (host wall, its own thread); "
+                                "exchange_ms = index by owner over xGMI peer copies + owner builds; "
+                                "step = max over shards by construction (one call, all shards joined)"}
+    if world == 1 and not args.no_cpu and args.config == "c2":
         out["cpu_baseline"] = cpu_baseline(store, size, bytes_alg, args.cpu_budget)
-    if args.e2e and rank == 0:
+    if args.e2e and world == 1:
         out_e2e = e2e(store, size, bytes_alg, ctx)
         print(json.dumps(out_e2e), file=sys.stderr, flush=True)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -183,8 +183,9 @@ int srd_validate_index(srd_ctx *ctx, const uint8_t *file, uint64_t file_len,
 void srd_result_free(srd_result *res);
 
 /* DataStore::open of one host store (the mmap) on n GPUs in ONE process,
- * without RCCL (data_store.rs:84-117).  ctxs[i] are contexts
- * (one per GPU; the same device may repeat).  The host pre-pass
+ * without RCCL (data_store.rs:84-117).  ctxs[i] are distinct
+ * contexts (one per GPU; the same device may repeat, the same context may
+ * not: SRD_ERR_ARG).  The host pre-pass
  * srd_shard_cuts splits the store into n entry ranges; one host thread per
  * context stages its span [span_off, hi) and runs srd_validate_span_device.
  * The host composes the shards (every shard proven, each lo == the previous
@@ -197,6 +198,63 @@ void srd_result_free(srd_result *res);
 int srd_validate_index_multi(srd_ctx *const *ctxs, uint32_t n_ctx,
                              const uint8_t *file, uint64_t file_len,
                              uint32_t flags, srd_result *out);
+
+/* ---- the same open over a store already resident in the GPUs' HBM ----
+ *   srd_validate_index_multi_device <- DataStore::open (data_store.rs:84-117:
+ *                                      recover_valid_chain :383-482 +
+ *                                      KeyIndexer::build key_indexer.rs:98-124)
+ *                                      with the file sharded by entry range over
+ *                                      the GPUs of one node, no RCCL
+ * Context i holds its shard in its own HBM: d_spans[i] = file bytes
+ * [span_offs[i], cuts[i+1]) (span_offs[i] a multiple of 16 KiB, <= cuts[i];
+ * span_offs[0] = 0; readable to srd_padded_size(cuts[i+1] - span_offs[i])).
+ * cuts[0] = 0 <= cuts[1] <= .. <= cuts[n] = file_len are entry tails (e.g.
+ * from the writer's layout or srd_shard_cuts); an empty shard (cuts[i] ==
+ * cuts[i+1]) needs no span.  One host thread per context validates its shard;
+ * the host composes them.  Index (latest wins over the whole chain):
+ *   default: by owner -- shards[i].index_* (device arrays on ctxs[i]'s GPU)
+ *            hold the keys with owner ((key_hash >> 32) * n) >> 32 == i, in
+ *            file order of each key's latest entry; every owner pulls its runs
+ *            from all shards over xGMI (hipMemcpyPeerAsync) in shard order;
+ *   SRD_FLAG_MERGE_INDEX: the whole index on ctxs[0]'s GPU
+ *            (summary->index_*, the order srd_validate_index_device gives).
+ * shards[i] (array of n) = chain segment i (device arrays on ctxs[i]'s GPU,
+ * owned by the context until its next call); the segments concatenated in
+ * shard order are the chain in file order.  A shard left unproven by its cut
+ * (a cut that is no chain tail) is re-validated together with its lower
+ * neighbour, the bytes gathered onto that neighbour's GPU over xGMI; a store
+ * that still does not compose (a torn tail, corruption, a shard error) is
+ * decided by the whole-file path on ctxs[0] (the store gathered there; its
+ * whole chain is then shards[0]).  summary (nullable) reports which path
+ * decided, the totals and host timings.  Each entry of ctxs must be a
+ * distinct context (the same device may repeat).  Synchronises. */
+#define SRD_FLAG_MERGE_INDEX 16u
+#define SRD_MULTI_COMPOSED 0u   /* every shard proven on its own */
+#define SRD_MULTI_NEIGHBOUR 1u  /* a run of unproven shards proven with its lower neighbour */
+#define SRD_MULTI_WHOLE_FILE 2u /* the whole-file path decided (torn tail / corruption / shard error) */
+typedef struct {
+  uint64_t file_len, final_len;  /* final_len: recover_valid_chain's answer */
+  uint64_t n_chain, n_index, n_crc_bad, n_candidates;  /* totals */
+  uint32_t mode;          /* SRD_MODE_OPTIMISTIC if every shard's pass was optimistic */
+  uint32_t path;          /* SRD_MULTI_* */
+  uint32_t n_shards;
+  uint32_t merged;        /* 1: the index is summary->index_* on ctxs[0] */
+  uint32_t shard_errors;  /* shards whose first validation failed with an error */
+  uint32_t reserved;
+  double validate_ms;     /* host wall time of the slowest shard's validation(s) */
+  double exchange_ms;     /* index exchange + builds */
+  double total_ms;        /* the whole call */
+  uint64_t *index_key_hash, *index_packed; /* merged: device arrays on ctxs[0] */
+} srd_multi_summary;
+int srd_validate_index_multi_device(srd_ctx *const *ctxs, uint32_t n_ctx,
+                                    const uint8_t *const *d_spans,
+                                    const uint64_t *span_offs,
+                                    const uint64_t *cuts, uint32_t flags,
+                                    srd_device_result *shards,
+                                    srd_multi_summary *summary);
+/* The summary of the last multi-GPU open (host or device input) that had ctx
+ * as ctxs[0]: which path decided it, totals, timings. */
+int srd_ctx_multi_summary(srd_ctx *ctx, srd_multi_summary *out);
 /* Staging of the last host-input call on ctx: *mode = 0 pinned input, 1
  * registered mapping, 2 bounce buffers, 3 pageable copy (-1 none yet);
  * *stage_ms = host wall time from the call's start until the store was in

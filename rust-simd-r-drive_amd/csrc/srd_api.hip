@@ -71,6 +71,8 @@ struct Ctx {
   hipStream_t stream = nullptr;
   std::vector<Buf> bufs;  // indexed by the enum below
   uint32_t cap = 64;      // candidate slots per span (4 tiles); grows x4 on overflow
+  uint32_t grown_cap = 64;   // the cap the last overflow needed ...
+  uint64_t grown_bytes = 0;  // ... for a store (span) of this many bytes
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
   srd_device_result res{};
   // host-input staging
@@ -101,6 +103,7 @@ struct Ctx {
   std::vector<void*> stage_pin;
   std::vector<hipStream_t> stage_streams;
   std::vector<hipEvent_t> stage_ev;
+  srd_multi_summary last_multi{};  // the last multi-GPU open with this context as ctxs[0]
 };
 
 enum BufId {
@@ -120,6 +123,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
+  B_XKEY, B_XVAL, B_GATHER,
   B_COUNT_
 };
 
@@ -358,10 +362,19 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
 extern "C" void* srd_ctx_stream(srd_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 // Candidate slots per span grow x4 on overflow and are remembered by the
-// context; a store much smaller per span than the one that grew them starts
-// lower again, so the records (40 B per slot) stay within ~2x the store.
+// context; a store of another size starts lower again, so the records (40 B
+// per slot) stay within ~2x the store.  A store within 2x of the size whose
+// overflow grew the cap keeps that cap (a dense store would otherwise
+// overflow -- and rescan -- on every call).
 static void fit_cap(Ctx* c, uint64_t n_spans, uint64_t bytes) {
-  while (c->cap > 64 && (uint64_t)c->cap * 40 * n_spans > 2 * bytes + (64ull << 20)) c->cap /= 4;
+  const bool similar = c->grown_bytes && bytes <= 2 * c->grown_bytes && 2 * bytes >= c->grown_bytes;
+  const uint32_t floor = similar ? c->grown_cap : 64;
+  while (c->cap > floor && (uint64_t)c->cap * 40 * n_spans > 2 * bytes + (64ull << 20)) c->cap /= 4;
+}
+static void grow_cap(Ctx* c, uint64_t bytes) {
+  c->cap = (uint32_t)std::min<uint64_t>((uint64_t)c->cap * 4, SPAN_BYTES);
+  c->grown_cap = c->cap;
+  c->grown_bytes = bytes;
 }
 
 // the scan kernel's per-wave results and last-block reduction (ScanArgs)
@@ -605,7 +618,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     }
     if ((uint32_t)h[2] == 0) break;
     if (c->cap >= SPAN_BYTES) { set_err("candidate overflow"); return SRD_ERR_INTERNAL; }
-    c->cap = (uint32_t)std::min<uint64_t>((uint64_t)c->cap * 4, SPAN_BYTES);
+    grow_cap(c, flen);
   }
   if (*K) {
     TRY(alloc_dense(c, *K));
@@ -931,7 +944,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     out->n_weak = hp.n_weak;
     if (hp.status & ST_OVERFLOW) {
       if (c->cap >= SPAN_BYTES) return 0;  // cannot happen (<= one candidate per byte); not provable here
-      c->cap = (uint32_t)std::min<uint64_t>((uint64_t)c->cap * 4, SPAN_BYTES);
+      grow_cap(c, flen - span_off);
       continue;
     }
     if (hp.status & ST_CAPK) {
@@ -1025,25 +1038,24 @@ extern "C" int srd_validate_span_device(srd_ctx* c, const uint8_t* d_span, uint6
   return r;
 }
 
-extern "C" int srd_index_partition_device(srd_ctx* c, const uint64_t* d_keys, const uint64_t* d_vals, uint64_t n,
-                                          uint32_t world, uint64_t* d_out_pairs, uint64_t* counts) {
-  if (!c || !counts || world == 0 || world > PART_MAX_WORLD || (n && (!d_keys || !d_vals || !d_out_pairs))) {
-    set_err("bad argument");
-    return SRD_ERR_ARG;
-  }
-  HIPCHK(hipSetDevice(c->device));
+// stable partition of n (key, value) device pairs by owner rank; interleaved
+// output at out (out_v == nullptr) or keys at out / values at out_v.  counts
+// (host, [world]) receives the group sizes.  Synchronises.
+static int partition_impl(Ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, uint32_t world,
+                          uint64_t* out, uint64_t* out_v, uint64_t* counts) {
   const uint64_t nc = (uint64_t)world * GLUE_BLOCKS + 1;
   TRY(ensure(c, B_PCNT, nc * 4));
   TRY(ensure(c, B_POFF, nc * 4 + 8 * PART_MAX_WORLD));
   TRY(ensure_cub(c, nc));
   PartArgs a{};
-  a.keys = d_keys;
-  a.vals = d_vals;
+  a.keys = keys;
+  a.vals = vals;
   a.n = n;
   a.world = world;
   a.cnt = P<uint32_t>(c, B_PCNT);
   a.off = P<uint32_t>(c, B_POFF);
-  a.out = d_out_pairs;
+  a.out = out;
+  a.out_v = out_v;
   a.counts = (uint64_t*)(P<uint32_t>(c, B_POFF) + ((nc + 1) & ~1ull));
   part_count_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(a);
   KCHK(c, "part_count_kernel");
@@ -1057,6 +1069,16 @@ extern "C" int srd_index_partition_device(srd_ctx* c, const uint64_t* d_keys, co
   HIPCHK(hipMemcpyAsync(counts, a.counts, world * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
+}
+
+extern "C" int srd_index_partition_device(srd_ctx* c, const uint64_t* d_keys, const uint64_t* d_vals, uint64_t n,
+                                          uint32_t world, uint64_t* d_out_pairs, uint64_t* counts) {
+  if (!c || !counts || world == 0 || world > PART_MAX_WORLD || (n && (!d_keys || !d_vals || !d_out_pairs))) {
+    set_err("bad argument");
+    return SRD_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  return partition_impl(c, d_keys, d_vals, n, world, d_out_pairs, nullptr, counts);
 }
 
 __global__ void set_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
@@ -1255,19 +1277,23 @@ static int ensure_file_buf(Ctx* c, uint64_t flen, uint8_t** d) {
 }
 
 static int stage_bounce(Ctx* c, const uint8_t* src, uint64_t len, uint8_t* dst, int workers) {
-  const int T = std::max(1, std::min(workers, c->stage_workers));
-  if (c->stage_pin.empty()) {
-    const int W = c->stage_workers;
-    c->stage_pin.assign(2 * W, nullptr);
-    c->stage_streams.assign(W, nullptr);
-    c->stage_ev.assign(2 * W, nullptr);
-    for (int i = 0; i < 2 * W; i++) {
-      HIPCHK(hipHostMalloc(&c->stage_pin[i], kBounceBytes, hipHostMallocDefault));
-      HIPCHK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
-    }
-    for (int w = 0; w < W; w++) HIPCHK(hipStreamCreateWithFlags(&c->stage_streams[w], hipStreamNonBlocking));
-  }
   const uint64_t nch = (len + kBounceBytes - 1) / kBounceBytes;
+  // T workers, each with two pinned bounce buffers and a stream: allocated
+  // when a call first needs them (the multi-GPU open gives each shard fewer)
+  const int T = (int)std::min<uint64_t>((uint64_t)std::max(1, std::min(workers, c->stage_workers)), nch);
+  for (int w = (int)c->stage_streams.size(); w < T; w++) {
+    void* pin[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    hipStream_t st = nullptr;
+    for (int k = 0; k < 2; k++) {
+      HIPCHK(hipHostMalloc(&pin[k], kBounceBytes, hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+    }
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    c->stage_pin.insert(c->stage_pin.end(), pin, pin + 2);
+    c->stage_ev.insert(c->stage_ev.end(), ev, ev + 2);
+    c->stage_streams.push_back(st);
+  }
   std::vector<int> rc(T, 0);
   auto work = [&](int w) {
     if (hipSetDevice(c->device) != hipSuccess) { rc[w] = SRD_ERR_HIP; return; }
@@ -1286,9 +1312,8 @@ static int stage_bounce(Ctx* c, const uint8_t* src, uint64_t len, uint8_t* dst, 
     if (hipStreamSynchronize(c->stage_streams[w]) != hipSuccess) rc[w] = SRD_ERR_HIP;
   };
   std::vector<std::thread> th;
-  const int used = (int)std::min<uint64_t>((uint64_t)T, nch);
-  for (int w = 1; w < used; w++) th.emplace_back(work, w);
-  if (used) work(0);
+  for (int w = 1; w < T; w++) th.emplace_back(work, w);
+  if (T) work(0);
   for (auto& t : th) t.join();
   for (int w = 0; w < T; w++)
     if (rc[w]) { set_err("bounce-buffer staging failed"); return rc[w]; }
@@ -1405,10 +1430,18 @@ extern "C" int srd_ctx_stage_info(srd_ctx* c, int* mode, double* stage_ms) {
 }
 
 // ---------------------------------------------------------------------------
-// DataStore::open on n GPUs in one process, no RCCL:
-// host cuts -> one host thread per context (stage span, validate span) ->
-// host composition -> chain arrays concatenated, shard indexes gathered to
-// ctxs[0] (peer copies) and merged latest-wins there in shard = file order.
+// DataStore::open on n GPUs in one process, no RCCL.
+//
+// srd_validate_index_multi_device: every context holds its entry-range shard
+// in its own HBM.  One host thread per context validates its span
+// (srd_validate_span_device) and, for the by-owner index, partitions its
+// shard-local index by owner; the host composes the shards; each owner then
+// pulls its runs from every shard in shard (= file) order over xGMI
+// (hipMemcpyPeerAsync; no collective library) and builds its part of the
+// latest-wins index.  With SRD_FLAG_MERGE_INDEX ctxs[0] pulls the whole
+// shard indexes instead and builds the one merged index.
+// srd_validate_index_multi (host input) stages the spans and calls the same
+// implementation with the merged index, then copies the result to the host.
 static void enable_peer(int dev0, int dev) {
   static std::mutex mu;
   static uint64_t done[64] = {};
@@ -1421,26 +1454,384 @@ static void enable_peer(int dev0, int dev) {
   done[dev0] |= 1ull << dev;
 }
 
+// the same context twice would be driven by two host threads at once (its
+// stream, workspace and staging buffers are not shareable)
+static int check_ctxs(srd_ctx* const* ctxs, uint32_t nc) {
+  if (nc > PART_MAX_WORLD) { set_err("bad argument: at most 64 contexts"); return SRD_ERR_ARG; }
+  for (uint32_t i = 0; i < nc; i++) {
+    if (!ctxs[i]) { set_err("bad argument: null context"); return SRD_ERR_ARG; }
+    for (uint32_t j = 0; j < i; j++)
+      if (ctxs[j] == ctxs[i]) { set_err("bad argument: each entry of ctxs must be a distinct context"); return SRD_ERR_ARG; }
+  }
+  return 0;
+}
+
+template <class F>
+static void parallel_for(uint32_t n, F&& f) {
+  std::vector<std::thread> th;
+  th.reserve(n);
+  for (uint32_t i = 1; i < n; i++) th.emplace_back(f, i);
+  if (n) f(0);
+  for (auto& t : th) t.join();
+}
+
+// device copy into dst's memory on dst's stream (peer copy over xGMI when the
+// source lives on another GPU)
+static hipError_t copy_to(Ctx* dst, void* d, const Ctx* src, const void* s, uint64_t bytes) {
+  if (!bytes) return hipSuccess;
+  if (src->device == dst->device) return hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, dst->stream);
+  enable_peer(dst->device, src->device);
+  return hipMemcpyPeerAsync(d, dst->device, s, src->device, bytes, dst->stream);
+}
+
+using Clock = std::chrono::steady_clock;
+static double ms_since(Clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+struct MultiIn {
+  srd_ctx* const* ctxs;
+  uint32_t nc;
+  const uint8_t* const* span;  // span[i] = file byte soff[i] on ctxs[i]'s device
+  const uint64_t* soff;
+  const uint64_t* cuts;        // [nc + 1]: shard i holds [soff[i], cuts[i + 1]) when cuts[i] < cuts[i + 1]
+  uint64_t flen;
+};
+
+// file bytes [x, y) assembled in dst's B_GATHER buffer from the shards whose
+// resident range covers them (the re-validation of a run of unproven shards
+// with its lower neighbour, and the whole-file path)
+static int gather_range(Ctx* dst, const MultiIn& in, uint64_t x, uint64_t y, const uint8_t** out) {
+  TRY(ensure(dst, B_GATHER, srd_padded_size(y - x)));
+  uint8_t* d = P<uint8_t>(dst, B_GATHER);
+  for (uint64_t pos = x; pos < y;) {
+    int best = -1;
+    uint64_t reach = pos;
+    for (uint32_t j = 0; j < in.nc; j++)
+      if (in.cuts[j] < in.cuts[j + 1] && in.soff[j] <= pos && in.cuts[j + 1] > reach) {
+        reach = in.cuts[j + 1];
+        best = (int)j;
+      }
+    if (best < 0) { set_err("internal: no shard holds file byte " + std::to_string(pos)); return SRD_ERR_INTERNAL; }
+    const uint64_t e = std::min(y, reach);
+    HIPCHK(copy_to(dst, d + (pos - x), in.ctxs[best], in.span[best] + (pos - in.soff[best]), e - pos));
+    pos = e;
+  }
+  *out = d;
+  return 0;
+}
+
+static void release_gather(Ctx* c) {
+  Buf& b = c->bufs[B_GATHER];
+  if (b.p) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(b.p);
+  }
+  b.p = nullptr;
+  b.n = 0;
+}
+
+struct MShard {
+  int rc = 0;
+  std::string err;
+  srd_device_result r{};
+  bool proven = false;
+  bool parted = false;
+  uint64_t cnt[PART_MAX_WORLD] = {};  // owner run lengths of the partitioned shard index
+};
+
+static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_result* shards, srd_multi_summary* sum) {
+  const auto t_call = Clock::now();
+  const uint32_t nc = in.nc;
+  const bool merged = flags & SRD_FLAG_MERGE_INDEX;
+  const uint32_t vflags = flags & ~(kStageFlags | SRD_FLAG_MERGE_INDEX);
+  std::vector<uint64_t> cuts(in.cuts, in.cuts + nc + 1);
+  std::vector<MShard> sh(nc);
+  std::vector<double> vms(nc, 0.0);
+  uint32_t path = SRD_MULTI_COMPOSED, n_err = 0;
+  std::string first_err;
+
+  // owner partition of shard i's index (by-owner layout, nc > 1)
+  auto part = [&](uint32_t i) -> int {
+    MShard& s = sh[i];
+    if (merged || nc == 1 || s.parted) return 0;
+    Ctx* c = in.ctxs[i];
+    const uint64_t n = s.r.n_index;
+    TRY(ensure(c, B_XKEY, std::max<uint64_t>(n, 1) * 8));
+    TRY(ensure(c, B_XVAL, std::max<uint64_t>(n, 1) * 8));
+    if (n) TRY(partition_impl(c, s.r.index_key_hash, s.r.index_packed, n, nc, P<uint64_t>(c, B_XKEY), P<uint64_t>(c, B_XVAL), s.cnt));
+    s.parted = true;
+    return 0;
+  };
+  auto validate = [&](uint32_t i, const uint8_t* d, uint64_t soff, uint64_t lo, uint64_t hi) {
+    const auto t0 = Clock::now();
+    MShard& s = sh[i];
+    s = MShard{};
+    if (lo == hi) { s.proven = true; return; }  // an empty shard composes trivially
+    srd_ctx* c = in.ctxs[i];
+    s.rc = srd_validate_span_device(c, d, soff, lo, hi, vflags, &s.r);
+    if (!s.rc) {
+      s.proven = s.r.final_len == hi && s.r.mode != SRD_MODE_SPAN_UNPROVEN;
+      if (s.proven) s.rc = part(i);
+    }
+    if (s.rc) s.err = g_err;
+    vms[i] += ms_since(t0);
+  };
+  auto composes = [&] {
+    bool ok = true;
+    for (auto& x : sh) ok = ok && !x.rc && x.proven;
+    return ok;
+  };
+  auto note_errors = [&] {
+    for (auto& x : sh)
+      if (x.rc) {
+        n_err++;
+        if (first_err.empty()) first_err = x.err;
+      }
+  };
+
+  parallel_for(nc, [&](uint32_t i) { validate(i, in.span[i], in.soff[i], cuts[i], cuts[i + 1]); });
+  bool composed = composes();
+  note_errors();
+  // shard 0 over the whole store IS the whole-file path (lo = 0)
+  const bool whole_already = cuts[1] == in.flen;
+  if (!composed && !n_err && !whole_already) {
+    // A cut that is no chain tail (a forged metadata record in a payload)
+    // leaves the shard above it unproven (no node has prev == the cut).
+    // Each run [a, b] of unproven shards is re-validated once together with
+    // its lower neighbour, as the span [cuts[a], cuts[b+1]) whose ends are
+    // tails the neighbours proved -- its bytes gathered onto ctxs[a]'s GPU:
+    // 2/nc of the store instead of all of it.  Still unproven (a torn tail,
+    // corruption): the whole-file path decides.
+    path = SRD_MULTI_NEIGHBOUR;
+    std::vector<std::pair<uint32_t, uint32_t>> runs;
+    uint32_t floor = 0;  // the first shard the next run may take
+    for (uint32_t i = 0; i < nc; i++) {
+      if (sh[i].proven) continue;
+      uint32_t b = i;
+      while (b + 1 < nc && !sh[b + 1].proven) b++;
+      // the lower neighbour: the first non-empty shard below (an empty shard
+      // "proves" nothing; its cut may be the forged one)
+      uint32_t a = i ? i - 1 : 0;
+      while (a > floor && cuts[a] == cuts[a + 1]) a--;
+      runs.emplace_back(std::max(a, floor), b);
+      floor = b + 1;
+      i = b;
+    }
+    for (auto [a, b] : runs)
+      for (uint32_t i = a + 1; i <= b; i++) {
+        cuts[i] = cuts[b + 1];  // shards a+1..b become empty; shard a spans the run
+        sh[i] = MShard{};
+        sh[i].proven = true;
+      }
+    parallel_for((uint32_t)runs.size(), [&](uint32_t k) {
+      const uint32_t a = runs[k].first;
+      const uint64_t lo = cuts[a], hi = cuts[a + 1], x = lo - lo % SPAN_BYTES;
+      const uint8_t* d = nullptr;
+      Ctx* c = in.ctxs[a];
+      int r = hipSetDevice(c->device) == hipSuccess ? 0 : SRD_ERR_HIP;
+      if (!r && lo < hi) r = gather_range(c, in, x, hi, &d);
+      if (r) {
+        sh[a] = MShard{};
+        sh[a].rc = r;
+        sh[a].err = g_err;
+        return;
+      }
+      validate(a, d, x, lo, hi);
+    });
+    composed = composes();
+    note_errors();
+  }
+  if (!composed && !whole_already) {
+    // a torn tail, corruption, or a shard that failed (capacity, allocation):
+    // recover_valid_chain's byte-wise search is global, so the whole-file
+    // path decides, on ctxs[0] with the store gathered there
+    path = SRD_MULTI_WHOLE_FILE;
+    for (uint32_t i = 1; i < nc; i++) {
+      sh[i] = MShard{};
+      cuts[i] = in.flen;
+    }
+    srd_ctx* c0 = in.ctxs[0];
+    const auto t0 = Clock::now();
+    sh[0] = MShard{};
+    const uint8_t* d = nullptr;
+    int r = hipSetDevice(c0->device) == hipSuccess ? 0 : SRD_ERR_HIP;
+    if (!r) r = gather_range(c0, in, 0, in.flen, &d);
+    if (!r) r = srd_validate_index_device(c0, d, in.flen, vflags, &sh[0].r);
+    if (!r) r = part(0);
+    vms[0] += ms_since(t0);
+    if (r) {
+      if (!first_err.empty()) set_err(g_err + " (after a shard error: " + first_err + ")");
+      release_gather(c0);
+      return r;
+    }
+  } else if (!composed) {
+    path = SRD_MULTI_WHOLE_FILE;  // shard 0 was the whole store: its answer is final
+    if (sh[0].rc) {
+      set_err(sh[0].err);
+      return sh[0].rc;
+    }
+  }
+  for (uint32_t i = 0; i < nc; i++) release_gather(in.ctxs[i]);
+
+  // ---- index exchange ----
+  const auto t_ex = Clock::now();
+  std::vector<uint64_t> ni(nc, 0);
+  std::vector<int> erc(nc, 0);
+  std::vector<std::string> eerr(nc);
+  uint64_t merged_n = 0;
+  uint64_t *mkey = nullptr, *mpacked = nullptr;
+  if (nc == 1) {
+    ni[0] = sh[0].r.n_index;
+    mkey = sh[0].r.index_key_hash;
+    mpacked = sh[0].r.index_packed;
+    merged_n = ni[0];
+  } else if (merged) {
+    Ctx* c0 = in.ctxs[0];
+    int r = hipSetDevice(c0->device) == hipSuccess ? 0 : SRD_ERR_HIP;
+    uint64_t NI = 0;
+    for (auto& x : sh) NI += x.r.n_index;
+    const uint64_t m1 = std::max<uint64_t>(NI, 1);
+    if (!r) r = ensure(c0, B_GKEY, m1 * 8);
+    if (!r) r = ensure(c0, B_GVAL, m1 * 8);
+    if (!r) r = ensure(c0, B_GOKEY, m1 * 8);
+    if (!r) r = ensure(c0, B_GOPACKED, m1 * 8);
+    uint64_t acc = 0;
+    for (uint32_t s = 0; s < nc && !r; s++) {
+      const uint64_t n = sh[s].r.n_index;
+      if (copy_to(c0, P<uint64_t>(c0, B_GKEY) + acc, in.ctxs[s], sh[s].r.index_key_hash, n * 8) != hipSuccess ||
+          copy_to(c0, P<uint64_t>(c0, B_GVAL) + acc, in.ctxs[s], sh[s].r.index_packed, n * 8) != hipSuccess) {
+        set_err("index gather: peer copy failed");
+        r = SRD_ERR_HIP;
+      }
+      acc += n;
+    }
+    if (!r) r = index_build_sep(c0, P<uint64_t>(c0, B_GKEY), P<uint64_t>(c0, B_GVAL), NI, P<uint64_t>(c0, B_GOKEY),
+                                P<uint64_t>(c0, B_GOPACKED), &merged_n);
+    if (r) return r;
+    mkey = P<uint64_t>(c0, B_GOKEY);
+    mpacked = P<uint64_t>(c0, B_GOPACKED);
+  } else {
+    // by owner: the shards re-validated above partition now
+    parallel_for(nc, [&](uint32_t i) {
+      if (hipSetDevice(in.ctxs[i]->device) != hipSuccess) { erc[i] = SRD_ERR_HIP; return; }
+      if ((erc[i] = part(i))) eerr[i] = g_err;
+    });
+    for (uint32_t i = 0; i < nc; i++)
+      if (erc[i]) { set_err(eerr[i]); return erc[i]; }
+    parallel_for(nc, [&](uint32_t p) {
+      Ctx* c = in.ctxs[p];
+      int& r = erc[p];
+      if (hipSetDevice(c->device) != hipSuccess) { r = SRD_ERR_HIP; eerr[p] = "hipSetDevice"; return; }
+      uint64_t NI = 0;
+      for (auto& x : sh) NI += x.cnt[p];
+      const uint64_t m1 = std::max<uint64_t>(NI, 1);
+      if (!r) r = ensure(c, B_GKEY, m1 * 8);
+      if (!r) r = ensure(c, B_GVAL, m1 * 8);
+      if (!r) r = ensure(c, B_GOKEY, m1 * 8);
+      if (!r) r = ensure(c, B_GOPACKED, m1 * 8);
+      uint64_t acc = 0;
+      for (uint32_t s = 0; s < nc && !r; s++) {
+        uint64_t off = 0;
+        for (uint32_t q = 0; q < p; q++) off += sh[s].cnt[q];
+        const uint64_t n = sh[s].cnt[p];
+        Ctx* cs = in.ctxs[s];
+        if (copy_to(c, P<uint64_t>(c, B_GKEY) + acc, cs, P<uint64_t>(cs, B_XKEY) + off, n * 8) != hipSuccess ||
+            copy_to(c, P<uint64_t>(c, B_GVAL) + acc, cs, P<uint64_t>(cs, B_XVAL) + off, n * 8) != hipSuccess) {
+          set_err("index exchange: peer copy failed");
+          r = SRD_ERR_HIP;
+        }
+        acc += n;
+      }
+      if (!r) r = index_build_sep(c, P<uint64_t>(c, B_GKEY), P<uint64_t>(c, B_GVAL), NI, P<uint64_t>(c, B_GOKEY),
+                                  P<uint64_t>(c, B_GOPACKED), &ni[p]);
+      if (r) eerr[p] = g_err;
+    });
+    for (uint32_t i = 0; i < nc; i++)
+      if (erc[i]) { set_err(eerr[i]); return erc[i]; }
+  }
+  const double ex_ms = ms_since(t_ex);
+
+  srd_multi_summary S{};
+  S.file_len = in.flen;
+  S.final_len = path == SRD_MULTI_WHOLE_FILE ? sh[0].r.final_len : in.flen;
+  S.mode = SRD_MODE_OPTIMISTIC;
+  for (uint32_t i = 0; i < nc; i++) {
+    srd_device_result o = sh[i].r;
+    if (cuts[i] == cuts[i + 1] && path != SRD_MULTI_WHOLE_FILE) memset(&o, 0, sizeof o);
+    if (path == SRD_MULTI_WHOLE_FILE && i) memset(&o, 0, sizeof o);
+    S.n_chain += o.n_chain;
+    S.n_crc_bad += o.n_crc_bad;
+    S.n_candidates += o.n_candidates;
+    if ((o.n_chain || i == 0) && o.mode != SRD_MODE_OPTIMISTIC) S.mode = SRD_MODE_FULL;
+    if (merged || nc == 1) {
+      if (nc > 1) {
+        o.n_index = 0;
+        o.index_key_hash = o.index_packed = nullptr;
+      }
+    } else {
+      Ctx* c = in.ctxs[i];
+      o.n_index = ni[i];
+      o.index_key_hash = P<uint64_t>(c, B_GOKEY);
+      o.index_packed = P<uint64_t>(c, B_GOPACKED);
+      S.n_index += ni[i];
+    }
+    shards[i] = o;
+  }
+  if (merged || nc == 1) {
+    S.n_index = merged_n;
+    S.index_key_hash = mkey;
+    S.index_packed = mpacked;
+  }
+  S.path = path;
+  S.n_shards = nc;
+  S.merged = (merged || nc == 1) ? 1u : 0u;
+  S.shard_errors = n_err;
+  for (double v : vms) S.validate_ms = std::max(S.validate_ms, v);
+  S.exchange_ms = ex_ms;
+  S.total_ms = ms_since(t_call);
+  if (sum) *sum = S;
+  in.ctxs[0]->last_multi = S;
+  return 0;
+}
+
+extern "C" int srd_validate_index_multi_device(srd_ctx* const* ctxs, uint32_t nc, const uint8_t* const* d_spans,
+                                               const uint64_t* span_offs, const uint64_t* cuts, uint32_t flags,
+                                               srd_device_result* shards, srd_multi_summary* summary) {
+  if (!ctxs || !nc || !d_spans || !span_offs || !cuts || !shards) { set_err("bad argument"); return SRD_ERR_ARG; }
+  TRY(check_ctxs(ctxs, nc));
+  const uint64_t flen = cuts[nc];
+  if (cuts[0] != 0 || flen > kMaxFile) { set_err("bad argument: cuts[0] must be 0 and file_len <= 2^48"); return SRD_ERR_ARG; }
+  for (uint32_t i = 0; i < nc; i++) {
+    if (cuts[i] > cuts[i + 1]) { set_err("bad argument: cuts must be non-decreasing"); return SRD_ERR_ARG; }
+    if (cuts[i] == cuts[i + 1]) continue;
+    if (!d_spans[i] || span_offs[i] % SPAN_BYTES || span_offs[i] > cuts[i] || (cuts[i] == 0 && span_offs[i])) {
+      set_err("bad argument: shard " + std::to_string(i) +
+              " needs a span starting at a multiple of 16 KiB at or below its lower tail");
+      return SRD_ERR_ARG;
+    }
+  }
+  MultiIn in{ctxs, nc, d_spans, span_offs, cuts, flen};
+  return multi_device_impl(in, flags, shards, summary);
+}
+
+extern "C" int srd_ctx_multi_summary(srd_ctx* c, srd_multi_summary* out) {
+  if (!c || !out) { set_err("bad argument"); return SRD_ERR_ARG; }
+  *out = c->last_multi;
+  return 0;
+}
+
 extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const uint8_t* file, uint64_t flen,
                                         uint32_t flags, srd_result* out) {
   if (!ctxs || !nc || !out || (!file && flen)) { set_err("bad argument"); return SRD_ERR_ARG; }
-  for (uint32_t i = 0; i < nc; i++)
-    if (!ctxs[i]) { set_err("bad argument: null context"); return SRD_ERR_ARG; }
+  TRY(check_ctxs(ctxs, nc));
   if (nc == 1) return srd_validate_index(ctxs[0], file, flen, flags, out);
-  std::vector<uint64_t> cuts(nc + 1);
+  std::vector<uint64_t> cuts(nc + 1), soff(nc, 0);
   {
     const char* why = "";
     const int r = srd_host::shard_cuts(file, flen, nc, cuts.data(), &why);
     if (r) { set_err(why); return r; }
   }
-  struct Shard {
-    int rc = 0;
-    std::string err;
-    srd_device_result r{};
-    bool proven = false;
-  };
-  std::vector<Shard> sh(nc);
-  const uint32_t vflags = flags & ~kStageFlags;
   // pinned input: each shard copies its span directly.  SRD_FLAG_STAGE_REGISTER:
   // the mapping is registered once for all shards (their spans overlap by
   // up to 16 KiB).  Otherwise each shard's bounce workers (the host threads
@@ -1460,92 +1851,32 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
       if (!pinned) reg_a = reg_e = 0;
     }
   }
-  auto run = [&](uint32_t i) {
+  std::vector<const uint8_t*> span(nc, nullptr);
+  std::vector<int> rc(nc, 0);
+  std::vector<std::string> err(nc);
+  parallel_for(nc, [&](uint32_t i) {
     srd_ctx* c = ctxs[i];
-    Shard& s = sh[i];
     const uint64_t lo = cuts[i], hi = cuts[i + 1];
-    if (lo == hi) { s.proven = true; return; }  // an empty shard composes trivially
-    if (hipSetDevice(c->device) != hipSuccess) { s.rc = SRD_ERR_HIP; s.err = "hipSetDevice"; return; }
-    const uint64_t span_off = lo - lo % SPAN_BYTES;
-    const uint8_t* d = nullptr;
-    s.rc = stage_host(c, file + span_off, hi - span_off, flags, &d, pinned,
-                      std::max(1, ctxs[0]->stage_workers / (int)nc));
-    if (!s.rc) s.rc = srd_validate_span_device(c, d, span_off, lo, hi, vflags, &s.r);
-    if (s.rc) { s.err = g_err; return; }
-    s.proven = s.r.final_len == hi && s.r.mode != SRD_MODE_SPAN_UNPROVEN;
-  };
-  {
-    std::vector<std::thread> th;
-    for (uint32_t i = 1; i < nc; i++) th.emplace_back(run, i);
-    run(0);
-    for (auto& t : th) t.join();
-  }
-  auto composes = [&] {
-    bool ok = true;
-    for (auto& x : sh) ok = ok && !x.rc && x.proven;
-    return ok;
-  };
-  bool composed = composes();
-  bool hard = false;
-  for (auto& x : sh) hard = hard || x.rc;
-  if (!composed && !hard) {
-    // A cut that is no chain tail (a forged metadata record in a payload)
-    // leaves the shard above it unproven (no node has prev == the cut).
-    // Each run [a, b] of unproven shards is re-validated once together with
-    // its lower neighbour, as the span [cuts[a-1], cuts[b+1]) whose ends are
-    // tails the neighbours proved: 2/nc of the store instead of all of it.
-    // Still unproven (a torn tail, corruption): the whole-file path decides.
-    std::vector<std::pair<uint32_t, uint32_t>> runs;
-    uint32_t floor = 0;  // the first shard the next run may take
-    for (uint32_t i = 0; i < nc; i++) {
-      if (sh[i].proven) continue;
-      uint32_t b = i;
-      while (b + 1 < nc && !sh[b + 1].proven) b++;
-      // the lower neighbour: the first non-empty shard below (an empty shard
-      // "proves" nothing; its cut may be the forged one)
-      uint32_t a = i ? i - 1 : 0;
-      while (a > floor && cuts[a] == cuts[a + 1]) a--;
-      runs.emplace_back(std::max(a, floor), b);
-      floor = b + 1;
-      i = b;
-    }
-    for (auto [a, b] : runs) {
-      for (uint32_t i = a + 1; i <= b; i++) {
-        cuts[i] = cuts[b + 1];  // shards a+1..b become empty; shard a spans the run
-        sh[i] = Shard{};
-        sh[i].proven = true;
-      }
-      sh[a] = Shard{};
-    }
-    std::vector<std::thread> th;
-    for (size_t j = 1; j < runs.size(); j++) th.emplace_back(run, runs[j].first);
-    run(runs[0].first);
-    for (auto& t : th) t.join();
-    composed = composes();
-  }
+    if (lo == hi) return;
+    soff[i] = lo - lo % SPAN_BYTES;
+    if (hipSetDevice(c->device) != hipSuccess) { rc[i] = SRD_ERR_HIP; err[i] = "hipSetDevice"; return; }
+    rc[i] = stage_host(c, file + soff[i], hi - soff[i], flags, &span[i], pinned,
+                       std::max(1, ctxs[0]->stage_workers / (int)nc));
+    if (rc[i]) err[i] = g_err;
+  });
   if (reg_a) {
     (void)hipSetDevice(ctxs[0]->device);
     (void)hipHostUnregister((void*)reg_a);
   }
-  // a torn tail, corruption, or a shard that failed (capacity, allocation):
-  // recover_valid_chain's byte-wise search is global, so the whole-file path
-  // decides
-  if (!composed) return srd_validate_index(ctxs[0], file, flen, flags, out);
+  for (uint32_t i = 0; i < nc; i++)
+    if (rc[i]) { set_err(err[i]); return rc[i]; }
+  std::vector<srd_device_result> sr(nc);
+  srd_multi_summary sum{};
+  MultiIn in{ctxs, nc, span.data(), soff.data(), cuts.data(), flen};
+  TRY(multi_device_impl(in, (flags & ~kStageFlags) | SRD_FLAG_MERGE_INDEX, sr.data(), &sum));
 
   memset(out, 0, sizeof *out);
-  std::vector<uint64_t> cb(nc), ib(nc);
-  uint64_t N = 0, NI = 0, bad = 0, cand = 0;
-  bool all_opt = true;
-  for (uint32_t i = 0; i < nc; i++) {
-    cb[i] = N;
-    ib[i] = NI;
-    N += sh[i].r.n_chain;
-    NI += sh[i].r.n_index;
-    bad += sh[i].r.n_crc_bad;
-    cand += sh[i].r.n_candidates;
-    if (cuts[i] != cuts[i + 1] && sh[i].r.mode != SRD_MODE_OPTIMISTIC) all_opt = false;
-  }
-  const uint64_t n1 = std::max<uint64_t>(N, 1);
+  const uint64_t N = sum.n_chain, n1 = std::max<uint64_t>(N, 1), k1 = std::max<uint64_t>(sum.n_index, 1);
   out->meta_off = (uint64_t*)malloc(n1 * 8);
   out->key_hash = (uint64_t*)malloc(n1 * 8);
   out->prev_offset = (uint64_t*)malloc(n1 * 8);
@@ -1554,23 +1885,28 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
   out->crc_stored = (uint32_t*)malloc(n1 * 4);
   out->crc_computed = (uint32_t*)malloc(n1 * 4);
   out->crc_ok = (uint8_t*)malloc(n1);
+  out->index_key_hash = (uint64_t*)malloc(k1 * 8);
+  out->index_packed = (uint64_t*)malloc(k1 * 8);
   if (!out->meta_off || !out->key_hash || !out->prev_offset || !out->payload_start || !out->payload_len ||
-      !out->crc_stored || !out->crc_computed || !out->crc_ok) {
+      !out->crc_stored || !out->crc_computed || !out->crc_ok || !out->index_key_hash || !out->index_packed) {
     srd_result_free(out);
     set_err("host allocation failed");
     return SRD_ERR_ALLOC;
   }
-  // chain arrays: each shard's segment D2H on its own stream (file order)
-  std::vector<int> rc(nc, 0);
-  auto pull = [&](uint32_t i) {
+  // chain segments D2H on each shard's stream (file order); the merged
+  // index from ctxs[0]
+  std::vector<uint64_t> cb(nc, 0);
+  for (uint32_t i = 1; i < nc; i++) cb[i] = cb[i - 1] + sr[i - 1].n_chain;
+  parallel_for(nc, [&](uint32_t i) {
     srd_ctx* c = ctxs[i];
-    const srd_device_result& r = sh[i].r;
+    const srd_device_result& r = sr[i];
     const uint64_t n = r.n_chain, b = cb[i];
-    if (!n) return;
+    const uint64_t nk = i == 0 ? sum.n_index : 0;
+    if (!n && !nk) return;
     if (hipSetDevice(c->device) != hipSuccess) { rc[i] = SRD_ERR_HIP; return; }
     hipError_t e = hipSuccess;
     auto cp = [&](void* dst, const void* src, uint64_t bytes) {
-      if (e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
+      if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
     };
     cp(out->meta_off + b, r.meta_off, n * 8);
     cp(out->key_hash + b, r.key_hash, n * 8);
@@ -1580,62 +1916,20 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
     cp(out->crc_stored + b, r.crc_stored, n * 4);
     cp(out->crc_computed + b, r.crc_computed, n * 4);
     cp(out->crc_ok + b, r.crc_ok, n);
+    cp(out->index_key_hash, sum.index_key_hash, nk * 8);
+    cp(out->index_packed, sum.index_packed, nk * 8);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) rc[i] = SRD_ERR_HIP;
-  };
-  {
-    std::vector<std::thread> th;
-    for (uint32_t i = 1; i < nc; i++) th.emplace_back(pull, i);
-    pull(0);
-    for (auto& t : th) t.join();
-  }
+  });
   for (uint32_t i = 0; i < nc; i++)
-    if (rc[i]) { srd_result_free(out); set_err("chain copy failed"); return rc[i]; }
-  // index: the shards' indexes to ctxs[0] in shard order, then latest wins
-  Ctx* c0 = ctxs[0];
-  int r = 0;
-  uint64_t ni = 0;
-  do {
-    if (hipSetDevice(c0->device) != hipSuccess) { r = SRD_ERR_HIP; set_err("hipSetDevice"); break; }
-    const uint64_t m1 = std::max<uint64_t>(NI, 1);
-    if ((r = ensure(c0, B_GKEY, m1 * 8)) || (r = ensure(c0, B_GVAL, m1 * 8)) || (r = ensure(c0, B_GOKEY, m1 * 8)) ||
-        (r = ensure(c0, B_GOPACKED, m1 * 8)))
-      break;
-    hipError_t e = hipSuccess;
-    for (uint32_t i = 0; i < nc && e == hipSuccess; i++) {
-      const uint64_t n = sh[i].r.n_index;
-      if (!n) continue;
-      enable_peer(c0->device, ctxs[i]->device);
-      e = hipMemcpyPeerAsync(P<uint64_t>(c0, B_GKEY) + ib[i], c0->device, sh[i].r.index_key_hash, ctxs[i]->device,
-                             n * 8, c0->stream);
-      if (e == hipSuccess)
-        e = hipMemcpyPeerAsync(P<uint64_t>(c0, B_GVAL) + ib[i], c0->device, sh[i].r.index_packed, ctxs[i]->device,
-                               n * 8, c0->stream);
-    }
-    if (e != hipSuccess) { r = SRD_ERR_HIP; set_err(std::string("index gather: ") + hipGetErrorString(e)); break; }
-    if ((r = index_build_sep(c0, P<uint64_t>(c0, B_GKEY), P<uint64_t>(c0, B_GVAL), NI, P<uint64_t>(c0, B_GOKEY),
-                             P<uint64_t>(c0, B_GOPACKED), &ni)))
-      break;
-    const uint64_t k1 = std::max<uint64_t>(ni, 1);
-    out->index_key_hash = (uint64_t*)malloc(k1 * 8);
-    out->index_packed = (uint64_t*)malloc(k1 * 8);
-    if (!out->index_key_hash || !out->index_packed) { r = SRD_ERR_ALLOC; set_err("host allocation failed"); break; }
-    if (ni) {
-      e = hipMemcpyAsync(out->index_key_hash, P<uint64_t>(c0, B_GOKEY), ni * 8, hipMemcpyDeviceToHost, c0->stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(out->index_packed, P<uint64_t>(c0, B_GOPACKED), ni * 8, hipMemcpyDeviceToHost, c0->stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
-      if (e != hipSuccess) { r = SRD_ERR_HIP; set_err("index copy failed"); break; }
-    }
-  } while (0);
-  if (r) { srd_result_free(out); return r; }
+    if (rc[i]) { srd_result_free(out); set_err("result copy failed"); return rc[i]; }
   out->file_len = flen;
-  out->final_len = flen;
+  out->final_len = sum.final_len;
   out->n_chain = N;
-  out->n_index = ni;
-  out->n_crc_bad = bad;
-  out->n_candidates = cand;
-  out->mode = all_opt ? SRD_MODE_OPTIMISTIC : SRD_MODE_FULL;
+  out->n_index = sum.n_index;
+  out->n_crc_bad = sum.n_crc_bad;
+  out->n_candidates = sum.n_candidates;
+  out->mode = sum.mode;
   return 0;
 }
 

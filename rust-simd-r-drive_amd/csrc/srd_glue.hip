@@ -930,7 +930,8 @@ struct PartArgs {
   uint32_t world;
   uint32_t* cnt;  // [world * GLUE_BLOCKS + 1], owner-major
   uint32_t* off;  // exclusive scan of cnt
-  uint64_t* out;  // [2n] interleaved (key, value), grouped by owner
+  uint64_t* out;  // [2n] interleaved (key, value), grouped by owner; or [n] keys when out_v is set
+  uint64_t* out_v;   // nullable: [n] values (separate arrays: an owner pulls its run with two plain copies)
   uint64_t* counts;  // [world]
 };
 __global__ __launch_bounds__(256) void part_count_kernel(PartArgs a) {
@@ -961,8 +962,13 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(PartArgs a) {
       const uint32_t r = block_rank256(own == o, wsum, &tot);
       if (own == o) {
         const uint64_t pos = (uint64_t)run[o] + r;
-        a.out[2 * pos] = k;
-        a.out[2 * pos + 1] = a.vals[i];
+        if (a.out_v) {
+          a.out[pos] = k;
+          a.out_v[pos] = a.vals[i];
+        } else {
+          a.out[2 * pos] = k;
+          a.out[2 * pos + 1] = a.vals[i];
+        }
       }
       __syncthreads();
       if (threadIdx.x == 0) run[o] += tot;

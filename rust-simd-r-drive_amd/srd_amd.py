@@ -37,6 +37,8 @@ TIMING_NONE, TIMING_SCAN, TIMING_CALL = 0, 1, 2  # srd_ctx_set_timing levels
 SRD_MODE_OPTIMISTIC = 0
 SRD_MODE_FULL = 1
 SRD_MODE_SPAN_UNPROVEN = 3
+SRD_FLAG_MERGE_INDEX = 16  # multi-GPU open: the whole index on ctxs[0] (default: by owner)
+SRD_MULTI_COMPOSED, SRD_MULTI_NEIGHBOUR, SRD_MULTI_WHOLE_FILE = 0, 1, 2  # srd_multi_summary.path
 SPAN_ALIGN = 16384  # span_off granularity of srd_validate_span_device
 METADATA_SIZE = 20
 NULL_BYTE = b"\x00"
@@ -57,6 +59,7 @@ EXPORTS = [
     "srd_batch_read_hashed_device", "srd_batch_read",
     "srd_iter_entries_device", "srd_estimate_compaction_savings_device", "srd_compact_device",
     "srd_shard_cuts", "srd_validate_index_multi", "srd_ctx_stage_info", "srd_index_hash_device",
+    "srd_validate_index_multi_device", "srd_ctx_multi_summary",
 ]
 
 
@@ -68,6 +71,18 @@ class DeviceResult(C.Structure):
         ("meta_off", C.c_void_p), ("key_hash", C.c_void_p), ("prev_offset", C.c_void_p),
         ("payload_start", C.c_void_p), ("payload_len", C.c_void_p),
         ("crc_stored", C.c_void_p), ("crc_computed", C.c_void_p), ("crc_ok", C.c_void_p),
+        ("index_key_hash", C.c_void_p), ("index_packed", C.c_void_p),
+    ]
+
+
+class MultiSummary(C.Structure):
+    """srd_multi_summary (include/srd_amd.h)"""
+    _fields_ = [
+        ("file_len", C.c_uint64), ("final_len", C.c_uint64), ("n_chain", C.c_uint64),
+        ("n_index", C.c_uint64), ("n_crc_bad", C.c_uint64), ("n_candidates", C.c_uint64),
+        ("mode", C.c_uint32), ("path", C.c_uint32), ("n_shards", C.c_uint32), ("merged", C.c_uint32),
+        ("shard_errors", C.c_uint32), ("reserved", C.c_uint32),
+        ("validate_ms", C.c_double), ("exchange_ms", C.c_double), ("total_ms", C.c_double),
         ("index_key_hash", C.c_void_p), ("index_packed", C.c_void_p),
     ]
 
@@ -135,6 +150,9 @@ def lib():
         L.srd_validate_index_multi.argtypes = [C.POINTER(vp), u32, vp, u64, u32, C.POINTER(DeviceResult)]
         L.srd_ctx_stage_info.argtypes = [vp, C.POINTER(i32), C.POINTER(C.c_double)]
         L.srd_index_hash_device.argtypes = [vp, vp, u64, vp, vp]
+        L.srd_validate_index_multi_device.argtypes = [C.POINTER(vp), u32, C.POINTER(vp), vp, vp, u32,
+                                                      C.POINTER(DeviceResult), C.POINTER(MultiSummary)]
+        L.srd_ctx_multi_summary.argtypes = [vp, C.POINTER(MultiSummary)]
         for f in EXPORTS:
             if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
                          "srd_padded_size", "srd_index_table_bytes"):
@@ -202,6 +220,12 @@ class Context:
 
     def stage_mode(self) -> str:
         return self.stage_info()[0]
+
+    def multi_summary(self) -> MultiSummary:
+        """srd_multi_summary of the last multi-GPU open with this context as ctxs[0]."""
+        m = MultiSummary()
+        _check(lib().srd_ctx_multi_summary(self.h, C.byref(m)))
+        return m
 
 
 _default_ctx = None
@@ -289,6 +313,25 @@ def validate_index_multi(file, ctxs, flags: int = 0) -> Result:
         return Result(r)
     finally:
         lib().srd_result_free(C.byref(r))
+
+
+def validate_index_multi_device(ctxs, spans, span_offs, cuts, flags: int = 0):
+    """DataStore::open of a store resident in the HBM of len(ctxs) GPUs, one
+    entry-range shard per context (srd_validate_index_multi_device; no RCCL):
+    spans[i] = device pointer of file byte span_offs[i] .. cuts[i+1] on
+    ctxs[i]'s GPU (0 for an empty shard).  Returns (shard results -- chain
+    segment i and, by default, the index part owned by i, device arrays on
+    ctxs[i]'s GPU --, MultiSummary)."""
+    n = len(ctxs)
+    hs = (C.c_void_p * n)(*[c.h.value for c in ctxs])
+    sp = (C.c_void_p * n)(*[int(x or 0) for x in spans])
+    so = np.ascontiguousarray(span_offs, np.uint64)
+    cu = np.ascontiguousarray(cuts, np.uint64)
+    assert so.size == n and cu.size == n + 1
+    res = (DeviceResult * n)()
+    summ = MultiSummary()
+    _check(lib().srd_validate_index_multi_device(hs, n, sp, _ptr(so), _ptr(cu), flags, res, C.byref(summ)))
+    return list(res), summ
 
 
 def index_hash_device(d_keys: int, n: int, d_out: int, ctx: Context | None = None) -> None:
