@@ -387,9 +387,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)  # ~55 ms timed: host-side jitter of single calls averages out
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", choices=["c2", "c3", "c5", "ops"], default="c2",
-                    help="c2: 4 KiB entries (headline); c3: Zipf-sized entries 64 B..1 MiB (variable length); "
-                         "c5: checksum-on-append batch write of 1M x 4 KiB from pinned host memory")
+    ap.add_argument("--config", choices=["c2", "c2torn", "c3", "c5", "ops"], default="c2",
+                    help="c2: 4 KiB entries (headline); c2torn: the C2 store + b'CORRUPT' (persistence_tests.rs:"
+                         "126-173: the torn-tail open, decided by the full pass); c3: Zipf-sized entries 64 B..1 MiB "
+                         "(variable length); c5: checksum-on-append batch write of 1M x 4 KiB from pinned host memory")
     ap.add_argument("--entries-per-gpu", type=int, default=None)
     ap.add_argument("--payload", type=int, default=4096)
     ap.add_argument("--no-cpu", action="store_true")
@@ -427,22 +428,28 @@ def main():
     if args.config == "ops":
         return bench_ops(args, ctx, local)
     n, L = args.entries_per_gpu, args.payload
+    torn = args.config == "c2torn"
+    if torn and world != 1:
+        sys.exit("bench.py: --config c2torn runs on one GPU")
     if n is None:  # N=1: C2 (1M x 4 KiB); N>1: the C4 partition (2^21 per GPU; N=8 is C4)
-        n = (1 << 20 if world == 1 else 1 << 21) if args.config == "c2" else 10_000_000
+        n = (1 << 20 if world == 1 else 1 << 21) if args.config in ("c2", "c2torn") else 10_000_000
     lens, seed = None, 0x5EED0001
     if args.config == "c3":
         lens, seed = S.zipf_lens(n * world), 0x5EED0004
     multi = None
     if world == 1:
         size = S.synth_store_len(n, L, lens)
-        store = torch.empty(S.padded_size(size), dtype=torch.uint8, device=f"cuda:{local}")
+        flen = size + (7 if torn else 0)  # c2torn: the tail b"CORRUPT" (persistence_tests.rs:126-173)
+        store = torch.empty(S.padded_size(flen), dtype=torch.uint8, device=f"cuda:{local}")
         S.synth_store_device(store.data_ptr(), n, L, lens, seed=seed, ctx=ctx)
+        if torn:
+            store[size:flen].copy_(torch.frombuffer(bytearray(b"CORRUPT"), dtype=torch.uint8))
         span = (0, 0, size)
 
         def step():
-            r = S.validate_index_device(store.data_ptr(), size, 0, ctx)
-            return r.final_len, r.n_chain, r.n_crc_bad, r.n_index
-        expect = (size, n, 0, n)
+            r = S.validate_index_device(store.data_ptr(), flen, 0, ctx)
+            return r.final_len, r.n_chain, r.n_crc_bad, r.n_index, r.mode
+        expect = (size, n, 0, n, S.SRD_MODE_FULL if torn else S.SRD_MODE_OPTIMISTIC)
     else:
         import ctypes as C
         import srd_shard as SH
@@ -476,8 +483,8 @@ def main():
         def step():
             S._check(S.lib().srd_validate_index_multi_device(hs, world, sp, S._ptr(so_a), S._ptr(cu_a), 0, res,
                                                              C.byref(summ)))
-            return summ.final_len, summ.n_chain, summ.n_crc_bad, summ.n_index
-        expect = (file_len, n * world, 0, n * world)
+            return summ.final_len, summ.n_chain, summ.n_crc_bad, summ.n_index, summ.path
+        expect = (file_len, n * world, 0, n * world, S.SRD_MULTI_COMPOSED)
     # algorithmic bytes, SURVEY.md 8(d): sum(L_i + 20) over every chain entry
     # of the whole store (all N shards); bytes_alg = the first shard's share
     if lens is None:
@@ -513,7 +520,8 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = bytes_total / dt * args.steps / 2**30
     scan_ms = scan_ms_sum / max(scan_n, 1)
-    if multi is not None:  # the slowest shard's scan bounds the step
+    if torn:  # both passes' scans per step (the optimistic pass fails, the full pass decides)
+        scan_ms = scan_ms_sum / args.steps  # the slowest shard's scan bounds the step
         shard_scan = [x / max(multi["n"], 1) for x in multi["scan_ms"]]
         scan_ms = max(shard_scan)
     achieved = bytes_alg / (scan_ms * 1e-3) / 1e9
@@ -545,7 +553,9 @@ def main():
         "data": "synthetic (counter-mode splitmix64 payloads, keys bench-key-{i}), generated in HBM",
         "config": {
             "workload": (f"{args.config.upper()}: {n} x " + (f"{L} B" if lens is None else "Zipf 64 B..1 MiB") +
-                         f" entries, {size} B store, validate+index (recover_valid_chain + CRC-32 every payload + "
+                         f" entries, {size} B store" + (" + the 7-byte torn tail b'CORRUPT' (recovered: final_len = "
+                                                        f"{size}, the full pass)" if torn else "") +
+                         ", validate+index (recover_valid_chain + CRC-32 every payload + "
                          f"KeyIndexer::build)") if world == 1 else
                         ((f"C4 partition ({'= C4' if world == 8 else f'prefix of C4, {world} of its 8 shards'})"
                           if args.config == "c2" and n == 1 << 21 and L == 4096 else args.config.upper()) +
@@ -562,8 +572,10 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "scan_kernel<false>",
+            "kernel": "scan_kernel<false> + scan_kernel<true> (both passes)" if torn else "scan_kernel<false>",
             "kernel_ms": round(scan_ms, 4),
+            "kernel_timing": "HIP events stamped with the scan dispatch's own start / stop (hipExtLaunchKernel) "
+                             "on the library stream, every timed step",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

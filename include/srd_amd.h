@@ -77,11 +77,11 @@ void srd_ctx_destroy(srd_ctx *ctx);
 /* The HIP stream the context launches on (hipStream_t as void*). */
 void *srd_ctx_stream(srd_ctx *ctx);
 const char *srd_last_error(void);
-/* HIP-event timing of the validate calls on ctx (each event record costs
- * ~10 us of a call's wall time): SRD_TIMING_NONE (the default),
- * SRD_TIMING_SCAN (the streaming scan's launches: bench.py's roofline),
- * SRD_TIMING_CALL (+ the device span of the whole call).  Not part of the
- * reference interface. */
+/* HIP-event timing of the validate calls on ctx: SRD_TIMING_NONE (the
+ * default), SRD_TIMING_SCAN (the streaming scan's launches: events stamped by
+ * the scan dispatch itself, hipExtLaunchKernel -- bench.py's roofline),
+ * SRD_TIMING_CALL (+ marker events around the whole call, ~10 us each).  Not
+ * part of the reference interface. */
 #define SRD_TIMING_NONE 0
 #define SRD_TIMING_SCAN 1
 #define SRD_TIMING_CALL 2
@@ -105,7 +105,7 @@ typedef struct {
   uint64_t n_candidates;   /* chain-node candidates recorded by the scan */
   uint64_t n_weak;         /* reserved (0) */
   uint32_t mode;           /* 0 = optimistic pass sufficed, 1 = full pass */
-  uint32_t reserved;
+  uint32_t reserved;       /* host results: 1 = arrays owned by the context */
   /* chain, file order; device pointers */
   uint64_t *meta_off, *key_hash, *prev_offset, *payload_start, *payload_len;
   uint32_t *crc_stored, *crc_computed;
@@ -175,8 +175,12 @@ int srd_index_build_device(srd_ctx *ctx, const uint64_t *d_pairs, uint64_t n,
                            uint64_t *d_out_keys, uint64_t *d_out_packed,
                            uint64_t *n_index);
 
-/* Same result with host-memory arrays (malloc'd; free with srd_result_free).
- * `file` is host memory (e.g. the mmap); it is staged to HBM inside. */
+/* Same result with host-memory arrays.  `file` is host memory (e.g. the
+ * mmap); it is staged to HBM inside.  The arrays live in pinned host memory
+ * owned by the context (ctxs[0] for the multi-GPU form), DMA'd there straight
+ * from HBM: valid until the next srd_validate_index(_multi) call on that
+ * context; srd_result_free releases nothing then, it only clears the struct
+ * (reserved == 1 marks such a result). */
 typedef srd_device_result srd_result;
 int srd_validate_index(srd_ctx *ctx, const uint8_t *file, uint64_t file_len,
                        uint32_t flags, srd_result *out);

@@ -4,6 +4,7 @@
 // Glue scans/compactions use hipCUB (library primitives, like calling
 // rocBLAS for a plain GEMM); every byte-touching hot kernel is hand-written
 // in srd_kernels.hip.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -104,6 +105,8 @@ struct Ctx {
   std::vector<hipStream_t> stage_streams;
   std::vector<hipEvent_t> stage_ev;
   srd_multi_summary last_multi{};  // the last multi-GPU open with this context as ctxs[0]
+  void* h_out = nullptr;  // pinned host result arrays (srd_validate_index / _multi)
+  uint64_t h_out_n = 0;
 };
 
 enum BufId {
@@ -225,12 +228,26 @@ int ensure_cub(Ctx* c, uint64_t n) {
 // stores above 2^40 bytes take the WIDE scan (48-bit prev offsets)
 constexpr uint64_t kWide = 1ull << 40;
 constexpr uint64_t kMaxFile = 1ull << 48;  // packed offsets are 48-bit (key_indexer.rs:12-15, 79-85)
+// With timing events, the scan is launched by hipExtLaunchKernel, which
+// stamps the events with the kernel's own start and stop (the dispatch
+// packet's, as rocprofv3 sees them) instead of marker packets around it: a
+// marker recorded on an idle stream before the launch runs while the host is
+// still submitting the kernel (+30 us on the bracket), and one after it
+// delays the next kernel (~6 us per call).
 template <bool FULL>
-static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s) {
-  if (a.flen > kWide)
-    scan_kernel<FULL, true><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(a);
-  else
-    scan_kernel<FULL, false><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(a);
+static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
+                        hipEvent_t e1 = nullptr) {
+  const dim3 grid(g), block(SCAN_WAVES_V2 * 64);
+  if (e0) {
+    if (a.flen > kWide)
+      hipExtLaunchKernelGGL(scan_kernel<FULL, true>, grid, block, 0, s, e0, e1, 0, a);
+    else
+      hipExtLaunchKernelGGL(scan_kernel<FULL, false>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.flen > kWide) {
+    scan_kernel<FULL, true><<<grid, block, 0, s>>>(a);
+  } else {
+    scan_kernel<FULL, false><<<grid, block, 0, s>>>(a);
+  }
 }
 
 static bool debug_env() {
@@ -343,6 +360,7 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->h_plan) hipHostFree(c->h_plan);
+  if (c->h_out) hipHostFree(c->h_out);
   for (int i = 0; i < 2; i++) {
     if (c->pin_ent[i]) hipHostFree(c->pin_ent[i]);
     if (c->wev_copied[i]) hipEventDestroy(c->wev_copied[i]);
@@ -596,14 +614,13 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     TRY(scan_wave_args(c, &a));
     if (n_spans) {
       unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
-      if (c->timing >= SRD_TIMING_SCAN) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+      hipEvent_t e0 = c->timing >= SRD_TIMING_SCAN ? c->ev[0] : nullptr;
       if (full)
-        launch_scan<true>(g, a, c->stream);
+        launch_scan<true>(g, a, c->stream, e0, c->ev[1]);
       else
-        launch_scan<false>(g, a, c->stream);
+        launch_scan<false>(g, a, c->stream, e0, c->ev[1]);
       KCHK(c, "scan_kernel");
       HIPCHK(hipGetLastError());
-      if (c->timing >= SRD_TIMING_SCAN) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     }
     size_t tb = c->bufs[B_CUB_TMP].n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_SPAN_COUNT),
@@ -674,8 +691,10 @@ static int alloc_index(Ctx* c, uint64_t n_cap, uint32_t log2_nbk) {
   TRY(ensure(c, B_LATEST8, n_cap + 1));
   return 0;
 }
+// the words every index build needs zeroed: the bucket fills and, after them,
+// the per-chunk non-latest counts (IdxArgs::ccount)
 static uint32_t* index_zero_words(Ctx* c, uint32_t log2_nbk, uint32_t* n) {
-  *n = 1u << log2_nbk;
+  *n = (1u << log2_nbk) + GLUE_BLOCKS;
   return P<uint32_t>(c, B_HOFF);
 }
 static uint32_t index_log2_buckets(uint64_t n_est) {
@@ -718,8 +737,6 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   }
   idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
   KCHK(c, "idx_dedup_kernel");
-  idx_count_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
-  KCHK(c, "idx_count_kernel");
   idx_emit_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
   KCHK(c, "idx_emit_kernel");
   HIPCHK(hipGetLastError());
@@ -776,6 +793,8 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
     const uint64_t spw = (ns_rel + total_waves - 1) / total_waves;
     const uint64_t wcap = spw * c->cap;
+    // the glue's record slots are 32-bit (d_slot): stores above ~1 TiB take the full pass
+    if (total_waves * wcap >= (1ull << 32)) return 0;
     TRY(alloc_scan(c, nt_rel, std::max<uint64_t>(ns_rel, total_waves * spw)));
     TRY(ensure(c, B_SPAN_FIRST, (ns_rel + 1) * 4));
     TRY(alloc_fast(c, capK, log2_nbk));
@@ -812,11 +831,9 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.n_zero_words = (uint32_t)(sizeof(Plan) / 4);
     a.sentinel = nullptr;
     TRY(scan_wave_args(c, &a));
-    if (c->timing >= SRD_TIMING_SCAN) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    launch_scan<false>(g, a, c->stream);
+    launch_scan<false>(g, a, c->stream, c->timing >= SRD_TIMING_SCAN ? c->ev[0] : nullptr, c->ev[1]);
     KCHK(c, "scan_kernel");
     HIPCHK(hipGetLastError());
-    if (c->timing >= SRD_TIMING_SCAN) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     Link2Args l{};
     l.file = d_file;
     l.flen = flen;
@@ -831,11 +848,12 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.wcap = wcap;
     l.c_m = a.c_m;
     l.c_rec = a.c_rec;
-    l.d_par = P<int64_t>(c, B_DPAR);
-    l.d_slot = P<uint64_t>(c, B_DSLOT);
-    l.has_child = P<uint32_t>(c, B_HASCHILD);
+    l.d_par = P<int32_t>(c, B_DPAR);
+    l.d_slot = P<uint32_t>(c, B_DSLOT);
+    l.childof = P<unsigned long long>(c, B_CHILDOF);
     l.s_lo = s_lo;
     l.span_lo = lo;
+    l.zero = index_zero_words(c, log2_nbk, &l.n_zero);  // chain_finalize claims the bucket fills
     link2_kernel<<<blocks(ns_rel, 64), 256, 0, c->stream>>>(l);
     KCHK(c, "link2_kernel");
     // ---- shape check, chain, finalize, index; retried on device with more
@@ -865,19 +883,31 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       sa.counters = (const unsigned long long*)cnt;
       sa.plan = pl;
       sa.zero = index_zero_words(c, log2_nbk, &sa.n_zero);  // child2 zeroes the index's bucket fills
-      for (int r = 0; r < (rounds ? 2 : 0); r++) {  // two more prune rounds per retry
+      if (rounds == 0) {
+        // round 0: link2's claims (every node claims its parent) are the
+        // core flags and the branch test; no marks
+        sa.has_child = nullptr;
+        sa.gen = mgen;
+      } else {
+        if (rounds == 2) {  // the retry's first marks: the nodes link2 claims were made on
+          sa.gen = mgen;
+          marks_from_claims_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa, marks);
+          KCHK(c, "marks_from_claims_kernel");
+        }
+        for (int r = 0; r < 2; r++) {  // two more prune rounds per retry
+          sa.has_child = marks;
+          sa.gen = mgen;
+          const uint32_t g2 = ++c->gen;
+          prune_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa, marks2, g2);
+          KCHK(c, "prune_kernel");
+          std::swap(marks, marks2);
+          mgen = g2;
+        }
         sa.has_child = marks;
         sa.gen = mgen;
-        const uint32_t g2 = ++c->gen;
-        prune_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa, marks2, g2);
-        KCHK(c, "prune_kernel");
-        std::swap(marks, marks2);
-        mgen = g2;
+        child2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);  // core-only claims
+        KCHK(c, "child2_kernel");
       }
-      sa.has_child = marks;
-      sa.gen = mgen;
-      child2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);
-      KCHK(c, "child2_kernel");
       check_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, 0, c->stream>>>(sa);
       KCHK(c, "check_kernel");
       HIPCHK(hipGetLastError());
@@ -924,10 +954,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
                 (unsigned long)hp.K, (unsigned long)hp.n_chain, (unsigned long)hp.root_t, (unsigned long)hp.start,
                 (unsigned long)hp.n_index, (unsigned long)hp.n_bad, (unsigned long)hp.n_slow, hp.status, hp.nroot,
                 hp.troot, hp.idx_overflow, log2_nbk, (unsigned long)capK, rounds);
-        fprintf(stderr, "shape: dangling=%u branch=%u nochild=%u\n", hp.why[0], hp.why[1], hp.why[2]);
-        for (uint32_t w = 0; w < std::min(hp.ndbg, 8u); w++)
-          fprintf(stderr, "  dangling g=%lu m=%lu p=%lu\n", (unsigned long)hp.dbg_g[w], (unsigned long)hp.dbg[2 * w],
-                  (unsigned long)hp.dbg[2 * w + 1]);
+        fprintf(stderr, "shape: dangling=%u branch=%u\n", hp.why[0], hp.why[1]);
       }
       if (!timed && c->timing >= SRD_TIMING_SCAN) {
         float ms = 0;
@@ -1171,7 +1198,18 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
                                                               P<int64_t>(c, B_JMP));
     KCHK(c, "status_init_kernel");
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
-    for (int round = 0; round < 80; round++) {
+    // pointer jumping: every round doubles how far each unresolved node
+    // looks along its parent chain, so ceil(log2 K) + 1 rounds resolve every
+    // node; they run back to back and one more round, with the change flag
+    // cleared before it, proves convergence with a single host sync
+    int rounds = 1;
+    while ((1ull << rounds) < K) rounds++;
+    for (int pass = 0; pass < 8; pass++) {
+      for (int r = 0; r <= (pass ? 0 : rounds); r++) {
+        status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, P<uint8_t>(c, B_ST), P<int64_t>(c, B_JMP),
+                                                                   (unsigned int*)(cnt + 4));
+        KCHK(c, "status_round_kernel");
+      }
       HIPCHK(hipMemsetAsync(cnt + 4, 0, 8, c->stream));
       status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, P<uint8_t>(c, B_ST), P<int64_t>(c, B_JMP),
                                                                  (unsigned int*)(cnt + 4));
@@ -1179,6 +1217,7 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
       HIPCHK(hipGetLastError());
       TRY(read_counters(c, h));
       if (!h[4]) break;
+      if (pass == 7) { set_err("internal: pointer jumping did not converge"); return SRD_ERR_INTERNAL; }
     }
     HIPCHK(hipMemsetAsync(cnt + 3, 0, 8, c->stream));
     valid_max_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<uint8_t>(c, B_ST), P<uint64_t>(c, B_DM), K,
@@ -1382,12 +1421,57 @@ static int stage_host_impl(Ctx* c, const uint8_t* src, uint64_t len, uint32_t fl
   return stage_bounce(c, src, len, d, workers);
 }
 
-template <class T>
-static T* d2h(Ctx* c, const T* d, uint64_t n, int* rc) {
-  T* h = (T*)malloc(std::max<uint64_t>(n, 1) * sizeof(T));
-  if (!h) { *rc = SRD_ERR_ALLOC; return nullptr; }
-  if (n && hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, c->stream) != hipSuccess) *rc = SRD_ERR_HIP;
-  return h;
+// Host results live in one pinned buffer the context owns (valid until the
+// next host-input call on it): the device arrays are DMA'd straight into it
+// -- no malloc'd pageable destinations (the runtime's own staging and their
+// first-touch page faults cost ~10 ms of a C2 open) -- and srd_result_free
+// only clears the struct (SRD_RESULT_CTX_OWNED in `reserved`).
+constexpr uint32_t SRD_RESULT_CTX_OWNED = 1u;
+static int host_result_arrays(Ctx* c, uint64_t n, uint64_t ni, srd_result* out) {
+  const uint64_t n1 = std::max<uint64_t>(n, 1), k1 = std::max<uint64_t>(ni, 1);
+  const uint64_t need = n1 * (5 * 8 + 2 * 4 + 1) + k1 * 16 + 64;
+  if (c->h_out_n < need) {
+    if (c->h_out) HIPCHK(hipHostFree(c->h_out));
+    c->h_out = nullptr;
+    c->h_out_n = 0;
+    if (hipHostMalloc(&c->h_out, need, hipHostMallocDefault) != hipSuccess) {
+      set_err("hipHostMalloc(results) failed");
+      return SRD_ERR_ALLOC;
+    }
+    c->h_out_n = need;
+  }
+  uint8_t* b = (uint8_t*)c->h_out;
+  auto take = [&](uint64_t bytes) { uint8_t* p = b; b += (bytes + 7) & ~7ull; return p; };
+  out->meta_off = (uint64_t*)take(n1 * 8);
+  out->key_hash = (uint64_t*)take(n1 * 8);
+  out->prev_offset = (uint64_t*)take(n1 * 8);
+  out->payload_start = (uint64_t*)take(n1 * 8);
+  out->payload_len = (uint64_t*)take(n1 * 8);
+  out->index_key_hash = (uint64_t*)take(k1 * 8);
+  out->index_packed = (uint64_t*)take(k1 * 8);
+  out->crc_stored = (uint32_t*)take(n1 * 4);
+  out->crc_computed = (uint32_t*)take(n1 * 4);
+  out->crc_ok = (uint8_t*)take(n1);
+  out->reserved = SRD_RESULT_CTX_OWNED;
+  return 0;
+}
+
+// chain entries [0, n) of a device result into host result entries [b, b + n)
+static hipError_t copy_chain_d2h(hipStream_t st, const srd_device_result& r, uint64_t n, srd_result* out,
+                                 uint64_t b) {
+  hipError_t e = hipSuccess;
+  auto cp = [&](void* dst, const void* src, uint64_t bytes) {
+    if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+  };
+  cp(out->meta_off + b, r.meta_off, n * 8);
+  cp(out->key_hash + b, r.key_hash, n * 8);
+  cp(out->prev_offset + b, r.prev_offset, n * 8);
+  cp(out->payload_start + b, r.payload_start, n * 8);
+  cp(out->payload_len + b, r.payload_len, n * 8);
+  cp(out->crc_stored + b, r.crc_stored, n * 4);
+  cp(out->crc_computed + b, r.crc_computed, n * 4);
+  cp(out->crc_ok + b, r.crc_ok, n);
+  return e;
 }
 
 extern "C" int srd_validate_index(srd_ctx* c, const uint8_t* file, uint64_t flen, uint32_t flags, srd_result* out) {
@@ -1398,27 +1482,22 @@ extern "C" int srd_validate_index(srd_ctx* c, const uint8_t* file, uint64_t flen
   srd_device_result r;
   TRY(srd_validate_index_device(c, d, flen, flags & ~kStageFlags, &r));
   *out = r;
-  int rc = 0;
-  uint64_t n = r.n_chain, ni = r.n_index;
-  out->meta_off = d2h(c, r.meta_off, n, &rc);
-  out->key_hash = d2h(c, r.key_hash, n, &rc);
-  out->prev_offset = d2h(c, r.prev_offset, n, &rc);
-  out->payload_start = d2h(c, r.payload_start, n, &rc);
-  out->payload_len = d2h(c, r.payload_len, n, &rc);
-  out->crc_stored = d2h(c, r.crc_stored, n, &rc);
-  out->crc_computed = d2h(c, r.crc_computed, n, &rc);
-  out->crc_ok = d2h(c, r.crc_ok, n, &rc);
-  out->index_key_hash = d2h(c, r.index_key_hash, ni, &rc);
-  out->index_packed = d2h(c, r.index_packed, ni, &rc);
+  TRY(host_result_arrays(c, r.n_chain, r.n_index, out));
+  HIPCHK(copy_chain_d2h(c->stream, r, r.n_chain, out, 0));
+  if (r.n_index) {
+    HIPCHK(hipMemcpyAsync(out->index_key_hash, r.index_key_hash, r.n_index * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->index_packed, r.index_packed, r.n_index * 8, hipMemcpyDeviceToHost, c->stream));
+  }
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (rc) { set_err("result copy failed"); srd_result_free(out); }
-  return rc;
+  return 0;
 }
 
 extern "C" void srd_result_free(srd_result* r) {
   if (!r) return;
-  free(r->meta_off); free(r->key_hash); free(r->prev_offset); free(r->payload_start); free(r->payload_len);
-  free(r->crc_stored); free(r->crc_computed); free(r->crc_ok); free(r->index_key_hash); free(r->index_packed);
+  if (!(r->reserved & SRD_RESULT_CTX_OWNED)) {
+    free(r->meta_off); free(r->key_hash); free(r->prev_offset); free(r->payload_start); free(r->payload_len);
+    free(r->crc_stored); free(r->crc_computed); free(r->crc_ok); free(r->index_key_hash); free(r->index_packed);
+  }
   memset(r, 0, sizeof *r);
 }
 
@@ -1876,48 +1955,22 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
   TRY(multi_device_impl(in, (flags & ~kStageFlags) | SRD_FLAG_MERGE_INDEX, sr.data(), &sum));
 
   memset(out, 0, sizeof *out);
-  const uint64_t N = sum.n_chain, n1 = std::max<uint64_t>(N, 1), k1 = std::max<uint64_t>(sum.n_index, 1);
-  out->meta_off = (uint64_t*)malloc(n1 * 8);
-  out->key_hash = (uint64_t*)malloc(n1 * 8);
-  out->prev_offset = (uint64_t*)malloc(n1 * 8);
-  out->payload_start = (uint64_t*)malloc(n1 * 8);
-  out->payload_len = (uint64_t*)malloc(n1 * 8);
-  out->crc_stored = (uint32_t*)malloc(n1 * 4);
-  out->crc_computed = (uint32_t*)malloc(n1 * 4);
-  out->crc_ok = (uint8_t*)malloc(n1);
-  out->index_key_hash = (uint64_t*)malloc(k1 * 8);
-  out->index_packed = (uint64_t*)malloc(k1 * 8);
-  if (!out->meta_off || !out->key_hash || !out->prev_offset || !out->payload_start || !out->payload_len ||
-      !out->crc_stored || !out->crc_computed || !out->crc_ok || !out->index_key_hash || !out->index_packed) {
-    srd_result_free(out);
-    set_err("host allocation failed");
-    return SRD_ERR_ALLOC;
-  }
+  const uint64_t N = sum.n_chain;
+  TRY(host_result_arrays(ctxs[0], N, sum.n_index, out));
   // chain segments D2H on each shard's stream (file order); the merged
   // index from ctxs[0]
   std::vector<uint64_t> cb(nc, 0);
   for (uint32_t i = 1; i < nc; i++) cb[i] = cb[i - 1] + sr[i - 1].n_chain;
   parallel_for(nc, [&](uint32_t i) {
     srd_ctx* c = ctxs[i];
-    const srd_device_result& r = sr[i];
-    const uint64_t n = r.n_chain, b = cb[i];
     const uint64_t nk = i == 0 ? sum.n_index : 0;
-    if (!n && !nk) return;
+    if (!sr[i].n_chain && !nk) return;
     if (hipSetDevice(c->device) != hipSuccess) { rc[i] = SRD_ERR_HIP; return; }
-    hipError_t e = hipSuccess;
-    auto cp = [&](void* dst, const void* src, uint64_t bytes) {
-      if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
-    };
-    cp(out->meta_off + b, r.meta_off, n * 8);
-    cp(out->key_hash + b, r.key_hash, n * 8);
-    cp(out->prev_offset + b, r.prev_offset, n * 8);
-    cp(out->payload_start + b, r.payload_start, n * 8);
-    cp(out->payload_len + b, r.payload_len, n * 8);
-    cp(out->crc_stored + b, r.crc_stored, n * 4);
-    cp(out->crc_computed + b, r.crc_computed, n * 4);
-    cp(out->crc_ok + b, r.crc_ok, n);
-    cp(out->index_key_hash, sum.index_key_hash, nk * 8);
-    cp(out->index_packed, sum.index_packed, nk * 8);
+    hipError_t e = copy_chain_d2h(c->stream, sr[i], sr[i].n_chain, out, cb[i]);
+    if (e == hipSuccess && nk)
+      e = hipMemcpyAsync(out->index_key_hash, sum.index_key_hash, nk * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && nk)
+      e = hipMemcpyAsync(out->index_packed, sum.index_packed, nk * 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) rc[i] = SRD_ERR_HIP;
   });

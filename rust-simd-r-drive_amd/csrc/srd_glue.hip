@@ -45,10 +45,7 @@ struct Plan {
   uint32_t nroot;      // core nodes linking to a root
   uint32_t troot;      // file_len itself is a root tail
   uint32_t idx_overflow;
-  uint32_t why[3];     // shape failures (diagnostics): dangling parent, branch, core node without core child
-  uint32_t ndbg;
-  uint64_t dbg[16];    // (m, p) of the first dangling core nodes
-  uint64_t dbg_g[8];   // their dense indices
+  uint32_t why[2];     // shape failures (diagnostics): dangling parent, branch
 };
 constexpr uint32_t ST_NOSTART = 1, ST_SHAPE = 2, ST_ROOTS = 4, ST_CAPK = 8, ST_OVERFLOW = 16;
 constexpr uint64_t NO_NODE = ~0ull;
@@ -179,17 +176,30 @@ struct Link2Args {
   uint64_t wcap;               // record slots per scan wave
   const uint64_t* c_m;
   u32x4* c_rec;  // tombstone flags are set in place
-  int64_t* d_par;
-  uint64_t* d_slot;
-  uint32_t* has_child;
+  int32_t* d_par;              // dense parent (PAR_ROOT / PAR_MISS)
+  uint32_t* d_slot;            // dense node -> record slot (< 2^32: the host checks)
+  unsigned long long* childof; // [capK] (gen << 32) | child: every node claims its parent (atomicMax)
   uint64_t s_lo;     // first resident span (span mode)
   uint64_t span_lo;  // span mode: the shard's lower tail (a node with p == span_lo is the shard's first entry); 0 = whole file
+  uint32_t* zero;    // zeroed here: the index's bucket fills (chain_finalize claims them)
+  uint32_t n_zero;
 };
 
 // 4 lanes per span.  The scan wrote each wave's records densely in file
 // order: record i of span sp lives at slot w*wcap + span_first[sp] + i and
 // has the dense index wave_base[w] + span_first[sp] + i.
+//
+// Every node with a parent claims it: childof[p] = max((gen << 32) | g).
+// check_kernel reads a node's core flag (someone links to it) and the claim
+// on its parent from these words alone -- no separate marking pass.  A
+// parent claimed by two nodes keeps the larger; if the loser is a chain node
+// the shape check fails and the retry rounds (prune + core-only claims)
+// decide, so the claim order never changes a result.
 __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
+  {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+    for (uint32_t i = t; i < a.n_zero; i += nt) a.zero[i] = 0;
+  }
   const uint64_t sp = a.s_lo + (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
   if (sp >= a.n_spans) return;
   const uint64_t w = (sp - a.s_lo) / a.spw;
@@ -247,9 +257,9 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
         par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
       }
     }
-    a.d_par[g] = par;
-    a.d_slot[g] = gi;
-    if (par >= 0 && (uint64_t)par < a.capK) a.has_child[par] = a.gen;
+    a.d_par[g] = (int32_t)par;
+    a.d_slot[g] = (uint32_t)gi;
+    if (par >= 0 && (uint64_t)par < a.capK) atomicMax(&a.childof[par], ((unsigned long long)a.gen << 32) | g);
   }
 }
 
@@ -259,10 +269,10 @@ struct ShapeArgs {
   uint32_t gen;
   const uint64_t* Kp;  // span_base + n_spans
   const uint64_t* c_m;  // the records' metadata offsets (slot d_slot[g])
-  const int64_t* d_par;
-  const uint64_t* d_slot;
+  const int32_t* d_par;
+  const uint32_t* d_slot;
   const u32x4* c_rec;
-  const uint32_t* has_child;
+  const uint32_t* has_child;  // retry rounds: the prune marks
   uint64_t* childof;
   uint8_t* flag;
   uint32_t* part;
@@ -290,6 +300,14 @@ __device__ __forceinline__ bool is_core(const ShapeArgs& a, uint64_t g, uint64_t
   if (g == start) return true;
   const int64_t p = a.d_par[g];
   return a.has_child[g] == a.gen && (p >= 0 || p == PAR_ROOT);
+}
+
+// the retry's round-0 marks: the nodes link2 claims were made on
+__global__ __launch_bounds__(256) void marks_from_claims_kernel(ShapeArgs a, uint32_t* marks_out) {
+  const uint64_t K = *a.Kp;
+  if (K > a.capK) return;
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x)
+    if ((a.childof[g] >> 32) == a.gen) marks_out[g] = a.gen;
 }
 
 __global__ __launch_bounds__(256) void prune_kernel(ShapeArgs a, uint32_t* marks_out, uint32_t gen_out) {
@@ -329,18 +347,33 @@ __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
   }
 }
 
+// The core nodes (the start node, and every node something links to whose own
+// parent was found) must form ONE chain from the start down to one root:
+//   (1) a core node's parent is a core node (else: dangling),
+//   (2) it holds the claim on its parent (else: another node claims it -- a
+//       branch, or a leaf that won the claim: the retry rounds decide),
+//   (3) exactly one core node links to a root (nroot, chain_finalize).
+// Then following parents from any core node ends at that root, and no node
+// has two core children: the core set is a single path, and its top is the
+// start node (no node lies above file_len - 20), so every core node but the
+// start has a core child without a test of its own.  Leaves (false
+// candidates nobody links to) are ignored -- recover_valid_chain's walk only
+// follows back-pointers from file_len (data_store.rs:404-470).  Round 0
+// reads the claims link2 made (core: (childof[g] >> 32) == gen); the retry
+// rounds, the prune marks and child2's core-only claims.
 __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
   __shared__ uint32_t wsum[CHAIN_WAVES];
   const uint64_t K = *a.Kp;
   if (K > a.capK) return;
   const uint64_t start = start_node(a, K);
   const uint64_t tag = (uint64_t)a.gen << 32;
+  const bool marks = a.has_child != nullptr;  // retry rounds
   uint64_t lo, hi;
   chunk_of(K, &lo, &hi);
   uint32_t cnt = 0;
   bool fail = false;
   // CR nodes per thread per pass, their loads issued level by level: the
-  // node's own words (marks, parent, child claim), then its parent's
+  // node's own words (parent, claim), then its parent's
   constexpr int CR = 4;
   for (uint64_t base = lo; base < hi; base += CR * CHAIN_THREADS) {
     uint64_t g[CR], cg[CR], cp[CR];
@@ -350,46 +383,37 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
     for (int r = 0; r < CR; r++) {
       g[r] = base + (uint64_t)r * CHAIN_THREADS + threadIdx.x;
       const uint64_t gg = g[r] < hi ? g[r] : lo;
-      hc[r] = a.has_child[gg];
       par[r] = a.d_par[gg];
       cg[r] = a.childof[gg];
+      hc[r] = marks ? a.has_child[gg] : 0u;
     }
 #pragma unroll
     for (int r = 0; r < CR; r++) {
       const uint64_t q = par[r] >= 0 ? (uint64_t)par[r] : lo;
-      hp[r] = a.has_child[q];
       pp[r] = a.d_par[q];
       cp[r] = a.childof[q];
+      hp[r] = marks ? a.has_child[q] : 0u;
     }
 #pragma unroll
     for (int r = 0; r < CR; r++) {
       if (g[r] >= hi) break;
       const int64_t p = par[r];
-      const bool core = g[r] == start || (hc[r] == a.gen && (p >= 0 || p == PAR_ROOT));  // is_core(g)
+      const bool linked = marks ? hc[r] == a.gen : (cg[r] & ~0xffffffffull) == tag;
+      const bool core = g[r] == start || (linked && (p >= 0 || p == PAR_ROOT));  // is_core(g)
       a.flag[g[r]] = core;
       if (!core) continue;
       cnt++;
+      const bool plinked = marks ? hp[r] == a.gen : (cp[r] & ~0xffffffffull) == tag;
       if (p == PAR_ROOT) {
         atomicAdd(&a.plan->nroot, 1u);
-        const u32x4 r0 = a.c_rec[2 * a.d_slot[g[r]]];
+        const u32x4 r0 = a.c_rec[2 * (uint64_t)a.d_slot[g[r]]];
         a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-      } else if (p < 0 || !((uint64_t)p == start || (hp[r] == a.gen && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
+      } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
         fail = true;  // dangling: the chain through g is broken (only the start node can get here)
         atomicAdd(&a.plan->why[0], 1u);
-        const uint32_t w = atomicAdd(&a.plan->ndbg, 1u);
-        if (w < 8) {
-          const u32x4 r0 = a.c_rec[2 * a.d_slot[g[r]]];
-          a.plan->dbg[2 * w] = a.c_m[a.d_slot[g[r]]];
-          a.plan->dbg[2 * w + 1] = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-          a.plan->dbg_g[w] = g[r];
-        }
       } else if (cp[r] != (tag | g[r])) {
-        fail = true;  // branch: another core node claims the same parent
+        fail = true;  // branch: another node holds the claim on the same parent
         atomicAdd(&a.plan->why[1], 1u);
-      }
-      if (g[r] != start && (cg[r] & ~0xffffffffull) != tag) {  // core node without a core child
-        fail = true;
-        atomicAdd(&a.plan->why[2], 1u);
       }
     }
   }
@@ -424,7 +448,7 @@ struct IdxArgs {
   uint32_t* bbase;       // [IDX_HBLOCKS * nbk]
   u64x2* srec;           // (key, chain index) per entry, in its bucket's range
   uint8_t* latest;       // [n] 1 = latest entry of its key
-  uint32_t* ccount;      // [GLUE_BLOCKS] latest entries per chain chunk (idx_count -> idx_emit)
+  uint32_t* ccount;      // [GLUE_BLOCKS] NON-latest entries per chain chunk (idx_dedup -> idx_emit; zero before)
   uint64_t* okey;
   uint64_t* opacked;
   Plan* plan;
@@ -859,34 +883,34 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
     slot[r] = s;
   }
   __syncthreads();
+  // latest flags, and the per-chunk count of the entries that are NOT the
+  // latest of their key (idx_emit's prefix: position = c - non-latest before
+  // c; a store without overwrites makes no atomics here)
+  const uint64_t n = idx_n(a);
+  const uint64_t ch = n ? (n + GLUE_BLOCKS - 1) / GLUE_BLOCKS : 1;  // chunk_of's chunk at GLUE_BLOCKS blocks
 #pragma unroll
   for (int r = 0; r < DR; r++) {
     if (lo + (uint64_t)r * 512 + threadIdx.x >= hi) break;
     const uint32_t c = (uint32_t)rec[r][1];
     const uint32_t best = rec[r][0] == IDX_EMPTY ? special : vals[slot[r]];
-    a.latest[c] = best == c + 1;
+    const bool latest = best == c + 1;
+    a.latest[c] = latest;
+    if (!latest) atomicAdd(&a.ccount[c / ch], 1u);
   }
 }
-__global__ __launch_bounds__(256) void idx_count_kernel(IdxArgs a) {
-  __shared__ uint32_t wsum[4];
-  uint64_t lo, hi;
-  chunk_of(idx_n(a), &lo, &hi);
-  uint32_t cnt = 0;
-  for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) cnt += a.latest[c];
-  const uint32_t t = block_sum256(cnt, wsum);
-  if (threadIdx.x == 0) a.ccount[blockIdx.x] = t;
-}
 
-
-
+// the index in chain order of each key's latest entry: entry c goes to
+// c - (entries before c that are not the latest of their key); launched on
+// GLUE_BLOCKS blocks (idx_dedup's chunks)
 __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
   __shared__ uint32_t wsum[4];
-  uint64_t before = 0, total = 0;
-  block_prefix(a.ccount, GLUE_BLOCKS, wsum, &before, &total);
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.plan->n_index = total;
+  const uint64_t n = idx_n(a);
+  uint64_t nl_before = 0, nl_total = 0;
+  block_prefix(a.ccount, GLUE_BLOCKS, wsum, &nl_before, &nl_total);
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.plan->n_index = n - nl_total;
   uint64_t lo, hi;
-  chunk_of(idx_n(a), &lo, &hi);
-  uint64_t run = before;
+  chunk_of(n, &lo, &hi);
+  uint64_t run = lo - nl_before;
   // ER rounds of 256 positions per pass: their flags and keys are loaded
   // together and ranked with one LDS exchange
   constexpr int ER = 4;
