@@ -521,7 +521,8 @@ def main():
     value = bytes_total / dt * args.steps / 2**30
     scan_ms = scan_ms_sum / max(scan_n, 1)
     if torn:  # both passes' scans per step (the optimistic pass fails, the full pass decides)
-        scan_ms = scan_ms_sum / args.steps  # the slowest shard's scan bounds the step
+        scan_ms = scan_ms_sum / args.steps
+    if multi is not None:  # the slowest shard's scan bounds the step
         shard_scan = [x / max(multi["n"], 1) for x in multi["scan_ms"]]
         scan_ms = max(shard_scan)
     achieved = bytes_alg / (scan_ms * 1e-3) / 1e9

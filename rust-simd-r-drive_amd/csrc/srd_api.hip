@@ -238,7 +238,12 @@ template <bool FULL>
 static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr) {
   const dim3 grid(g), block(SCAN_WAVES_V2 * 64);
-  if (e0) {
+  static const bool marker = [] { const char* e = getenv("SRD_SCAN_MARKER_EVENTS"); return e && *e == '1'; }();
+  if (e0 && marker) {  // timing A/B only: marker events around a plain launch
+    (void)hipEventRecord(e0, s);
+    launch_scan<FULL>(g, a, s);
+    (void)hipEventRecord(e1, s);
+  } else if (e0) {
     if (a.flen > kWide)
       hipExtLaunchKernelGGL(scan_kernel<FULL, true>, grid, block, 0, s, e0, e1, 0, a);
     else
@@ -529,6 +534,8 @@ static void set_out_ptrs(Ctx* c, srd_device_result* out) {
   out->index_packed = P<uint64_t>(c, B_IPACKED);
 }
 
+static int index_build_sep(Ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, uint64_t* okeys,
+                           uint64_t* opacked, uint64_t* n_index);
 // finalize + index for a chain of n entries whose chain_g / walk state are set
 static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint32_t flags,
                   srd_device_result* out) {
@@ -573,9 +580,10 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
       HIPCHK(hipGetLastError());
     }
   }
-  // ---- KeyIndexer::build ----
+  // ---- KeyIndexer::build (bucketed; the global table if a bucket overflows) ----
   uint64_t nidx = 0;
-  TRY(index_global(c, n, &nidx));
+  TRY(index_build_sep(c, P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_IKEY),
+                      P<uint64_t>(c, B_IPACKED), &nidx));
   uint64_t h[8];
   TRY(read_counters(c, h));
   out->n_index = nidx;
@@ -1194,24 +1202,32 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     TRY(ensure(c, B_ST, K));
     TRY(ensure(c, B_JMP, K * 8));
     TRY(ensure(c, B_VFLAG, K * 4));
-    status_init_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<int64_t>(c, B_DPAR), K, P<uint8_t>(c, B_ST),
+    // run heads (alloc_dense sized B_DHEAD / B_RUNHEAD and the hipCUB scratch for K)
+    uint64_t* runhead = P<uint64_t>(c, B_RUNHEAD);
+    run_key_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<int64_t>(c, B_DPAR), K, P<uint64_t>(c, B_DHEAD));
+    KCHK(c, "run_key_kernel");
+    size_t tbs = c->bufs[B_CUB_TMP].n;
+    HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tbs, P<uint64_t>(c, B_DHEAD), runhead,
+                                             hipcub::Max(), (int)K, c->stream));
+    status_init_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<int64_t>(c, B_DPAR), runhead, K, P<uint8_t>(c, B_ST),
                                                               P<int64_t>(c, B_JMP));
     KCHK(c, "status_init_kernel");
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
-    // pointer jumping: every round doubles how far each unresolved node
-    // looks along its parent chain, so ceil(log2 K) + 1 rounds resolve every
-    // node; they run back to back and one more round, with the change flag
-    // cleared before it, proves convergence with a single host sync
+    // pointer jumping over the run heads: every round doubles how far each
+    // unresolved head looks along its chain of runs, so ceil(log2 K) + 1
+    // rounds resolve every head; they run back to back and one more round,
+    // with the change flag cleared before it, proves convergence with a
+    // single host sync
     int rounds = 1;
     while ((1ull << rounds) < K) rounds++;
     for (int pass = 0; pass < 8; pass++) {
       for (int r = 0; r <= (pass ? 0 : rounds); r++) {
-        status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, P<uint8_t>(c, B_ST), P<int64_t>(c, B_JMP),
-                                                                   (unsigned int*)(cnt + 4));
+        status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, runhead, P<uint8_t>(c, B_ST),
+                                                                   P<int64_t>(c, B_JMP), (unsigned int*)(cnt + 4));
         KCHK(c, "status_round_kernel");
       }
       HIPCHK(hipMemsetAsync(cnt + 4, 0, 8, c->stream));
-      status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, P<uint8_t>(c, B_ST), P<int64_t>(c, B_JMP),
+      status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, runhead, P<uint8_t>(c, B_ST), P<int64_t>(c, B_JMP),
                                                                  (unsigned int*)(cnt + 4));
       KCHK(c, "status_round_kernel");
       HIPCHK(hipGetLastError());
@@ -1219,6 +1235,8 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
       if (!h[4]) break;
       if (pass == 7) { set_err("internal: pointer jumping did not converge"); return SRD_ERR_INTERNAL; }
     }
+    status_spread_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, runhead, P<uint8_t>(c, B_ST));
+    KCHK(c, "status_spread_kernel");
     HIPCHK(hipMemsetAsync(cnt + 3, 0, 8, c->stream));
     valid_max_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<uint8_t>(c, B_ST), P<uint64_t>(c, B_DM), K,
                                                             (unsigned long long*)(cnt + 3), P<uint32_t>(c, B_VFLAG));

@@ -336,6 +336,25 @@ __device__ __forceinline__ void crc_lane_bases(uint32_t (&R)[4], int lane) {
   for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
 }
 
+// The optimistic pass starts at the node whose metadata ends at file_len
+// (data_store.rs:388-479's first tail t = file_len): true when the 20 bytes
+// there fail recover_valid_chain's node test (:404-470) for a strong node
+// (p >= 20, p < m, a nonzero checksum field, the prepad / tombstone rule)
+// and are no root (p == 0: the whole file is one entry).  Every lane reads
+// the same words (one request per wave).
+__device__ __forceinline__ bool start_not_a_node(const uint8_t* file, uint64_t flen) {
+  const uint64_t m = flen - 20;
+  uint64_t kh, p;
+  uint32_t crc;
+  ld_meta(file, m, &kh, &p, &crc);
+  if (p == 0) return false;
+  const uint32_t bw = *(const uint32_t*)(file + ((m - 1) & ~3ull));
+  const bool zb = ((bw >> (8 * ((m - 1) & 3))) & 0xffu) == 0;
+  const uint64_t dp = m - p;
+  const bool node = p >= 20 && p < m && crc != 0 && (dp > prepad64(p) || (dp == 1 && zb));
+  return !node;
+}
+
 // WIDE: stores above 2^40 bytes (prev offsets up to 48 bits, key_indexer.rs:12-15):
 // the level-1 filter looks for the two zero bytes m+14, m+15 at any alignment
 template <bool FULL, bool WIDE>
@@ -368,6 +387,19 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   uint64_t k0 = s0 * SPAN_TILES;
   uint64_t k1 = min((s0 + spw) * SPAN_TILES, a.n_tiles);
   if (k0 >= k1) k0 = k1 = a.k_lo;  // no tiles (the loops below do nothing): the wave joins the epilogue
+
+  if (!FULL && start_not_a_node(file, flen)) {
+    // the optimistic pass needs a recorded node at file_len - 20; without
+    // one it cannot prove anything (a torn tail, b"CORRUPT" appended): the
+    // waves skip their tiles, record nothing (zero span counts) and the
+    // glue reports ST_NOSTART, so the full pass starts ~0.9 ms earlier
+    const uint64_t sa = k0 / SPAN_TILES, sb = (k1 + SPAN_TILES - 1) / SPAN_TILES;
+    for (uint64_t sp = sa + lane; sp < sb; sp += 64) {
+      a.span_count[sp] = 0;
+      a.span_first[sp] = 0;
+    }
+    k0 = k1 = a.k_lo;
+  }
 
   uint32_t count = 0;
   uint64_t wtotal = 0;  // wave-uniform: records of the wave's spans
@@ -862,8 +894,10 @@ __global__ __launch_bounds__(64) void link_kernel(LinkArgs a) {
     const uint64_t m = a.c_m[gi], p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     const uint64_t mp = p - 20;  // p >= 20 by construction
     const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // span s holds m in [16 KiB s - 14, 16 KiB (s+1) - 14)
-    int64_t par = PAR_MISS;
-    if (sp2 < a.n_spans) {
+    // the parent is usually the previous record of the span: one load instead
+    // of a binary search
+    int64_t par = (i > 0 && a.c_m[gi - 1] == mp) ? (int64_t)(gb + i - 1) : PAR_MISS;
+    if (par == PAR_MISS && sp2 < a.n_spans) {
       uint32_t lo = 0, hi = min(a.span_count[sp2], a.cap);
       const uint64_t* cm = a.c_m + sp2 * a.cap;
       while (lo < hi) {
@@ -974,28 +1008,48 @@ __global__ void scatter_chain_kernel(const uint32_t* onpath, const uint32_t* cpo
 // --------------------------------------------------------------------------
 // full mode: statuses by pointer jumping
 // --------------------------------------------------------------------------
-__global__ void status_init_kernel(const int64_t* par, uint64_t n, uint8_t* st, int64_t* jmp) {
-  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n) return;
-  int64_t p = par[g];
-  st[g] = p == PAR_ROOT ? 1 : (p == PAR_MISS ? 2 : 0);
-  jmp[g] = p;
+// Statuses (1: reaches a root, 2: reaches a miss) by pointer jumping over
+// RUNS: node g continues its predecessor's run when par[g] == g - 1 (the
+// common case: consecutive chain entries), so a run shares its head's status
+// and only heads jump -- from a head to the head of its parent's run.  A C2
+// store with a torn tail has ~4K runs (false candidates break them) among 1M
+// nodes: every round is a cheap pass, and log2(runs) rounds resolve them.
+__global__ void run_key_kernel(const int64_t* par, uint64_t n, uint64_t* key) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) key[g] = (g > 0 && par[g] == (int64_t)g - 1) ? 0 : g + 1;
 }
-__global__ void status_round_kernel(uint64_t n, uint8_t* st, int64_t* jmp, unsigned int* changed) {
-  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n || st[g]) return;
-  int64_t j = jmp[g];
-  uint8_t s = st[j];
+// runhead[g] = 1 + the head of g's run (inclusive max scan of run_key)
+__global__ void status_init_kernel(const int64_t* par, const uint64_t* runhead, uint64_t n, uint8_t* st,
+                                   int64_t* jmp) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n || runhead[g] != g + 1) return;  // heads only
+  const int64_t p = par[g];
+  st[g] = p == PAR_ROOT ? 1 : (p == PAR_MISS ? 2 : 0);
+  jmp[g] = p >= 0 ? (int64_t)runhead[p] - 1 : p;
+}
+__global__ void status_round_kernel(uint64_t n, const uint64_t* runhead, uint8_t* st, int64_t* jmp,
+                                    unsigned int* changed) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n || runhead[g] != g + 1 || st[g]) return;
+  const int64_t j = jmp[g];
+  const uint8_t s = st[j];
   if (s) st[g] = s;
   else { jmp[g] = jmp[j]; *changed = 1; }
 }
+__global__ void status_spread_kernel(uint64_t n, const uint64_t* runhead, uint8_t* st) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n && runhead[g] != g + 1) st[g] = st[runhead[g] - 1];
+}
+// the largest valid node: one atomic per wave (a million atomics on one
+// word serialise: 0.83 ms at C2)
 __global__ void valid_max_kernel(const uint8_t* st, const uint64_t* d_m, uint64_t n,
                                  unsigned long long* best_g1, uint32_t* vflag) {
-  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n) return;
-  bool v = st[g] == 1;
-  vflag[g] = v;
-  if (v) atomicMax(best_g1, (unsigned long long)(g + 1));
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool v = g < n && st[g] == 1;
+  if (g < n) vflag[g] = v;
+  const uint64_t b = __ballot(v);
+  if (b && (threadIdx.x & 63) == 0)
+    atomicMax(best_g1, (unsigned long long)((g & ~63ull) + 64 - __builtin_clzll(b)));  // (highest valid g) + 1
 }
 // remap parents into the compacted valid space
 __global__ void remap_kernel(const uint64_t* vlist, const uint64_t* nv, const int64_t* par,
