@@ -659,7 +659,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     l.d_m = P<uint64_t>(c, B_DM);
     l.d_par = P<int64_t>(c, B_DPAR);
     l.d_slot = P<uint64_t>(c, B_DSLOT);
-    link_kernel<<<(unsigned)n_spans, 64, 0, c->stream>>>(l);
+    link_kernel<<<blocks(n_spans, 64), 256, 0, c->stream>>>(l);
     KCHK(c, "link_kernel");
     HIPCHK(hipGetLastError());
   } else {
@@ -1195,6 +1195,7 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
   out->mode = 1;
   TRY(run_scan(c, d_file, flen, true, &K, h));
   out->n_candidates = K;
+  if (debug_env()) fprintf(stderr, "full pass: K=%lu candidates\n", (unsigned long)K);
   out->n_weak = 0;
   const uint64_t max_root = h[0];
   uint64_t best_g1 = 0, tlin = 0;
@@ -1202,19 +1203,32 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     TRY(ensure(c, B_ST, K));
     TRY(ensure(c, B_JMP, K * 8));
     TRY(ensure(c, B_VFLAG, K * 4));
-    // run heads (alloc_dense sized B_DHEAD / B_RUNHEAD and the hipCUB scratch for K)
-    uint64_t* runhead = P<uint64_t>(c, B_RUNHEAD);
-    run_key_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<int64_t>(c, B_DPAR), K, P<uint64_t>(c, B_DHEAD));
-    KCHK(c, "run_key_kernel");
+    // core runs (alloc_dense sized B_CORE, B_DHEAD / B_RUNHEAD and the hipCUB
+    // scratch for K): core[g] = something links to g; prevcore = 1 + the last
+    // core node <= g; chead = 1 + the head of a core node's run
+    const unsigned kb = blocks(K, 256);
+    const int64_t* par = P<int64_t>(c, B_DPAR);
+    uint8_t* core = P<uint8_t>(c, B_CORE);
+    uint64_t* key = P<uint64_t>(c, B_DHEAD);
+    uint64_t* chead = P<uint64_t>(c, B_RUNHEAD);
+    uint8_t* st = P<uint8_t>(c, B_ST);
+    int64_t* jmp = P<int64_t>(c, B_JMP);
+    HIPCHK(hipMemsetAsync(core, 0, K, c->stream));
+    child_kernel<<<kb, 256, 0, c->stream>>>(par, K, core);
+    KCHK(c, "child_kernel");
+    core_flag_key_kernel<<<kb, 256, 0, c->stream>>>(core, K, key);
+    KCHK(c, "core_flag_key_kernel");
     size_t tbs = c->bufs[B_CUB_TMP].n;
-    HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tbs, P<uint64_t>(c, B_DHEAD), runhead,
-                                             hipcub::Max(), (int)K, c->stream));
-    status_init_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<int64_t>(c, B_DPAR), runhead, K, P<uint8_t>(c, B_ST),
-                                                              P<int64_t>(c, B_JMP));
+    HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tbs, key, chead, hipcub::Max(), (int)K, c->stream));
+    head_key_kernel<<<kb, 256, 0, c->stream>>>(core, par, chead, K, key);
+    KCHK(c, "head_key_kernel");
+    tbs = c->bufs[B_CUB_TMP].n;
+    HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tbs, key, chead, hipcub::Max(), (int)K, c->stream));
+    status_init_kernel<<<kb, 256, 0, c->stream>>>(par, core, chead, K, st, jmp);
     KCHK(c, "status_init_kernel");
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
-    // pointer jumping over the run heads: every round doubles how far each
-    // unresolved head looks along its chain of runs, so ceil(log2 K) + 1
+    // pointer jumping over the core run heads: every round doubles how far
+    // each unresolved head looks along its chain of runs, so ceil(log2 K) + 1
     // rounds resolve every head; they run back to back and one more round,
     // with the change flag cleared before it, proves convergence with a
     // single host sync
@@ -1222,25 +1236,27 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     while ((1ull << rounds) < K) rounds++;
     for (int pass = 0; pass < 8; pass++) {
       for (int r = 0; r <= (pass ? 0 : rounds); r++) {
-        status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, runhead, P<uint8_t>(c, B_ST),
-                                                                   P<int64_t>(c, B_JMP), (unsigned int*)(cnt + 4));
+        status_round_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st, jmp, (unsigned int*)(cnt + 4));
         KCHK(c, "status_round_kernel");
       }
       HIPCHK(hipMemsetAsync(cnt + 4, 0, 8, c->stream));
-      status_round_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, runhead, P<uint8_t>(c, B_ST), P<int64_t>(c, B_JMP),
-                                                                 (unsigned int*)(cnt + 4));
+      status_round_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st, jmp, (unsigned int*)(cnt + 4));
       KCHK(c, "status_round_kernel");
       HIPCHK(hipGetLastError());
       TRY(read_counters(c, h));
       if (!h[4]) break;
       if (pass == 7) { set_err("internal: pointer jumping did not converge"); return SRD_ERR_INTERNAL; }
     }
-    status_spread_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(K, runhead, P<uint8_t>(c, B_ST));
-    KCHK(c, "status_spread_kernel");
-    HIPCHK(hipMemsetAsync(cnt + 3, 0, 8, c->stream));
-    valid_max_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<uint8_t>(c, B_ST), P<uint64_t>(c, B_DM), K,
-                                                            (unsigned long long*)(cnt + 3), P<uint32_t>(c, B_VFLAG));
+    status_spread_core_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st);
+    KCHK(c, "status_spread_core_kernel");
+    status_spread_leaf_kernel<<<kb, 256, 0, c->stream>>>(K, par, core, st);
+    KCHK(c, "status_spread_leaf_kernel");
+    const unsigned vb = blocks(K, 256);
+    TRY(ensure(c, B_JMP, std::max<uint64_t>(K, vb) * 8));  // per-block maxima (the jump pointers are dead now)
+    valid_max_kernel<<<vb, 256, 0, c->stream>>>(P<uint8_t>(c, B_ST), K, P<uint64_t>(c, B_JMP), P<uint32_t>(c, B_VFLAG));
     KCHK(c, "valid_max_kernel");
+    max_reduce_kernel<<<1, 1024, 0, c->stream>>>(P<uint64_t>(c, B_JMP), vb, (unsigned long long*)(cnt + 3));
+    KCHK(c, "max_reduce_kernel");
     HIPCHK(hipGetLastError());
     TRY(read_counters(c, h));
     best_g1 = h[3];

@@ -884,11 +884,14 @@ struct LinkArgs {
   uint64_t* d_slot;
 };
 
-__global__ __launch_bounds__(64) void link_kernel(LinkArgs a) {
-  const uint64_t sp = blockIdx.x;
+// 4 lanes per span, 64 spans per block (one 64-thread block per span left
+// most lanes idle and put 256K blocks through the dispatcher at C2)
+__global__ __launch_bounds__(256) void link_kernel(LinkArgs a) {
+  const uint64_t sp = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  if (sp >= a.n_spans) return;
   const uint32_t n = min(a.span_count[sp], a.cap);
   const uint64_t gb = a.span_base[sp];
-  for (uint32_t i = threadIdx.x; i < n; i += 64) {
+  for (uint32_t i = threadIdx.x & 3; i < n; i += 4) {
     const uint64_t gi = sp * a.cap + i;
     const u32x4 r0 = a.c_rec[2 * gi];
     const uint64_t m = a.c_m[gi], p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
@@ -1009,47 +1012,70 @@ __global__ void scatter_chain_kernel(const uint32_t* onpath, const uint32_t* cpo
 // full mode: statuses by pointer jumping
 // --------------------------------------------------------------------------
 // Statuses (1: reaches a root, 2: reaches a miss) by pointer jumping over
-// RUNS: node g continues its predecessor's run when par[g] == g - 1 (the
-// common case: consecutive chain entries), so a run shares its head's status
-// and only heads jump -- from a head to the head of its parent's run.  A C2
-// store with a torn tail has ~4K runs (false candidates break them) among 1M
-// nodes: every round is a cheap pass, and log2(runs) rounds resolve them.
-__global__ void run_key_kernel(const int64_t* par, uint64_t n, uint64_t* key) {
+// runs of CORE nodes (something links to them).  The full pass records every
+// node, also the weak ones a metadata record's checksum and zero prepad leave
+// (~2 per entry at C2: leaves whose random "prev" mostly misses), so chain
+// nodes are rarely adjacent; among core nodes they are: a core node whose
+// parent is the previous core node continues that one's run.  Runs share
+// their head's status and only heads jump (to the head of their parent's
+// run); a leaf then takes its parent's status.  A torn C2 store: one run.
+__global__ void status_init_kernel(const int64_t* par, const uint8_t* core, const uint64_t* chead, uint64_t n,
+                                   uint8_t* st, int64_t* jmp) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) key[g] = (g > 0 && par[g] == (int64_t)g - 1) ? 0 : g + 1;
-}
-// runhead[g] = 1 + the head of g's run (inclusive max scan of run_key)
-__global__ void status_init_kernel(const int64_t* par, const uint64_t* runhead, uint64_t n, uint8_t* st,
-                                   int64_t* jmp) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n || runhead[g] != g + 1) return;  // heads only
+  if (g >= n || !core[g] || chead[g] != g + 1) return;  // core run heads only
   const int64_t p = par[g];
   st[g] = p == PAR_ROOT ? 1 : (p == PAR_MISS ? 2 : 0);
-  jmp[g] = p >= 0 ? (int64_t)runhead[p] - 1 : p;
+  jmp[g] = p >= 0 ? (int64_t)chead[p] - 1 : p;  // a parent has a child: it is core
 }
-__global__ void status_round_kernel(uint64_t n, const uint64_t* runhead, uint8_t* st, int64_t* jmp,
-                                    unsigned int* changed) {
+__global__ void status_round_kernel(uint64_t n, const uint8_t* core, const uint64_t* chead, uint8_t* st,
+                                    int64_t* jmp, unsigned int* changed) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n || runhead[g] != g + 1 || st[g]) return;
+  if (g >= n || !core[g] || chead[g] != g + 1 || st[g]) return;
   const int64_t j = jmp[g];
   const uint8_t s = st[j];
   if (s) st[g] = s;
   else { jmp[g] = jmp[j]; *changed = 1; }
 }
-__global__ void status_spread_kernel(uint64_t n, const uint64_t* runhead, uint8_t* st) {
+__global__ void status_spread_core_kernel(uint64_t n, const uint8_t* core, const uint64_t* chead, uint8_t* st) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n && runhead[g] != g + 1) st[g] = st[runhead[g] - 1];
+  if (g < n && core[g] && chead[g] != g + 1) st[g] = st[chead[g] - 1];
 }
-// the largest valid node: one atomic per wave (a million atomics on one
-// word serialise: 0.83 ms at C2)
-__global__ void valid_max_kernel(const uint8_t* st, const uint64_t* d_m, uint64_t n,
-                                 unsigned long long* best_g1, uint32_t* vflag) {
+__global__ void status_spread_leaf_kernel(uint64_t n, const int64_t* par, const uint8_t* core, uint8_t* st) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n || core[g]) return;
+  const int64_t p = par[g];
+  st[g] = p == PAR_ROOT ? 1 : (p == PAR_MISS ? 2 : st[p]);
+}
+__global__ void core_flag_key_kernel(const uint8_t* core, uint64_t n, uint64_t* key) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) key[g] = core[g] ? g + 1 : 0;
+}
+
+// the largest valid node: a block maximum per block (same-address atomics
+// serialise: even one per wave, ~16K of them, took 0.83 ms at C2), then one
+// block reduces them
+__global__ __launch_bounds__(256) void valid_max_kernel(const uint8_t* st, uint64_t n, uint64_t* bmax,
+                                                        uint32_t* vflag) {
+  __shared__ uint64_t wm[4];
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool v = g < n && st[g] == 1;
   if (g < n) vflag[g] = v;
   const uint64_t b = __ballot(v);
-  if (b && (threadIdx.x & 63) == 0)
-    atomicMax(best_g1, (unsigned long long)((g & ~63ull) + 64 - __builtin_clzll(b)));  // (highest valid g) + 1
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = b ? (g & ~63ull) + 64 - __builtin_clzll(b) : 0;  // max g + 1
+  __syncthreads();
+  if (threadIdx.x == 0) bmax[blockIdx.x] = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+}
+__global__ __launch_bounds__(1024) void max_reduce_kernel(const uint64_t* v, uint64_t n, unsigned long long* out) {
+  __shared__ uint64_t wm[16];
+  uint64_t m = 0;
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) m = max(m, v[i]);
+  m = wave_max_u64(m);
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; w++) m = max(m, wm[w]);
+    *out = m;
+  }
 }
 // remap parents into the compacted valid space
 __global__ void remap_kernel(const uint64_t* vlist, const uint64_t* nv, const int64_t* par,
