@@ -126,7 +126,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
-  B_XKEY, B_XVAL, B_GATHER,
+  B_XKEY, B_XVAL, B_GATHER, B_RFLAG,
   B_COUNT_
 };
 
@@ -1234,13 +1234,16 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     // single host sync
     int rounds = 1;
     while ((1ull << rounds) < K) rounds++;
+    TRY(ensure(c, B_RFLAG, 4 * 72));
+    unsigned int* rflag = P<unsigned int>(c, B_RFLAG);
     for (int pass = 0; pass < 8; pass++) {
-      for (int r = 0; r <= (pass ? 0 : rounds); r++) {
-        status_round_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st, jmp, (unsigned int*)(cnt + 4));
+      HIPCHK(hipMemsetAsync(rflag, 0, 4 * 72, c->stream));
+      for (int r = 0; r <= (pass ? 0 : std::min(rounds, 70)); r++) {
+        status_round_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st, jmp, rflag + r, r ? rflag + r - 1 : nullptr);
         KCHK(c, "status_round_kernel");
       }
       HIPCHK(hipMemsetAsync(cnt + 4, 0, 8, c->stream));
-      status_round_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st, jmp, (unsigned int*)(cnt + 4));
+      status_round_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st, jmp, (unsigned int*)(cnt + 4), nullptr);
       KCHK(c, "status_round_kernel");
       HIPCHK(hipGetLastError());
       TRY(read_counters(c, h));

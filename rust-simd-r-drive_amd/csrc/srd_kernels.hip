@@ -900,16 +900,30 @@ __global__ __launch_bounds__(256) void link_kernel(LinkArgs a) {
     // the parent is usually the previous record of the span: one load instead
     // of a binary search
     int64_t par = (i > 0 && a.c_m[gi - 1] == mp) ? (int64_t)(gb + i - 1) : PAR_MISS;
-    if (par == PAR_MISS && sp2 < a.n_spans) {
-      uint32_t lo = 0, hi = min(a.span_count[sp2], a.cap);
-      const uint64_t* cm = a.c_m + sp2 * a.cap;
-      while (lo < hi) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (cm[mid] < mp) lo = mid + 1; else hi = mid;
+    if (par == PAR_MISS) {
+      // The metadata the parent would have at p - 20, read from the file:
+      // its prev == 0 makes it the root entry (data_store.rs:404-416);
+      // otherwise only bytes that pass the node test can be a recorded
+      // candidate, so the binary search runs for those alone (the weak
+      // nodes a record's checksum and zero prepad leave have random "prev"
+      // values: their parents mostly fail here, one line read instead of
+      // three to four dependent ones)
+      uint64_t pkh, pp;
+      uint32_t pcrc;
+      ld_meta(a.file, mp, &pkh, &pp, &pcrc);
+      const uint64_t dp = mp - pp;
+      if (pp == 0) {
+        if (p >= 21) par = PAR_ROOT;
+      } else if (pp >= 20 && pp < mp && (dp > prepad64(pp) || dp == 1) && sp2 < a.n_spans) {
+        uint32_t lo = 0, hi = min(a.span_count[sp2], a.cap);
+        const uint64_t* cm = a.c_m + sp2 * a.cap;
+        while (lo < hi) {
+          uint32_t mid = (lo + hi) >> 1;
+          if (cm[mid] < mp) lo = mid + 1; else hi = mid;
+        }
+        if (lo < min(a.span_count[sp2], a.cap) && cm[lo] == mp) par = (int64_t)(a.span_base[sp2] + lo);
       }
-      if (lo < min(a.span_count[sp2], a.cap) && cm[lo] == mp) par = (int64_t)(a.span_base[sp2] + lo);
     }
-    if (par == PAR_MISS && p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) par = PAR_ROOT;
     const uint64_t g = gb + i;
     a.d_m[g] = m;
     a.d_par[g] = par;
@@ -1027,8 +1041,11 @@ __global__ void status_init_kernel(const int64_t* par, const uint8_t* core, cons
   st[g] = p == PAR_ROOT ? 1 : (p == PAR_MISS ? 2 : 0);
   jmp[g] = p >= 0 ? (int64_t)chead[p] - 1 : p;  // a parent has a child: it is core
 }
+// prev (nullable): the previous round's change flag -- a round after one in
+// which no head jumped has nothing left to do (every head resolved)
 __global__ void status_round_kernel(uint64_t n, const uint8_t* core, const uint64_t* chead, uint8_t* st,
-                                    int64_t* jmp, unsigned int* changed) {
+                                    int64_t* jmp, unsigned int* changed, const unsigned int* prev) {
+  if (prev && *prev == 0) return;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n || !core[g] || chead[g] != g + 1 || st[g]) return;
   const int64_t j = jmp[g];
