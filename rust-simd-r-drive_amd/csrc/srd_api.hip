@@ -1239,11 +1239,14 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     for (int pass = 0; pass < 8; pass++) {
       HIPCHK(hipMemsetAsync(rflag, 0, 4 * 72, c->stream));
       for (int r = 0; r <= (pass ? 0 : std::min(rounds, 70)); r++) {
-        status_round_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st, jmp, rflag + r, r ? rflag + r - 1 : nullptr);
+        // a fixed grid (grid-stride): a round after convergence exits at once
+        status_round_kernel<<<std::min(kb, 1024u), 256, 0, c->stream>>>(K, core, chead, st, jmp, rflag + r,
+                                                                       r ? rflag + r - 1 : nullptr);
         KCHK(c, "status_round_kernel");
       }
       HIPCHK(hipMemsetAsync(cnt + 4, 0, 8, c->stream));
-      status_round_kernel<<<kb, 256, 0, c->stream>>>(K, core, chead, st, jmp, (unsigned int*)(cnt + 4), nullptr);
+      status_round_kernel<<<std::min(kb, 1024u), 256, 0, c->stream>>>(K, core, chead, st, jmp, (unsigned int*)(cnt + 4),
+                                                                     nullptr);
       KCHK(c, "status_round_kernel");
       HIPCHK(hipGetLastError());
       TRY(read_counters(c, h));

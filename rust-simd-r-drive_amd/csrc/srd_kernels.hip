@@ -1046,12 +1046,13 @@ __global__ void status_init_kernel(const int64_t* par, const uint8_t* core, cons
 __global__ void status_round_kernel(uint64_t n, const uint8_t* core, const uint64_t* chead, uint8_t* st,
                                     int64_t* jmp, unsigned int* changed, const unsigned int* prev) {
   if (prev && *prev == 0) return;
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n || !core[g] || chead[g] != g + 1 || st[g]) return;
-  const int64_t j = jmp[g];
-  const uint8_t s = st[j];
-  if (s) st[g] = s;
-  else { jmp[g] = jmp[j]; *changed = 1; }
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x) {
+    if (!core[g] || chead[g] != g + 1 || st[g]) continue;
+    const int64_t j = jmp[g];
+    const uint8_t s = st[j];
+    if (s) st[g] = s;
+    else { jmp[g] = jmp[j]; *changed = 1; }
+  }
 }
 __global__ void status_spread_core_kernel(uint64_t n, const uint8_t* core, const uint64_t* chead, uint8_t* st) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
