@@ -72,6 +72,9 @@ class ShardedResult:
     local: object = None        # backend's shard-local result (chain arrays in the context's device
                                 # buffers: valid until the next call on that context), or the
                                 # exception of a failed shard
+    retried: bool = False       # a run of unproven shards was re-validated with its lower neighbour
+    lo: int = 0                 # this rank's shard after that re-validation (lo == hi: emptied)
+    hi: int = 0
 
 
 class HipBackend:
@@ -142,10 +145,40 @@ def backend_device(backend) -> torch.device:
     return torch.device("cpu") if d is None else torch.device("cuda", d) if isinstance(d, int) else torch.device(d)
 
 
+def neighbour_runs(proven: list[bool], cuts: list[int]) -> list[tuple[int, int]]:
+    """The re-validation plan when shards are unproven (srd_validate_index_multi's
+    rule): each run [i, b] of consecutive unproven shards is taken over by its
+    lower neighbour a -- the first non-empty shard below (an empty shard proves
+    nothing; its cut may be the forged one), or the run itself at shard 0 --
+    which re-validates [cuts[a], cuts[b+1]): both ends are tails the
+    neighbours proved.  Returns [(a, b)]."""
+    runs, floor, i, n = [], 0, 0, len(proven)
+    while i < n:
+        if proven[i]:
+            i += 1
+            continue
+        b = i
+        while b + 1 < n and not proven[b + 1]:
+            b += 1
+        a = i - 1 if i else 0
+        while a > floor and cuts[a] == cuts[a + 1]:
+            a -= 1
+        runs.append((max(a, floor), b))
+        floor = b + 1
+        i = b + 1
+    return runs
+
+
 def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, hi: int, file_len: int,
-                           group=None) -> ShardedResult:
+                           group=None, retry: bool = True) -> ShardedResult:
     """One rank's part of the sharded open: validate its shard, check the
-    composition, exchange the index.  Collective over `group`."""
+    composition, exchange the index.  Collective over `group`.
+
+    Shards left unproven by a cut that is no chain tail are retried once with
+    their lower neighbour (neighbour_runs): the run's ranks send their bytes
+    to the neighbour rank (point-to-point), which re-validates the merged
+    span; the others keep their shards.  Only what is still unproven (a torn
+    tail, corruption) returns composed = False for the whole-file path."""
     world = dist.get_world_size(group)
     dev = buf.device
     # collectives run where the backend lives: device memory for nccl (RCCL
@@ -182,9 +215,17 @@ def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, h
         rows[i][2] == rows[i + 1][1] for i in range(world - 1))
     n_chain = sum(r[3] for r in rows)
     n_bad = sum(r[4] for r in rows)
+    cuts = [r[1] for r in rows] + [rows[-1][2]]
+    hard = isinstance(local, Exception)
+    errs = torch.tensor([int(hard)], dtype=torch.int64, device=cd)
+    dist.all_reduce(errs, group=group)
+    consistent = cuts[0] == 0 and cuts[-1] == file_len and all(rows[i][2] == rows[i + 1][1] for i in range(world - 1))
+    if not composed and retry and not int(errs.item()) and consistent:
+        return _retry_with_neighbours(backend, buf, span_off, lo, hi, file_len, group, [bool(r[0]) for r in rows],
+                                      cuts)
     if not composed:
         empty = torch.empty(0, dtype=torch.int64, device=dev)
-        return ShardedResult(0, False, 0, 0, 0, empty, empty, local)
+        return ShardedResult(0, False, 0, 0, 0, empty, empty, local, lo=lo, hi=hi)
     # 2. index exchange: pairs to their owners
     me = dist.get_rank(group)
     rc = [rows[r][5 + me] for r in range(world)]
@@ -193,4 +234,43 @@ def sharded_validate_index(backend, buf: torch.Tensor, span_off: int, lo: int, h
     okeys, opacked = backend.build(got.to(dev))
     ni = torch.tensor([okeys.numel()], dtype=torch.int64, device=cd)
     dist.all_reduce(ni, group=group)
-    return ShardedResult(file_len, True, n_chain, n_bad, int(ni.item()), okeys, opacked, local)
+    return ShardedResult(file_len, True, n_chain, n_bad, int(ni.item()), okeys, opacked, local, lo=lo, hi=hi)
+
+
+def _retry_with_neighbours(backend, buf, span_off, lo, hi, file_len, group, proven, cuts) -> ShardedResult:
+    """Ranks a+1..b of a run send their bytes [lo_i, hi_i) to rank a, which
+    appends them to its span: its new shard is [cuts[a], cuts[b+1]); the
+    senders' shards become empty at cuts[b+1].  Then the normal protocol,
+    without a second retry."""
+    me = dist.get_rank(group)
+    dev = buf.device
+    cd = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
+    runs = neighbour_runs(proven, cuts)
+    n_lo, n_hi, n_buf, n_off = lo, hi, buf, span_off
+    for a, b in runs:
+        if a < me <= b:  # a sender: its bytes go to rank a, its shard empties
+            if hi > lo:
+                dist.send(buf[lo - span_off: hi - span_off].contiguous().to(cd), a, group=group)
+            n_lo = n_hi = cuts[b + 1]
+            n_buf = torch.empty(0, dtype=torch.uint8, device=dev)
+            n_off = n_lo - n_lo % S.SPAN_ALIGN
+        elif me == a:  # the neighbour: its span [span_off, hi) + the run's bytes
+            parts = [buf[: hi - span_off] if hi > lo else torch.empty(0, dtype=torch.uint8, device=dev)]
+            for i in range(a + 1, b + 1):
+                if cuts[i + 1] > cuts[i]:
+                    t = torch.empty(cuts[i + 1] - cuts[i], dtype=torch.uint8, device=cd)
+                    dist.recv(t, i, group=group)
+                    parts.append(t.to(dev))
+            n_lo = cuts[a]
+            n_hi = cuts[b + 1]
+            n_off = n_lo - n_lo % S.SPAN_ALIGN
+            # the merged bytes start at the neighbour's span, or -- an empty
+            # neighbour -- at its cut (the bytes below a shard's lower tail
+            # are never read as entries: zeros are fine there)
+            start = span_off if hi > lo else cuts[a + 1]
+            merged = torch.cat([p.reshape(-1) for p in parts])
+            n_buf = torch.zeros(S.padded_size(n_hi - n_off) if n_hi > n_lo else 1, dtype=torch.uint8, device=dev)
+            n_buf[start - n_off: start - n_off + merged.numel()].copy_(merged)
+    res = sharded_validate_index(backend, n_buf, n_off, n_lo, n_hi, file_len, group, retry=False)
+    res.retried = True
+    return res

@@ -84,7 +84,7 @@ def _host_worker(rank, world, port, store_bytes, q):
         res = SH.sharded_open_host(SH.HipBackend(ctx, 0), store)
         q.put((rank, res.composed, res.final_len, res.n_chain, res.n_crc_bad, res.n_index,
                dict(zip(res.owner_keys.cpu().numpy().view(np.uint64).tolist(),
-                        res.owner_packed.cpu().numpy().view(np.uint64).tolist()))))
+                        res.owner_packed.cpu().numpy().view(np.uint64).tolist())), res.retried))
         torch.cuda.synchronize()
         ctx.close()
     finally:
@@ -125,24 +125,32 @@ def test_sharded_open_host_zipf(world):
     out = _run_host(world, store)
     want = O.key_indexer_build(store, store.size)
     merged = {}
-    for rank, composed, final_len, n_chain, n_bad, n_index, idx in out:
-        assert (composed, final_len, n_chain, n_bad, n_index) == (True, store.size, 1500, 0, len(want))
+    for rank, composed, final_len, n_chain, n_bad, n_index, idx, retried in out:
+        assert (composed, final_len, n_chain, n_bad, n_index, retried) == (True, store.size, 1500, 0, len(want), False)
         assert not (merged.keys() & idx.keys())
         merged.update(idx)
     assert merged == want
 
 
 def test_sharded_open_host_refutes_bad_cuts():
-    """A forged tail under the cut target, and a torn tail: the shards do not
-    compose, so the whole-file path decides (checked here against the oracle)."""
+    """A forged tail under the cut target: the shard above it is unproven and
+    is re-validated with its lower neighbour (the bytes sent rank to rank):
+    composed, the index the oracle's.  A torn tail stays unproven after that
+    retry, so the whole-file path decides (checked here against the oracle)."""
     import oracle as O
     import srd_amd as S
     from test_shard_gloo import fake_cut_store
     fake, _ = fake_cut_store()
+    out = _run_host(2, fake)
+    want = O.key_indexer_build(fake, fake.size)
+    merged = {}
+    for rank, composed, final_len, n_chain, n_bad, n_index, idx, retried in out:
+        assert (composed, retried, final_len, n_index) == (True, True, fake.size, len(want))
+        merged.update(idx)
+    assert merged == want
     torn = np.concatenate([_zipf_host_store(600), np.frombuffer(b"CORRUPT", np.uint8)])
-    for store in (fake, torn):
-        out = _run_host(2, store)
-        assert all(not composed for _, composed, *_ in out)
-        r = S.validate_index(store)
-        assert r.final_len == O.recover_valid_chain(store)
-        assert r.index() == O.key_indexer_build(store, r.final_len)
+    out = _run_host(2, torn)
+    assert all(not composed for _, composed, *_ in out)
+    r = S.validate_index(torn)
+    assert r.final_len == O.recover_valid_chain(torn)
+    assert r.index() == O.key_indexer_build(torn, r.final_len)

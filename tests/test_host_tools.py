@@ -48,6 +48,11 @@ def test_c_abi_layout_matches_bindings():
         assert out[f"srd_result.{name}"] == getattr(S.DeviceResult, name).offset, name
     for name, _ in S.WriteEntry._fields_:
         assert out[f"srd_write_entry.{name}"] == getattr(S.WriteEntry, name).offset, name
+    for name, _ in S.MultiSummary._fields_:
+        assert out[f"srd_multi_summary.{name}"] == getattr(S.MultiSummary, name).offset, name
+    assert out["sizeof(srd_multi_summary)"] == C.sizeof(S.MultiSummary) == 112
+    assert "pub mode: u32, pub path: u32, pub n_shards: u32, pub merged: u32," in open(
+        os.path.join(ROOT, "INTEGRATION.md")).read()
     assert out["sizeof(srd_result)"] == C.sizeof(S.DeviceResult) == 144
     assert out["sizeof(srd_write_entry)"] == C.sizeof(S.WriteEntry) == 40
     # the Rust #[repr(C)] SrdResult of INTEGRATION.md: 7 u64, 2 u32, 10 pointers

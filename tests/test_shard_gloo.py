@@ -196,7 +196,8 @@ def _host_worker(rank, world, port, store_bytes, q):
         store = np.frombuffer(store_bytes, np.uint8)
         res = SH.sharded_open_host(OracleBackend(store), store)
         q.put((rank, res.composed, res.final_len, res.n_chain, res.n_index,
-               dict(zip(res.owner_keys.numpy().view(np.uint64).tolist(), res.owner_packed.numpy().view(np.uint64).tolist()))))
+               dict(zip(res.owner_keys.numpy().view(np.uint64).tolist(), res.owner_packed.numpy().view(np.uint64).tolist())),
+               res.retried))
     finally:
         dist.destroy_process_group()
 
@@ -219,8 +220,8 @@ def test_sharded_open_host_byte_cuts(world):
         assert p.exitcode == 0
     want = O.key_indexer_build(store, store.size)
     merged = {}
-    for rank, composed, final_len, n_chain, n_index, idx in out:
-        assert composed and final_len == store.size and n_chain == 400 and n_index == len(want)
+    for rank, composed, final_len, n_chain, n_index, idx, retried in out:
+        assert composed and not retried and final_len == store.size and n_chain == 400 and n_index == len(want)
         assert not (merged.keys() & idx.keys())
         merged.update(idx)
     assert merged == want
@@ -269,4 +270,25 @@ def test_fake_tail_cut_is_refuted():
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    assert all(not composed for _, composed, *_ in out)
+    # the forged cut leaves a shard unproven; the retry with its lower
+    # neighbour composes, and the index is the whole-file one
+    import oracle as O
+    want = O.key_indexer_build(store, store.size)
+    merged = {}
+    for rank, composed, final_len, n_chain, n_index, idx, retried in out:
+        assert composed and retried and final_len == store.size and n_index == len(want)
+        merged.update(idx)
+    assert merged == want
+
+
+@pytest.mark.parametrize("proven,cuts,want", [
+    ([True, False], [0, 5, 9], [(0, 1)]),
+    ([False, True], [0, 5, 9], [(0, 0)]),
+    ([True, True, False, False, True], [0, 1, 2, 3, 4, 5], [(1, 3)]),
+    ([True, True, False], [0, 4, 4, 9], [(0, 2)]),  # the empty shard 1 is skipped
+    ([False, True, False], [0, 4, 4, 9], [(0, 0), (1, 2)]),  # the floor stops at the previous run's end
+])
+def test_neighbour_runs(proven, cuts, want):
+    sys.path[:0] = [os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    import srd_shard as SH
+    assert SH.neighbour_runs(proven, cuts) == want
