@@ -107,6 +107,7 @@ struct Ctx {
   srd_multi_summary last_multi{};  // the last multi-GPU open with this context as ctxs[0]
   void* h_out = nullptr;  // pinned host result arrays (srd_validate_index / _multi)
   uint64_t h_out_n = 0;
+  uint8_t lgen = 0;  // generation of the index build's non-latest marks (B_LATEST8)
 };
 
 enum BufId {
@@ -126,7 +127,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
-  B_XKEY, B_XVAL, B_GATHER, B_RFLAG,
+  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED,
   B_COUNT_
 };
 
@@ -459,6 +460,7 @@ static int alloc_out(Ctx* c, uint64_t n) {
   TRY(ensure(c, B_SLOW, n * 8));
   TRY(ensure(c, B_IKEY, n * 8));
   TRY(ensure(c, B_IPACKED, n * 8));
+  TRY(ensure(c, B_O_PACKED, n * 8));
   return 0;
 }
 
@@ -696,7 +698,16 @@ static int alloc_index(Ctx* c, uint64_t n_cap, uint32_t log2_nbk) {
   TRY(ensure(c, B_HIST, nbk * IDX_HBLOCKS * 4));
   TRY(ensure(c, B_HOFF, (nbk + GLUE_BLOCKS) * 4));
   TRY(ensure(c, B_SKEY, nbk * IDX_TCAP * 16));
-  TRY(ensure(c, B_LATEST8, n_cap + 1));
+  TRY(ensure_z(c, B_LATEST8, n_cap + 1));  // zero on (re)allocation: no entry carries a live generation
+  return 0;
+}
+// a fresh generation of the non-latest marks for each index build (the
+// array is cleared once every 255 builds)
+static int next_lgen(Ctx* c) {
+  if (++c->lgen == 0) {
+    HIPCHK(hipMemsetAsync(P<void>(c, B_LATEST8), 0, c->bufs[B_LATEST8].n, c->stream));
+    c->lgen = 1;
+  }
   return 0;
 }
 // the words every index build needs zeroed: the bucket fills and, after them,
@@ -718,6 +729,7 @@ static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
   ia.ccount = ia.bfill + ((size_t)1 << log2_nbk);
   ia.srec = P<u64x2>(c, B_SKEY);
   ia.latest = P<uint8_t>(c, B_LATEST8);
+  ia.lgen = c->lgen;
   return ia;
 }
 // fused: chain_finalize_kernel already claimed the bucket ranges and wrote
@@ -726,7 +738,9 @@ static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
 static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
                                  const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
                                  Plan* pl, bool fused = false) {
+  TRY(next_lgen(c));
   IdxArgs ia = index_args(c, log2_nbk);
+  ia.alias = fused ? 1u : 0u;
   ia.kh = kh;
   ia.mo = mo;
   ia.n_dev = n_dev;
@@ -941,6 +955,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.o_tail = P<uint32_t>(c, B_O_TAIL);
       f.o_ok = P<uint8_t>(c, B_O_OK);
       f.n_bad = (unsigned long long*)&pl->n_bad;
+      f.o_packed = P<uint64_t>(c, B_O_PACKED);
       chain_finalize_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, (1u << log2_nbk) * 4, c->stream>>>(
           sa, f, index_args(c, log2_nbk), log2_nbk);
       KCHK(c, "chain_finalize_kernel");
@@ -995,8 +1010,13 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     if (hp.idx_overflow || index_global_env()) {
       c->ev3_recorded = false;
       TRY(index_global(c, hp.n_chain, &out->n_index));
+      hp.idx_alias = 0;
     }
     set_out_ptrs(c, out);
+    if (hp.idx_alias) {  // every entry its key's latest: the index is the chain's own arrays
+      out->index_key_hash = P<uint64_t>(c, B_O_KH);
+      out->index_packed = P<uint64_t>(c, B_O_PACKED);
+    }
     *done = true;
     return 0;
   }

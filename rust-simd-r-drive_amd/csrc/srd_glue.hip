@@ -45,6 +45,7 @@ struct Plan {
   uint32_t nroot;      // core nodes linking to a root
   uint32_t troot;      // file_len itself is a root tail
   uint32_t idx_overflow;
+  uint32_t idx_alias;  // every chain entry is its key's latest: the index IS (o_kh, o_packed) (idx_emit)
   uint32_t why[2];     // shape failures (diagnostics): dangling parent, branch
 };
 constexpr uint32_t ST_NOSTART = 1, ST_SHAPE = 2, ST_ROOTS = 4, ST_CAPK = 8, ST_OVERFLOW = 16;
@@ -447,7 +448,9 @@ struct IdxArgs {
   uint32_t* bfill;
   uint32_t* bbase;       // [IDX_HBLOCKS * nbk]
   u64x2* srec;           // (key, chain index) per entry, in its bucket's range
-  uint8_t* latest;       // [n] 1 = latest entry of its key
+  uint8_t* latest;       // [n] == lgen: NOT the latest entry of its key (idx_dedup writes only those)
+  uint8_t lgen;          // this build's generation (1..255; the host clears the array on wrap)
+  uint32_t alias;        // fused pass: with no non-latest entry idx_emit writes nothing (Plan::idx_alias)
   uint32_t* ccount;      // [GLUE_BLOCKS] NON-latest entries per chain chunk (idx_dedup -> idx_emit; zero before)
   uint64_t* okey;
   uint64_t* opacked;
@@ -753,6 +756,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
         const uint64_t c = run + rank[r];
         f.o_mo[c] = e[r].mo;
         f.o_kh[c] = kh[r];
+        f.o_packed[c] = ((kh[r] >> 48) << 48) | (e[r].mo & 0xFFFFFFFFFFFFull);  // key_indexer.rs:79-85
         f.o_prev[c] = e[r].p;
         f.o_crc_st[c] = e[r].crc_st;
         atomicAdd(&hist[idx_bucket(kh[r], log2_nbk)], 1u);
@@ -893,9 +897,12 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
     if (lo + (uint64_t)r * 512 + threadIdx.x >= hi) break;
     const uint32_t c = (uint32_t)rec[r][1];
     const uint32_t best = rec[r][0] == IDX_EMPTY ? special : vals[slot[r]];
-    const bool latest = best == c + 1;
-    a.latest[c] = latest;
-    if (!latest) atomicAdd(&a.ccount[c / ch], 1u);
+    // only the (rare) non-latest entries are marked: a byte store per entry,
+    // scattered over the chain, costs partial-line writes for every key
+    if (best != c + 1) {
+      a.latest[c] = a.lgen;
+      atomicAdd(&a.ccount[c / ch], 1u);
+    }
   }
 }
 
@@ -907,7 +914,13 @@ __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
   const uint64_t n = idx_n(a);
   uint64_t nl_before = 0, nl_total = 0;
   block_prefix(a.ccount, GLUE_BLOCKS, wsum, &nl_before, &nl_total);
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.plan->n_index = n - nl_total;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.plan->n_index = n - nl_total;
+    a.plan->idx_alias = a.alias && nl_total == 0;
+  }
+  // every entry the latest of its key (a store without overwrites): the
+  // index is the chain's (key_hash, packed) arrays chain_finalize wrote
+  if (a.alias && nl_total == 0) return;
   uint64_t lo, hi;
   chunk_of(n, &lo, &hi);
   uint64_t run = lo - nl_before;
@@ -921,7 +934,7 @@ __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
 #pragma unroll
     for (int r = 0; r < ER; r++) {
       const uint64_t c = base + (uint64_t)r * 256 + threadIdx.x, cc = c < hi ? c : lo;
-      f[r] = c < hi && a.latest[cc];
+      f[r] = c < hi && a.latest[cc] != a.lgen;
       key[r] = a.kh[cc];
       mo[r] = a.mo[cc];
     }

@@ -1135,6 +1135,7 @@ struct FinArgs {
   uint32_t coff;
   // outputs
   uint64_t *o_mo, *o_kh, *o_prev, *o_start, *o_len;
+  uint64_t* o_packed;  // nullable: pack(tag16, meta_off48) per chain entry (the optimistic pass's index alias)
   uint32_t *o_crc_st, *o_crc, *o_pieces;  // o_pieces: bit0 suf ok, bit1 sxm ok (slow path input)
   uint32_t *o_suf, *o_sxm, *o_tail;
   uint8_t* o_ok;
@@ -1293,6 +1294,7 @@ __device__ bool finalize_core(const FinArgs& a, uint64_t c, uint64_t gi, int64_t
   len = mo - start;
   a.o_mo[c] = mo;
   a.o_kh[c] = kh;
+  if (a.o_packed) a.o_packed[c] = ((kh >> 48) << 48) | (mo & 0xFFFFFFFFFFFFull);  // key_indexer.rs:79-85
   a.o_prev[c] = p;
   a.o_start[c] = start;
   a.o_len[c] = len;
