@@ -91,6 +91,8 @@ struct Ctx {
   uint32_t gen = 0;     // generation tag of has_child / childof
   uint64_t last_n = 0;  // chain length of the previous call (index bucket sizing)
   Plan* h_plan = nullptr;  // pinned host copy
+  uint64_t* h_pub = nullptr;  // pinned: idx_emit's published outcome (IdxArgs::pub)
+  uint32_t pub_seq = 0;
   // batch writer (srd_batch_write): side copy stream, double-buffer events,
   // pinned entry tables and pinned bounce buffers (non-contiguous inputs)
   hipStream_t cstream = nullptr;
@@ -274,6 +276,35 @@ static hipError_t spin_sync(hipStream_t s) {
 #endif
 }
 
+// Spin until idx_emit's published words (IdxArgs::pub) all carry this
+// call's seq; if the stream completes without them (an error), fail.
+static int wait_publish(Ctx* c, uint64_t* w) {
+  const uint32_t seq = c->pub_seq;
+  volatile const uint64_t* pub = c->h_pub;
+  for (uint64_t it = 0;; it++) {
+    bool ok = true;
+    for (int i = 0; i < PUB_WORDS; i++) {
+      w[i] = pub[i];
+      ok = ok && (uint32_t)(w[i] >> 32) == seq;
+    }
+    if (ok) return 0;
+    if ((it & 1023) == 1023) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e == hipSuccess) {  // finished: re-read once, the words may have landed meanwhile
+        bool ok2 = true;
+        for (int i = 0; i < PUB_WORDS; i++) {
+          w[i] = pub[i];
+          ok2 = ok2 && (uint32_t)(w[i] >> 32) == seq;
+        }
+        if (ok2) return 0;
+        set_err("internal: the glue finished without publishing its outcome");
+        return SRD_ERR_INTERNAL;
+      }
+      if (e != hipErrorNotReady) HIPCHK(e);
+    }
+  }
+}
+
 int read_counters(Ctx* c, uint64_t* h) {
   HIPCHK(hipMemcpyAsync(h, P<uint64_t>(c, B_COUNTERS), 8 * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -349,6 +380,8 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   // timeline at each record (four per call)
   for (auto& e : c->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventReleaseToDevice));
   HIPCHK(hipHostMalloc((void**)&c->h_plan, sizeof(Plan), hipHostMallocDefault));
+  HIPCHK(hipHostMalloc((void**)&c->h_pub, 64, hipHostMallocCoherent));  // fine-grained: the device's system-scope stores land here
+  memset(c->h_pub, 0, 64);
   c->stage_workers = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
@@ -366,6 +399,7 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->h_plan) hipHostFree(c->h_plan);
+  if (c->h_pub) hipHostFree(c->h_pub);
   if (c->h_out) hipHostFree(c->h_out);
   for (int i = 0; i < 2; i++) {
     if (c->pin_ent[i]) hipHostFree(c->pin_ent[i]);
@@ -741,6 +775,10 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   TRY(next_lgen(c));
   IdxArgs ia = index_args(c, log2_nbk);
   ia.alias = fused ? 1u : 0u;
+  if (fused) {
+    ia.pub = c->h_pub;
+    ia.pub_seq = ++c->pub_seq;
+  }
   ia.kh = kh;
   ia.mo = mo;
   ia.n_dev = n_dev;
@@ -969,8 +1007,29 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
         c->ev3_recorded = true;
       }
       HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(spin_sync(c->stream));
-      hp = *c->h_plan;
+      // the outcome idx_emit publishes to pinned memory when it starts; a
+      // proven chain whose index aliases the chain arrays needs nothing else
+      // (the plan copy after it finishes on its own); anything else waits
+      // for the stream and reads the whole plan
+      bool fast = false;
+      if (!index_global_env() && !(c->timing >= SRD_TIMING_CALL)) {
+        uint64_t w[PUB_WORDS];
+        TRY(wait_publish(c, w));
+        const uint32_t fl = (uint32_t)w[0];
+        if ((fl & 0x3ffu) == 0x100u) {  // status 0, aliased index, no bucket overflow
+          fast = true;
+          hp = Plan{};
+          hp.n_chain = (uint32_t)w[1];
+          hp.n_index = (uint32_t)w[2];
+          hp.n_bad = (uint32_t)w[3];
+          hp.K = (uint32_t)w[4];
+          hp.idx_alias = 1;
+        }
+      }
+      if (!fast) {
+        HIPCHK(spin_sync(c->stream));
+        hp = *c->h_plan;
+      }
       if (debug_env()) {
         fprintf(stderr, "plan K=%lu n_chain=%lu root_t=%lu start=%lu n_index=%lu bad=%lu slow=%lu st=%u nroot=%u "
                 "troot=%u idxov=%u log2nbk=%u capK=%lu rounds=%d\n",

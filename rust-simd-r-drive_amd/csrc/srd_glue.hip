@@ -434,6 +434,7 @@ constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
 // below IDX_TCAP, and an overflowing one sends the build to the global table)
 constexpr int IDX_BUCKET_AVG = 1280;
 constexpr uint64_t IDX_EMPTY = ~0ull;
+constexpr int PUB_WORDS = 5;  // flags, n_chain, n_index, n_bad, K
 
 struct IdxArgs {
   const uint64_t* kh;    // chain key hashes (o_kh)
@@ -451,6 +452,12 @@ struct IdxArgs {
   uint8_t* latest;       // [n] == lgen: NOT the latest entry of its key (idx_dedup writes only those)
   uint8_t lgen;          // this build's generation (1..255; the host clears the array on wrap)
   uint32_t alias;        // fused pass: with no non-latest entry idx_emit writes nothing (Plan::idx_alias)
+  // fused pass: idx_emit's block 0 publishes the call's outcome straight to
+  // pinned host memory (PUB_WORDS words, each (seq << 32) | value) as soon
+  // as it starts -- the host reads it there instead of waiting for the plan
+  // copy and the stream's completion signal
+  uint64_t* pub;
+  uint32_t pub_seq;
   uint32_t* ccount;      // [GLUE_BLOCKS] NON-latest entries per chain chunk (idx_dedup -> idx_emit; zero before)
   uint64_t* okey;
   uint64_t* opacked;
@@ -917,6 +924,20 @@ __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.plan->n_index = n - nl_total;
     a.plan->idx_alias = a.alias && nl_total == 0;
+    if (a.pub) {
+      // every value < 2^31 (the dense capacity bounds K and the chain); one
+      // 8-byte system-scope store each: the host accepts the words once all
+      // carry this call's seq
+      const Plan* pl = a.plan;
+      const uint64_t tag = (uint64_t)a.pub_seq << 32;
+      const uint32_t fl = (pl->status & 0xffu) | (a.alias && nl_total == 0 ? 0x100u : 0u) |
+                          (pl->idx_overflow ? 0x200u : 0u);
+      const uint64_t w[PUB_WORDS] = {tag | fl, tag | (uint32_t)pl->n_chain, tag | (uint32_t)(n - nl_total),
+                                     tag | (uint32_t)pl->n_bad, tag | (uint32_t)pl->K};
+#pragma unroll
+      for (int i = 0; i < PUB_WORDS; i++)
+        __hip_atomic_store(a.pub + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   // every entry the latest of its key (a store without overwrites): the
   // index is the chain's (key_hash, packed) arrays chain_finalize wrote
