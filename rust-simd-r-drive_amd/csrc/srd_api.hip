@@ -2623,6 +2623,16 @@ extern "C" int srd_compact_device(srd_ctx* c, const uint8_t* d_file, uint64_t fl
   return 0;
 }
 
+#ifdef SRD_WAVE_STAMPS
+// timing-only build: the last scan's per-wave end stamps and per-block start
+// stamps (s_memrealtime, 100 MHz)
+extern "C" int srd_debug_wave_stamps(uint64_t* out) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_stamp), sizeof(uint64_t) * (8192 + 1024)));
+  return 0;
+}
+#endif
+
 // host self-test of the CRC algebra (no GPU): checks the tables against a
 // byte-wise CRC on pseudo-random data with the same combine the kernels use.
 extern "C" int srd_selftest_host(void) {

@@ -69,6 +69,9 @@ struct DevTables {
   uint32_t mx64[4][256];           // v -> v * X^64 byte tables (the long-entry Horner step)
 };
 __device__ DevTables g_tabs;
+#ifdef SRD_WAVE_STAMPS
+__device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]: block b's start
+#endif
 
 struct ScanArgs {
   const uint8_t* file;
@@ -364,6 +367,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     for (uint32_t i = threadIdx.x; i < a.n_zero_words; i += blockDim.x) a.zero_words[i] = 0;
     if (threadIdx.x == 0 && a.sentinel) *a.sentinel = 0;
   }
+#ifdef SRD_WAVE_STAMPS
+  if (threadIdx.x == 0) g_wave_stamp[8192 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
   load_crc_lds(lds);
 
   const int lane = threadIdx.x & 63;
@@ -814,6 +820,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   if (lane == 0) {
     a.wave_total[w] = wtotal | (ovf ? (1ull << 63) : 0ull);
     a.wave_root[w] = rootmax;  // wave-uniform already
+#ifdef SRD_WAVE_STAMPS  // timing-only build (tools/wave_stamps.py): each wave's end, 100 MHz clock
+    if (w < 8192) g_wave_stamp[w] = __builtin_amdgcn_s_memrealtime();
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint32_t& s_last = lds.s_last;
