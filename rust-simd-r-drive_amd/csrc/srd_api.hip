@@ -75,6 +75,7 @@ struct Ctx {
   uint32_t grown_cap = 64;   // the cap the last overflow needed ...
   uint64_t grown_bytes = 0;  // ... for a store (span) of this many bytes
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
+  uint32_t scan_wq[4] = {0, 0, 0, 0};  // ScanPart::wq (scan_weights())
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -359,6 +360,23 @@ int walk_and_mark(Ctx* c, const int64_t* par, const uint64_t* slot, uint64_t n, 
 
 struct srd_ctx : Ctx {};
 
+// ScanPart::wq, the per-wave share of each age group (waves 4q..4q+3 of a
+// block).  Default: inverse to the finish times an even split gave on MI355X
+// (wave slots 0-3 / 4-7 / 8-11 / 12-15 ended at 1 : 1.069 : 1.125 : 1.179,
+// tools/wave_stamps.py); SRD_SCAN_WEIGHTS="a,b,c,d" sets relative shares
+// ("1,1,1,1" is the even split).
+static void scan_weights(uint32_t (&wq)[4]) {
+  double f[4] = {1.0, 1.0 / 1.069, 1.0 / 1.125, 1.0 / 1.179};
+  if (const char* e = getenv("SRD_SCAN_WEIGHTS")) {
+    double g[4];
+    if (sscanf(e, "%lf,%lf,%lf,%lf", &g[0], &g[1], &g[2], &g[3]) == 4 && g[0] > 0 && g[1] > 0 && g[2] > 0 && g[3] > 0)
+      for (int q = 0; q < 4; q++) f[q] = g[q];
+  }
+  const double sum = f[0] + f[1] + f[2] + f[3];
+  uint32_t used = 0;
+  for (int q = 0; q < 3; q++) used += wq[q] = (uint32_t)(16384.0 * f[q] / sum);
+  wq[3] = 16384 - used;
+}
 extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   if (!out) { set_err("null out"); return SRD_ERR_ARG; }
   int n = 0;
@@ -386,6 +404,7 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->scan_blocks = (unsigned)ncu;
+  scan_weights(c->scan_wq);
   *out = c;
   return 0;
 }
@@ -433,6 +452,22 @@ static void grow_cap(Ctx* c, uint64_t bytes) {
   c->cap = (uint32_t)std::min<uint64_t>((uint64_t)c->cap * 4, SPAN_BYTES);
   c->grown_cap = c->cap;
   c->grown_bytes = bytes;
+}
+
+static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g) {
+  ScanPart p{};
+  p.s_lo = s_lo;
+  p.ns = ns;
+  p.g = g;
+  for (int q = 0; q < 4; q++) p.wq[q] = c->scan_wq[q];
+  return p;
+}
+// an upper bound on the spans of one wave
+static uint64_t part_max_wave_spans(const ScanPart& p) {
+  if (!p.g) return 1;
+  const uint32_t wmax = std::max(std::max(p.wq[0], p.wq[1]), std::max(p.wq[2], p.wq[3]));
+  const uint64_t nb = (p.ns + p.g - 1) / p.g;
+  return (nb * wmax + 65535) / 65536 + 1;
 }
 
 // the scan kernel's per-wave results and last-block reduction (ScanArgs)
@@ -658,6 +693,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     TRY(scan_wave_args(c, &a));
     if (n_spans) {
       unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
+      a.part = scan_part(c, 0, n_spans, g);
       hipEvent_t e0 = c->timing >= SRD_TIMING_SCAN ? c->ev[0] : nullptr;
       if (full)
         launch_scan<true>(g, a, c->stream, e0, c->ev[1]);
@@ -847,11 +883,12 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     // index buckets: ~IDX_BUCKET_AVG chain entries per bucket
     const uint64_t n_est = std::max<uint64_t>(std::max<uint64_t>(c->last_n, (flen - span_off) / 4096), 1);
     const uint32_t log2_nbk = index_log2_buckets(n_est);
-    // the scan's partition: total_waves waves of spw spans; each wave's
-    // records are dense in its region of wcap = spw * cap slots
+    // the scan's partition (ScanPart): total_waves waves of at most spw
+    // spans; each wave's records are dense in its region of wcap = spw * cap slots
     const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
+    const ScanPart part = scan_part(c, s_lo, ns_rel, g);
     const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
-    const uint64_t spw = (ns_rel + total_waves - 1) / total_waves;
+    const uint64_t spw = part_max_wave_spans(part);
     const uint64_t wcap = spw * c->cap;
     // the glue's record slots are 32-bit (d_slot): stores above ~1 TiB take the full pass
     if (total_waves * wcap >= (1ull << 32)) return 0;
@@ -872,6 +909,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     // per-tile / per-span arrays hold the resident range only: their base
     // pointers are shifted so kernels index them by absolute tile / span
     ScanArgs a{};
+    a.part = part;
     a.file = d_file;
     a.flen = flen;
     a.n_tiles = n_tiles;
@@ -904,7 +942,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.span_first = a.span_first;
     l.wave_base = a.wave_base;
     l.wave_total = a.wave_total;
-    l.spw = spw;
+    l.part = part;
     l.wcap = wcap;
     l.c_m = a.c_m;
     l.c_rec = a.c_rec;

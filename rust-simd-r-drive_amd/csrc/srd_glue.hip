@@ -173,7 +173,7 @@ struct Link2Args {
   const uint32_t* span_first;  // scan_kernel: span's first record inside its wave's region
   const uint64_t* wave_base;   // scan_kernel's last block: dense index of each scan wave's first record
   const uint64_t* wave_total;  // records per scan wave (bit 63: overflow)
-  uint64_t spw;                // spans per scan wave (the scan's partition)
+  ScanPart part;               // the scan's wave partition (span -> wave)
   uint64_t wcap;               // record slots per scan wave
   const uint64_t* c_m;
   u32x4* c_rec;  // tombstone flags are set in place
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
   }
   const uint64_t sp = a.s_lo + (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
   if (sp >= a.n_spans) return;
-  const uint64_t w = (sp - a.s_lo) / a.spw;
+  const uint64_t w = part_span_wave(a.part, sp - a.s_lo);
   const uint32_t n = a.span_count[sp], first = a.span_first[sp];
   const uint64_t gw = w * a.wcap, gb = a.wave_base[w] + first;
   for (uint32_t i = threadIdx.x & 3; i < n; i += 4) {
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     // order: one load instead of a binary search.
     int64_t par = hp && mprev == mp ? (int64_t)(g - 1) : PAR_MISS;
     if (par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
-      const uint64_t w2 = (sp2 - a.s_lo) / a.spw;
+      const uint64_t w2 = part_span_wave(a.part, sp2 - a.s_lo);
       const uint32_t f2 = a.span_first[sp2];
       const uint32_t n2 = (uint32_t)min<uint64_t>(a.span_count[sp2], a.wcap - min<uint64_t>(f2, a.wcap));
       uint32_t lo = 0, hi = n2;

@@ -73,7 +73,52 @@ __device__ DevTables g_tabs;
 __device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]: block b's start
 #endif
 
+// The scan's wave partition (both passes; link2 inverts it).  Block b of g
+// takes the resident spans [st(b), st(b+1)), st(b) = b*ns/g; inside a block
+// wave v takes the share [cw(v), cw(v+1)) (units of 1/65536) of the block's
+// spans.  Waves of one SIMD do not progress equally: the SIMD issues for
+// its oldest waves first, so with an even split waves 0-3 (the oldest on
+// each SIMD) finished ~15% before waves 12-15 (tools/wave_stamps.py); the
+// per-age-group shares wq[q] (waves 4q..4q+3) even out the finish times.
+struct ScanPart {
+  uint64_t s_lo;   // first resident span
+  uint64_t ns;     // resident spans
+  uint32_t g;      // scan blocks
+  uint32_t wq[4];  // per-wave share of age group q; 4 * (wq[0] + .. + wq[3]) == 65536
+};
+// cumulative share of the waves below v (v <= 16)
+__host__ __device__ __forceinline__ uint64_t part_cw(const ScanPart& p, uint32_t v) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int k = (int)v - 4 * q;
+    c += (uint64_t)(k <= 0 ? 0 : k >= 4 ? 4 : k) * p.wq[q];
+  }
+  return c;
+}
+__host__ __device__ __forceinline__ uint64_t part_block_start(const ScanPart& p, uint64_t b) {
+  return b * p.ns / p.g;
+}
+// wave v of block b: resident-relative spans [*r0, *r1)
+__host__ __device__ __forceinline__ void part_wave_range(const ScanPart& p, uint64_t b, uint32_t v,
+                                                         uint64_t* r0, uint64_t* r1) {
+  const uint64_t bs = part_block_start(p, b), nb = part_block_start(p, b + 1) - bs;
+  *r0 = bs + ((nb * part_cw(p, v)) >> 16);
+  *r1 = bs + ((nb * part_cw(p, v + 1)) >> 16);
+}
+// the scan wave (b * 16 + v) holding resident-relative span rel < ns
+__device__ __forceinline__ uint64_t part_span_wave(const ScanPart& p, uint64_t rel) {
+  uint64_t b = rel * p.g / p.ns;
+  while (b + 1 < p.g && part_block_start(p, b + 1) <= rel) b++;
+  const uint64_t bs = part_block_start(p, b), nb = part_block_start(p, b + 1) - bs, o = rel - bs;
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t j = 1; j < 16; j++) v += o >= ((nb * part_cw(p, j)) >> 16) ? 1u : 0u;
+  return b * 16 + v;
+}
+
 struct ScanArgs {
+  ScanPart part;
   const uint8_t* file;
   uint64_t flen;
   uint64_t n_tiles, n_spans;
@@ -384,14 +429,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   uint32_t* win = lds.win[wv];
   const uint32_t nib_lane = lds_off(lds.nib) + 4u * (lane & 31);  // 2 KiB-aligned table base + the lane's bank
 
-  // balanced contiguous tile range per wave (whole spans)
+  // contiguous tile range per wave (whole spans, ScanPart)
   const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES_V2;
   const uint64_t w = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
-  const uint64_t s_lo = a.k_lo / SPAN_TILES;
-  const uint64_t spw = (a.n_spans - s_lo + total_waves - 1) / total_waves;
-  const uint64_t s0 = s_lo + w * spw;
-  uint64_t k0 = s0 * SPAN_TILES;
-  uint64_t k1 = min((s0 + spw) * SPAN_TILES, a.n_tiles);
+  uint64_t r0, r1;
+  part_wave_range(a.part, blockIdx.x, (uint32_t)wv, &r0, &r1);
+  uint64_t k0 = (a.part.s_lo + r0) * SPAN_TILES;
+  uint64_t k1 = min((a.part.s_lo + r1) * SPAN_TILES, a.n_tiles);
   if (k0 >= k1) k0 = k1 = a.k_lo;  // no tiles (the loops below do nothing): the wave joins the epilogue
 
   if (!FULL && start_not_a_node(file, flen)) {
