@@ -545,10 +545,14 @@ static int alloc_hash(Ctx* c, uint64_t n) {
   return 0;
 }
 
-static bool index_global_env() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("SRD_INDEX_GLOBAL"); v = (e && *e && *e != '0') ? 1 : 0; }
-  return v;
+// timing-only builds (make variant DEFS=-DSRD_INDEX_GLOBAL): every index by
+// the global table; the product build takes it only on a bucket overflow
+static constexpr bool index_global_env() {
+#ifdef SRD_INDEX_GLOBAL
+  return true;
+#else
+  return false;
+#endif
 }
 
 // KeyIndexer::build over n (key_hash, meta_off) pairs in file order with one
@@ -1036,7 +1040,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
           sa, f, index_args(c, log2_nbk), log2_nbk);
       KCHK(c, "chain_finalize_kernel");
       HIPCHK(hipGetLastError());
-      // ---- KeyIndexer::build (bucketed; SRD_INDEX_GLOBAL=1: one global table, timing experiments) ----
+      // ---- KeyIndexer::build (bucketed; the global table in SRD_INDEX_GLOBAL timing builds) ----
       if (!index_global_env())
         TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
                                   P<uint64_t>(c, B_IPACKED), pl, true));
@@ -1074,7 +1078,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
                 (unsigned long)hp.K, (unsigned long)hp.n_chain, (unsigned long)hp.root_t, (unsigned long)hp.start,
                 (unsigned long)hp.n_index, (unsigned long)hp.n_bad, (unsigned long)hp.n_slow, hp.status, hp.nroot,
                 hp.troot, hp.idx_overflow, log2_nbk, (unsigned long)capK, rounds);
-        fprintf(stderr, "shape: dangling=%u branch=%u\n", hp.why[0], hp.why[1]);
       }
       if (!timed && c->timing >= SRD_TIMING_SCAN) {
         float ms = 0;

@@ -2,30 +2,41 @@
 // after srd_kernels.hip).
 //
 // Everything between the streaming scan and the final result runs with the
-// counts kept in device memory (struct Plan), so the host enqueues the whole
-// pass and synchronises once at the end:
+// counts kept in device memory (struct Plan); the host enqueues the pass and
+// waits once, on the outcome idx_emit publishes to pinned host memory:
 //
-//   link2   parent lookup per candidate (4 lanes per span), marks has_child
-//   child2  every core node (has a child, or is the start node at file_len-20)
-//           publishes itself as its parent's child: childof[p] = gen:g
-//   check   shape test + per-block core counts: the core nodes must form ONE
-//           chain from the start down to a root (each core node's parent
-//           names it as the child, every core node but the start has a core
-//           child, exactly one core node links to a root).  Leaves (false
-//           candidates nobody links to) are ignored -- the same pruning as
-//           recover_valid_chain's walk only ever following back-pointers
-//           from file_len (data_store.rs:404-470).  A failed test sends the
-//           call to the full pass; it never changes a result.
-//   plan    one block: scans the block counts, decides n_chain / status
-//   scatter chain_g[1 + rank] = record slot of core node g (file order)
-//   finalize / slow (srd_kernels.hip) with n_chain read from the plan
-//   index   KeyIndexer::build (key_indexer.rs:98-124) as a bucketed build:
-//           hist -> exclusive scan -> scatter into XXH3 buckets -> one block
-//           per bucket dedups in an LDS open-addressing table (latest wins)
-//           -> count / scan / emit in chain order.
+//   scan            (srd_kernels.hip) strong candidates only, each wave's
+//                   records dense in its region (ScanPart), wave bases by the
+//                   scan's last block; block 0 zeroes the plan
+//   link2           4 lanes per span: node test of single-candidate records,
+//                   parent lookup (previous record, else a binary search in
+//                   the parent's span), 32-bit d_par / d_slot, and every node
+//                   claims its parent: childof[p] = max(gen:g); zeroes the
+//                   index bucket fills
+//   check           shape test from the claims alone: the core nodes (claimed
+//                   by someone, or the start node at file_len - 20) must form
+//                   ONE chain from the start down to a root -- each core node's
+//                   parent claimed by it, exactly one core node linking to a
+//                   root.  Leaves (false candidates nobody links to) are
+//                   ignored, the pruning recover_valid_chain's walk gets from
+//                   only following back-pointers from file_len
+//                   (data_store.rs:404-470).  Per-block core counts.  A failed
+//                   test retries with more prune rounds (marks_from_claims),
+//                   then sends the call to the full pass; it never changes a
+//                   result.
+//   chain_finalize  plan (every block derives it, block 0 publishes), the chain
+//                   rank of each core node, the per-entry outputs and CRC from
+//                   the scan's pieces (slow entries by one wave each), and
+//                   KeyIndexer::build's bucket claims + scatter
+//   idx_dedup       one block per XXH3 bucket: marks the non-latest entries
+//                   (generation bytes); none marked -> the index aliases
+//                   (o_kh, o_packed)
+//   idx_emit        compacts the latest entries in chain order (or nothing,
+//                   aliased) and publishes the outcome (PUB_WORDS) to the host
 //
-// Generation tags (gen:g in one u64, gen in has_child) make the per-node
-// marks self-invalidating between calls, so no per-call memsets are needed.
+// Generation tags (gen:g in one u64, lgen bytes for the non-latest marks)
+// make the per-node marks self-invalidating between calls, so no per-call
+// memsets are needed.
 #pragma once
 
 namespace srd {
@@ -46,7 +57,6 @@ struct Plan {
   uint32_t troot;      // file_len itself is a root tail
   uint32_t idx_overflow;
   uint32_t idx_alias;  // every chain entry is its key's latest: the index IS (o_kh, o_packed) (idx_emit)
-  uint32_t why[2];     // shape failures (diagnostics): dangling parent, branch
 };
 constexpr uint32_t ST_NOSTART = 1, ST_SHAPE = 2, ST_ROOTS = 4, ST_CAPK = 8, ST_OVERFLOW = 16;
 constexpr uint64_t NO_NODE = ~0ull;
@@ -411,10 +421,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
         a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
       } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
         fail = true;  // dangling: the chain through g is broken (only the start node can get here)
-        atomicAdd(&a.plan->why[0], 1u);
       } else if (cp[r] != (tag | g[r])) {
         fail = true;  // branch: another node holds the claim on the same parent
-        atomicAdd(&a.plan->why[1], 1u);
       }
     }
   }

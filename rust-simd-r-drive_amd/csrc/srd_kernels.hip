@@ -61,16 +61,17 @@ struct DevTables {
   uint32_t x32768;
   uint32_t pow8[64];
   uint32_t invpow[4097];
-  uint32_t nib[8 * 16 * 32];       // half-tile lane-weight nibble tables
+  alignas(16) uint32_t nib[8 * 16 * 32];  // half-tile lane-weight nibble tables
   uint32_t m16k[4][256];           // v -> v * x^16384 byte tables
-  uint32_t last[3][4][256];        // chain q's last slice-by-4 step, shifted: v -> v * x^(32 + 128 (3 - q))
+  alignas(16) uint32_t last[3][4][256];   // chain q's last slice-by-4 step, shifted: v -> v * x^(32 + 128 (3 - q))
   uint32_t xtile[65];              // X^e, X = x^32768 (one tile), e = 0..64
   uint32_t xt64[65];               // X^(64 q), q = 0..64 (with xtile: X^n for n < 4160 in one multiply)
   uint32_t mx64[4][256];           // v -> v * X^64 byte tables (the long-entry Horner step)
 };
 __device__ DevTables g_tabs;
 #ifdef SRD_WAVE_STAMPS
-__device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]: block b's start
+__device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]: block b's start;
+                                                // [8192 + 256 + b]: its tables loaded; [8192 + 1023]: the epilogue's end
 #endif
 
 // The scan's wave partition (both passes; link2 inverts it).  Block b of g
@@ -368,14 +369,23 @@ __device__ __forceinline__ uint32_t half_suffix_xor(uint32_t v, int lane) {
 }
 
 // the LDS tables of the line-CRC machinery (crc_line*, lane_weight); ends
-// with a block barrier
+// with a block barrier.  One 1024-thread block: every thread issues its three
+// global loads (one table word, 16 B of the nibble tables, 16 B of the last-
+// step tables) before any LDS store, then writes its word's 32 replicas with
+// 16-byte stores (a load -> store loop per word took ~10 us of the scan)
 __device__ __forceinline__ void load_crc_lds(ScanLds& lds) {
-  for (int i = threadIdx.x; i < 4 * 256 * 32; i += blockDim.x) {
-    const int hi = i >> 14, b = (i >> 6) & 255, t = hi * 2 + ((i >> 5) & 1);
-    lds.tab[i] = g_tabs.tab[t][b];
-  }
-  for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) lds.nib[i] = g_tabs.nib[i];
-  for (int i = threadIdx.x; i < 3 * 4 * 256; i += blockDim.x) lds.last[i] = (&g_tabs.last[0][0][0])[i];
+  static_assert(SCAN_WAVES_V2 * 64 == 1024 && sizeof(lds.nib) == 1024 * 16 && sizeof(lds.last) <= 1024 * 16,
+                "one 16-byte piece of nib / last per thread");
+  const uint32_t u = threadIdx.x;  // tab word u: hi = u >> 9, b = (u >> 1) & 255, t = 2 hi + (u & 1)
+  const uint32_t tv = g_tabs.tab[2 * (u >> 9) + (u & 1)][(u >> 1) & 255];
+  const u32x4 nv = ((const u32x4*)g_tabs.nib)[u];
+  constexpr uint32_t NLAST = sizeof(lds.last) / 16;
+  const u32x4 lv = ((const u32x4*)&g_tabs.last[0][0][0])[u < NLAST ? u : 0];
+  u32x4* const tr = (u32x4*)(lds.tab + 32 * u);  // tab_lookup's layout: word (hi, b, t & 1, copy)
+#pragma unroll
+  for (int j = 0; j < 8; j++) tr[j] = u32x4{tv, tv, tv, tv};
+  ((u32x4*)lds.nib)[u] = nv;
+  if (u < NLAST) ((u32x4*)lds.last)[u] = lv;
   __syncthreads();
 }
 // lane l's slice-by-4 lookup bases (tab_lookup)
@@ -416,6 +426,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   if (threadIdx.x == 0) g_wave_stamp[8192 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
   load_crc_lds(lds);
+#ifdef SRD_WAVE_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 256) g_wave_stamp[8192 + 256 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   const int lane = threadIdx.x & 63;
   // wave id via readfirstlane: provably uniform, so all tile bookkeeping
@@ -881,43 +894,81 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // exclusive prefix of the wave counts: thread t owns waves [t*q, (t+1)*q)
-  uint64_t* s_part = (uint64_t*)lds.tab;  // the CRC tables are dead now: 1024 partials
+  // exclusive prefix of the wave counts: thread t owns waves [t*q, (t+1)*q).
+  // q <= 4 (up to 256 blocks): the thread's waves are loaded together into
+  // registers (one round trip instead of 2q dependent ones: the last block's
+  // epilogue is on the critical path of every call)
+  constexpr int QR = 4;
+  uint64_t* s_wsum = (uint64_t*)lds.tab;  // the CRC tables are dead now
   uint64_t* s_root = lds.s_root;
   uint64_t* s_ovf = lds.s_ovf;
   const uint32_t T = blockDim.x, t = threadIdx.x;
   const uint64_t q = (total_waves + T - 1) / T;
   uint64_t sum = 0, rmax = 0, o = 0;
-  for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
-    const uint64_t v = a.wave_total[i];
-    sum += v & ~(1ull << 63);
-    o |= v >> 63;
-    rmax = max(rmax, a.wave_root[i]);
+  uint64_t vt[QR];
+  if (q <= QR) {
+    uint64_t vr[QR];
+#pragma unroll
+    for (int j = 0; j < QR; j++) {
+      const uint64_t i = min(t * q + j, total_waves - 1);
+      vt[j] = a.wave_total[i];
+      vr[j] = a.wave_root[i];
+    }
+#pragma unroll
+    for (int j = 0; j < QR; j++) {
+      const bool in = (uint64_t)j < q && t * q + j < total_waves;
+      vt[j] = in ? vt[j] : 0ull;
+      sum += vt[j] & ~(1ull << 63);
+      o |= vt[j] >> 63;
+      rmax = max(rmax, in ? vr[j] : 0ull);
+    }
+  } else {
+    for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
+      const uint64_t v = a.wave_total[i];
+      sum += v & ~(1ull << 63);
+      o |= v >> 63;
+      rmax = max(rmax, a.wave_root[i]);
+    }
   }
-  s_part[t] = sum;
   rmax = wave_max_u64(rmax);
   for (int d = 32; d > 0; d >>= 1) o |= __shfl_xor(o, d);
-  if (lane == 0) { s_root[wv] = rmax; s_ovf[wv] = o; }
-  __syncthreads();
-  for (uint32_t d = 1; d < T; d <<= 1) {  // inclusive Hillis-Steele scan of the T partials
-    const uint64_t x = t >= d ? s_part[t - d] : 0;
-    __syncthreads();
-    s_part[t] += x;
-    __syncthreads();
+  // inclusive scan of the T partials: inside each wave, then over the waves
+  uint64_t x = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
   }
-  uint64_t run = t ? s_part[t - 1] : 0;
-  for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
-    a.wave_base[i] = run;
-    run += a.wave_total[i] & ~(1ull << 63);
+  if (lane == 63) { s_wsum[wv] = x; s_root[wv] = rmax; s_ovf[wv] = o; }
+  __syncthreads();
+  uint64_t wpre = 0;
+  for (int i = 0; i < wv; i++) wpre += s_wsum[i];
+  uint64_t run = wpre + x - sum;
+  if (q <= QR) {
+#pragma unroll
+    for (int j = 0; j < QR; j++) {
+      if ((uint64_t)j < q && t * q + j < total_waves) {
+        a.wave_base[t * q + j] = run;
+        run += vt[j] & ~(1ull << 63);
+      }
+    }
+  } else {
+    for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
+      a.wave_base[i] = run;
+      run += a.wave_total[i] & ~(1ull << 63);
+    }
   }
   if (t == 0) {
-    uint64_t mr = 0, oo = 0;
-    for (int i = 0; i < SCAN_WAVES_V2; i++) { mr = max(mr, s_root[i]); oo |= s_ovf[i]; }
-    *a.k_total = s_part[T - 1];
+    uint64_t mr = 0, oo = 0, tot = 0;
+    for (int i = 0; i < SCAN_WAVES_V2; i++) { mr = max(mr, s_root[i]); oo |= s_ovf[i]; tot += s_wsum[i]; }
+    *a.k_total = tot;
     a.counters[0] = mr;
     a.counters[1] = 0;
     a.counters[2] = oo;
     *a.done = 0;  // for the next launch on this context
+#ifdef SRD_WAVE_STAMPS
+    g_wave_stamp[8192 + 1023] = __builtin_amdgcn_s_memrealtime();
+#endif
   }
 }
 

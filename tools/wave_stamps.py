@@ -32,7 +32,14 @@ for rep in range(5):
     bend = we.reshape(256, 16).max(1)
     xcd = [round(float(bend[i::8].mean()), 1) for i in range(8)]
     wv = we.reshape(256, 16)
-    out.append({"block_start_us_max": round(float(bs.max()), 2), "wave_end_us_pct_0_1_10_50_90_99_100": [round(float(x), 1) for x in q],
+    ld = (st[8192 + 256:8192 + 512].astype(np.int64) - t0) / 100.0
+    bend_all = we.reshape(256, 16).max(1)
+    epi = (int(st[8192 + 1023]) - t0) / 100.0
+    out.append({"block_start_us_max": round(float(bs.max()), 2),
+                "tables_loaded_us_pct_50_100": [round(float(np.percentile(ld, 50)), 2), round(float(ld.max()), 2)],
+                "block_end_us_pct_0_10_50_90_100": [round(float(x), 1) for x in np.percentile(bend_all, [0, 10, 50, 90, 100])],
+                "block_end_mean": round(float(bend_all.mean()), 1),
+                "epilogue_end_us": round(epi, 1), "wave_end_us_pct_0_1_10_50_90_99_100": [round(float(x), 1) for x in q],
                 "block_end_mean_per_xcd": xcd,
                 "mean_end_by_wave_slot": [round(float(x), 1) for x in wv.mean(0)],
                 "std_over_blocks_of_slot_mean": round(float(wv.mean(1).std()), 1),
