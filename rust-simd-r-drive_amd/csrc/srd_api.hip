@@ -76,7 +76,6 @@ struct Ctx {
   uint64_t grown_bytes = 0;  // ... for a store (span) of this many bytes
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
   uint32_t scan_wq[4] = {0, 0, 0, 0};  // ScanPart::wq (scan_weights())
-  uint32_t scan_dyn_pct = 10;           // share of the spans claimed at run time (ScanPart chunks; SRD_SCAN_DYN)
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -131,7 +130,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
-  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_DYN,
+  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED,
   B_COUNT_
 };
 
@@ -406,7 +405,6 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->scan_blocks = (unsigned)ncu;
   scan_weights(c->scan_wq);
-  if (const char* e = getenv("SRD_SCAN_DYN")) c->scan_dyn_pct = (uint32_t)std::min(50, std::max(0, atoi(e)));
   *out = c;
   return 0;
 }
@@ -456,25 +454,12 @@ static void grow_cap(Ctx* c, uint64_t bytes) {
   c->grown_bytes = bytes;
 }
 
-// ScanPart over the resident spans [s_lo, s_lo + ns) for g blocks: the last
-// scan_dyn_pct % of them in chunks claimed at run time (stores of at least
-// 32 spans per wave; at most SCAN_MAX_CHUNKS chunks, so that the scan's last
-// block keeps the region counts in registers).  wcap / ccap: set by the caller.
-constexpr uint64_t SCAN_MAX_CHUNKS = 12288;
 static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g) {
   ScanPart p{};
   p.s_lo = s_lo;
   p.ns = ns;
-  p.ns_all = ns;
   p.g = g;
-  p.dyn_spans = 1;
   for (int q = 0; q < 4; q++) p.wq[q] = c->scan_wq[q];
-  const uint64_t pool = ns * c->scan_dyn_pct / 100;
-  if (g && ns >= 32ull * 16 * g && pool) {
-    p.dyn_spans = (uint32_t)std::max<uint64_t>(2, (pool + SCAN_MAX_CHUNKS - 1) / SCAN_MAX_CHUNKS);
-    p.n_dyn = (uint32_t)(pool / p.dyn_spans);
-    p.ns = ns - (uint64_t)p.n_dyn * p.dyn_spans;
-  }
   return p;
 }
 // an upper bound on the spans of one wave
@@ -485,22 +470,19 @@ static uint64_t part_max_wave_spans(const ScanPart& p) {
   return (nb * wmax + 65535) / 65536 + 1;
 }
 
-// the scan kernel's per-region results and last-block reduction, and the
-// chunk claim counters (ScanArgs; a->part set)
+// the scan kernel's per-wave results and last-block reduction (ScanArgs)
 static int scan_wave_args(Ctx* c, ScanArgs* a) {
-  const uint64_t W = std::max<uint64_t>(part_regions(a->part), 1);
+  const uint64_t W = (uint64_t)c->scan_blocks * SCAN_WAVES_V2;
   TRY(ensure(c, B_WTOT, W * 8));
   TRY(ensure(c, B_WROOT, W * 8));
   TRY(ensure(c, B_WBASE, W * 8));
   TRY(ensure(c, B_KTOT, 64));
   TRY(ensure_z(c, B_DONE, 64));  // zero once; the scan's last block resets it
-  TRY(ensure_z(c, B_DYN, SCAN_DYN_POOLS * SCAN_DYN_STRIDE * 4));  // likewise
   a->wave_total = P<uint64_t>(c, B_WTOT);
   a->wave_root = P<uint64_t>(c, B_WROOT);
   a->wave_base = P<uint64_t>(c, B_WBASE);
   a->k_total = P<uint64_t>(c, B_KTOT);
   a->done = P<uint32_t>(c, B_DONE);
-  a->dyn_next = P<uint32_t>(c, B_DYN);
   return 0;
 }
 
@@ -711,11 +693,11 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
     TRY(ensure(c, B_SPAN_FIRST, (n_spans + 1) * 4));
     a.span_first = P<uint32_t>(c, B_SPAN_FIRST);
-    // the full pass stores records at span * cap + slot (no regions)
-    const unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
-    a.part = scan_part(c, 0, n_spans, g);
+    a.wcap = 0;  // the full pass stores records at span * cap + slot
     TRY(scan_wave_args(c, &a));
     if (n_spans) {
+      unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
+      a.part = scan_part(c, 0, n_spans, g);
       hipEvent_t e0 = c->timing >= SRD_TIMING_SCAN ? c->ev[0] : nullptr;
       if (full)
         launch_scan<true>(g, a, c->stream, e0, c->ev[1]);
@@ -905,18 +887,16 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     // index buckets: ~IDX_BUCKET_AVG chain entries per bucket
     const uint64_t n_est = std::max<uint64_t>(std::max<uint64_t>(c->last_n, (flen - span_off) / 4096), 1);
     const uint32_t log2_nbk = index_log2_buckets(n_est);
-    // the scan's partition (ScanPart): static waves of at most spw spans,
-    // then chunks of dyn_spans; each range's records are dense in its own
-    // region (wcap = spw * cap slots, ccap = dyn_spans * cap)
+    // the scan's partition (ScanPart): total_waves waves of at most spw
+    // spans; each wave's records are dense in its region of wcap = spw * cap slots
     const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
-    ScanPart part = scan_part(c, s_lo, ns_rel, g);
+    const ScanPart part = scan_part(c, s_lo, ns_rel, g);
+    const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
     const uint64_t spw = part_max_wave_spans(part);
-    part.wcap = spw * c->cap;
-    part.ccap = (uint64_t)part.dyn_spans * c->cap;
-    const uint64_t slots = part_region_base(part, part_regions(part));
+    const uint64_t wcap = spw * c->cap;
     // the glue's record slots are 32-bit (d_slot): stores above ~1 TiB take the full pass
-    if (slots >= (1ull << 32)) return 0;
-    TRY(alloc_scan(c, nt_rel, std::max<uint64_t>(ns_rel, (slots + c->cap - 1) / c->cap)));
+    if (total_waves * wcap >= (1ull << 32)) return 0;
+    TRY(alloc_scan(c, nt_rel, std::max<uint64_t>(ns_rel, total_waves * spw)));
     TRY(ensure(c, B_SPAN_FIRST, (ns_rel + 1) * 4));
     TRY(alloc_fast(c, capK, log2_nbk));
     if (c->gen >= 0xFFFFFFF0u || c->gen == 0) {  // tag wrap: clear the marks once
@@ -944,6 +924,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.c_m = P<uint64_t>(c, B_CM);  // wave regions, indexed by the wave of this launch
     a.c_rec = P<u32x4>(c, B_CREC);
     a.span_first = P<uint32_t>(c, B_SPAN_FIRST) - s_lo;
+    a.wcap = wcap;
     a.counters = (unsigned long long*)cnt;
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
     a.k_lo = k_lo;
@@ -966,6 +947,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.wave_base = a.wave_base;
     l.wave_total = a.wave_total;
     l.part = part;
+    l.wcap = wcap;
     l.c_m = a.c_m;
     l.c_rec = a.c_rec;
     l.d_par = P<int32_t>(c, B_DPAR);
@@ -2688,11 +2670,6 @@ extern "C" int srd_compact_device(srd_ctx* c, const uint8_t* d_file, uint64_t fl
 extern "C" int srd_debug_wave_stamps(uint64_t* out) {
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_stamp), sizeof(uint64_t) * (8192 + 1024)));
-  return 0;
-}
-extern "C" int srd_debug_wave_dbg(uint64_t* out) {
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_dbg), sizeof(uint64_t) * 4096 * 4));
   return 0;
 }
 #endif

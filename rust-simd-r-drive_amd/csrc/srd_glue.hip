@@ -181,9 +181,10 @@ struct Link2Args {
   uint32_t gen;
   const uint32_t* span_count;
   const uint32_t* span_first;  // scan_kernel: span's first record inside its wave's region
-  const uint64_t* wave_base;   // scan_kernel's last block: dense index of each region's first record
-  const uint64_t* wave_total;  // records per region (bit 63: overflow)
-  ScanPart part;               // the scan's partition (span -> record region)
+  const uint64_t* wave_base;   // scan_kernel's last block: dense index of each scan wave's first record
+  const uint64_t* wave_total;  // records per scan wave (bit 63: overflow)
+  ScanPart part;               // the scan's wave partition (span -> wave)
+  uint64_t wcap;               // record slots per scan wave
   const uint64_t* c_m;
   u32x4* c_rec;  // tombstone flags are set in place
   int32_t* d_par;              // dense parent (PAR_ROOT / PAR_MISS)
@@ -195,9 +196,9 @@ struct Link2Args {
   uint32_t n_zero;
 };
 
-// 4 lanes per span.  The scan wrote each region's records densely in file
-// order: record i of span sp (region w) lives at slot part_region_base(w) +
-// span_first[sp] + i and has the dense index wave_base[w] + span_first[sp] + i.
+// 4 lanes per span.  The scan wrote each wave's records densely in file
+// order: record i of span sp lives at slot w*wcap + span_first[sp] + i and
+// has the dense index wave_base[w] + span_first[sp] + i.
 //
 // Every node with a parent claims it: childof[p] = max((gen << 32) | g).
 // check_kernel reads a node's core flag (someone links to it) and the claim
@@ -212,25 +213,25 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
   }
   const uint64_t sp = a.s_lo + (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
   if (sp >= a.n_spans) return;
-  const uint64_t w = part_span_region(a.part, sp - a.s_lo);
+  const uint64_t w = part_span_wave(a.part, sp - a.s_lo);
   const uint32_t n = a.span_count[sp], first = a.span_first[sp];
-  const uint64_t gw = part_region_base(a.part, w), wcap = part_region_cap(a.part, w), gb = a.wave_base[w] + first;
+  const uint64_t gw = w * a.wcap, gb = a.wave_base[w] + first;
   for (uint32_t i = threadIdx.x & 3; i < n; i += 4) {
-    if ((uint64_t)first + i >= wcap) return;  // region overflow: the scan reported it (ST_OVERFLOW)
+    if ((uint64_t)first + i >= a.wcap) return;  // wave overflow: scatter_plan reports ST_OVERFLOW
     const uint64_t gi = gw + first + i, g = gb + i;
     if (g >= a.capK) return;  // chain_finalize reports ST_CAPK
     const uint64_t m = a.c_m[gi];
     const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
-    // the previous record in file order: the slot before (same region),
-    // else the previous region's last record
+    // the previous record in file order: the slot before (same wave), else
+    // the previous wave's last record
     uint64_t mprev = 0;
     bool hp = true;
     if (first + i > 0) {
       mprev = a.c_m[gi - 1];
     } else {
       const uint64_t wt = w ? (a.wave_total[w - 1] & ~(1ull << 63)) : 0;
-      hp = wt > 0 && w > 0 && wt <= part_region_cap(a.part, w - 1);
-      if (hp) mprev = a.c_m[part_region_base(a.part, w - 1) + wt - 1];
+      hp = wt > 0 && wt <= a.wcap;
+      if (hp) mprev = a.c_m[(w - 1) * a.wcap + wt - 1];
     }
     const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     bool node = true;
@@ -248,12 +249,11 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     // order: one load instead of a binary search.
     int64_t par = hp && mprev == mp ? (int64_t)(g - 1) : PAR_MISS;
     if (par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
-      const uint64_t w2 = part_span_region(a.part, sp2 - a.s_lo);
-      const uint64_t cap2 = part_region_cap(a.part, w2);
+      const uint64_t w2 = part_span_wave(a.part, sp2 - a.s_lo);
       const uint32_t f2 = a.span_first[sp2];
-      const uint32_t n2 = (uint32_t)min<uint64_t>(a.span_count[sp2], cap2 - min<uint64_t>(f2, cap2));
+      const uint32_t n2 = (uint32_t)min<uint64_t>(a.span_count[sp2], a.wcap - min<uint64_t>(f2, a.wcap));
       uint32_t lo = 0, hi = n2;
-      const uint64_t* cm = a.c_m + part_region_base(a.part, w2) + f2;
+      const uint64_t* cm = a.c_m + w2 * a.wcap + f2;
       while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (cm[mid] < mp) lo = mid + 1; else hi = mid;

@@ -70,36 +70,22 @@ struct DevTables {
 };
 __device__ DevTables g_tabs;
 #ifdef SRD_WAVE_STAMPS
-__device__ uint64_t g_wave_dbg[4096 * 4];      // [4w]: static range end, [4w+1] chunks, [4w+2] claim ticks, [4w+3] first chunk start
 __device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]: block b's start;
                                                 // [8192 + 256 + b]: its tables loaded; [8192 + 1023]: the epilogue's end
 #endif
 
-// The scan's work partition (both passes; link2 inverts it).  Resident spans
-// [0, ns) are split statically: block b of g takes [st(b), st(b+1)),
-// st(b) = b*ns/g, and inside a block wave v takes the share [cw(v), cw(v+1))
-// (units of 1/65536) of the block's spans.  Waves of one SIMD do not progress
-// equally: the SIMD issues for its oldest waves first, so with an even split
-// waves 0-3 (the oldest on each SIMD) finished ~15% before waves 12-15
-// (tools/wave_stamps.py); the per-age-group shares wq[q] (waves 4q..4q+3)
-// even out the finish times.  The spans [ns, ns_all) form n_dyn chunks of
-// dyn_spans spans that the waves claim once their static range is done (8
-// claim counters, one per XCD pool, then the other pools): the CUs of one
-// launch finish ~60-80 us apart on a static split alone.
-// Record regions (optimistic pass): static wave w < tw = g*16 at w*wcap,
-// chunk c = region tw + c at tw*wcap + c*ccap; each region is dense in file
-// order and the regions are in file order.
-constexpr uint32_t SCAN_DYN_POOLS = 8;
-constexpr uint32_t SCAN_DYN_STRIDE = 64;  // one 256-B line per claim counter: same-line atomics serialize
+// The scan's wave partition (both passes; link2 inverts it).  Block b of g
+// takes the resident spans [st(b), st(b+1)), st(b) = b*ns/g; inside a block
+// wave v takes the share [cw(v), cw(v+1)) (units of 1/65536) of the block's
+// spans.  Waves of one SIMD do not progress equally: the SIMD issues for
+// its oldest waves first, so with an even split waves 0-3 (the oldest on
+// each SIMD) finished ~15% before waves 12-15 (tools/wave_stamps.py); the
+// per-age-group shares wq[q] (waves 4q..4q+3) even out the finish times.
 struct ScanPart {
-  uint64_t s_lo;       // first resident span
-  uint64_t ns;         // statically partitioned spans
-  uint64_t ns_all;     // resident spans
-  uint64_t wcap, ccap; // record slots of a static wave's / a chunk's region
-  uint32_t g;          // scan blocks
-  uint32_t wq[4];      // per-wave share of age group q; 4 * (wq[0] + .. + wq[3]) == 65536
-  uint32_t dyn_spans;  // spans per chunk
-  uint32_t n_dyn;      // chunks
+  uint64_t s_lo;   // first resident span
+  uint64_t ns;     // resident spans
+  uint32_t g;      // scan blocks
+  uint32_t wq[4];  // per-wave share of age group q; 4 * (wq[0] + .. + wq[3]) == 65536
 };
 // cumulative share of the waves below v (v <= 16)
 __host__ __device__ __forceinline__ uint64_t part_cw(const ScanPart& p, uint32_t v) {
@@ -121,24 +107,8 @@ __host__ __device__ __forceinline__ void part_wave_range(const ScanPart& p, uint
   *r0 = bs + ((nb * part_cw(p, v)) >> 16);
   *r1 = bs + ((nb * part_cw(p, v + 1)) >> 16);
 }
-// chunk c: resident-relative spans [*r0, *r1)
-__host__ __device__ __forceinline__ void part_chunk_range(const ScanPart& p, uint64_t c, uint64_t* r0, uint64_t* r1) {
-  *r0 = p.ns + c * p.dyn_spans;
-  *r1 = min(*r0 + p.dyn_spans, p.ns_all);
-}
-__host__ __device__ __forceinline__ uint64_t part_regions(const ScanPart& p) {
-  return (uint64_t)p.g * 16 + p.n_dyn;
-}
-__host__ __device__ __forceinline__ uint64_t part_region_base(const ScanPart& p, uint64_t r) {
-  const uint64_t tw = (uint64_t)p.g * 16;
-  return r < tw ? r * p.wcap : tw * p.wcap + (r - tw) * p.ccap;
-}
-__host__ __device__ __forceinline__ uint64_t part_region_cap(const ScanPart& p, uint64_t r) {
-  return r < (uint64_t)p.g * 16 ? p.wcap : p.ccap;
-}
-// the region (static wave b * 16 + v, or chunk) holding resident-relative span rel < ns_all
-__device__ __forceinline__ uint64_t part_span_region(const ScanPart& p, uint64_t rel) {
-  if (rel >= p.ns) return (uint64_t)p.g * 16 + (rel - p.ns) / p.dyn_spans;
+// the scan wave (b * 16 + v) holding resident-relative span rel < ns
+__device__ __forceinline__ uint64_t part_span_wave(const ScanPart& p, uint64_t rel) {
   uint64_t b = rel * p.g / p.ns;
   while (b + 1 < p.g && part_block_start(p, b + 1) <= rel) b++;
   const uint64_t bs = part_block_start(p, b), nb = part_block_start(p, b + 1) - bs, o = rel - bs;
@@ -176,20 +146,18 @@ struct ScanArgs {
   // block writes wave_base[w] = exclusive prefix of the counts, *k_total,
   // counters[0] (max root tail), [1] = 0, [2] (overflow); `done` counts the
   // finished blocks (the last block resets it to 0)
-  uint64_t* wave_total;  // per region (part_regions())
+  uint64_t* wave_total;
   uint64_t* wave_root;
   uint64_t* wave_base;
   uint64_t* k_total;
   uint32_t* done;
-  // optimistic pass: the records of each region (ScanPart) are DENSE in
-  // file order (consecutive span flushes fill whole cache lines; per-span
-  // slots left most lines partial: +0.11 ms of HBM writes at C2);
-  // span_first[s] = index of span s's first record inside its region (the
-  // full pass keeps span*cap + slot)
+  // optimistic pass: the records of scan wave w are DENSE in file order at
+  // [w*wcap, (w+1)*wcap) (consecutive span flushes fill whole cache lines;
+  // per-span slots left most lines partial: +0.11 ms of HBM writes at C2);
+  // span_first[s] = index of span s's first record inside its wave's region
+  // (the full pass keeps span*cap + slot)
   uint32_t* span_first;
-  // the chunk claim counters (SCAN_DYN_POOLS, SCAN_DYN_STRIDE apart; zero
-  // before the launch, reset by the last block)
-  uint32_t* dyn_next;
+  uint64_t wcap;
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -474,27 +442,27 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   uint32_t* win = lds.win[wv];
   const uint32_t nib_lane = lds_off(lds.nib) + 4u * (lane & 31);  // 2 KiB-aligned table base + the lane's bank
 
-  // the wave's ranges (whole spans, ScanPart): its static range, then the
-  // chunks it claims; each range records into its own region
-  const uint64_t total_regions = part_regions(a.part);
-  uint64_t rgn = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
-  uint64_t rbase = part_region_base(a.part, rgn), rcap = part_region_cap(a.part, rgn);
-  uint64_t k0, k1;
-  auto set_range = [&](uint64_t r0, uint64_t r1) {
-    k0 = (a.part.s_lo + r0) * SPAN_TILES;
-    k1 = min((a.part.s_lo + r1) * SPAN_TILES, a.n_tiles);
-    if (k0 >= k1) k0 = k1 = a.k_lo;  // no tiles (the loops below do nothing)
-  };
-  {
-    uint64_t r0, r1;
-    part_wave_range(a.part, blockIdx.x, (uint32_t)wv, &r0, &r1);
-    set_range(r0, r1);
+  // contiguous tile range per wave (whole spans, ScanPart)
+  const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES_V2;
+  const uint64_t w = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
+  uint64_t r0, r1;
+  part_wave_range(a.part, blockIdx.x, (uint32_t)wv, &r0, &r1);
+  uint64_t k0 = (a.part.s_lo + r0) * SPAN_TILES;
+  uint64_t k1 = min((a.part.s_lo + r1) * SPAN_TILES, a.n_tiles);
+  if (k0 >= k1) k0 = k1 = a.k_lo;  // no tiles (the loops below do nothing): the wave joins the epilogue
+
+  if (!FULL && start_not_a_node(file, flen)) {
+    // the optimistic pass needs a recorded node at file_len - 20; without
+    // one it cannot prove anything (a torn tail, b"CORRUPT" appended): the
+    // waves skip their tiles, record nothing (zero span counts) and the
+    // glue reports ST_NOSTART, so the full pass starts ~0.9 ms earlier
+    const uint64_t sa = k0 / SPAN_TILES, sb = (k1 + SPAN_TILES - 1) / SPAN_TILES;
+    for (uint64_t sp = sa + lane; sp < sb; sp += 64) {
+      a.span_count[sp] = 0;
+      a.span_first[sp] = 0;
+    }
+    k0 = k1 = a.k_lo;
   }
-  // the optimistic pass needs a recorded node at file_len - 20; without one
-  // it cannot prove anything (a torn tail, b"CORRUPT" appended): the waves
-  // skip their tiles, record nothing (zero span counts) and the glue reports
-  // ST_NOSTART, so the full pass starts ~0.9 ms earlier
-  const bool nostart = !FULL && start_not_a_node(file, flen);
 
   uint32_t count = 0;
   uint64_t wtotal = 0;  // wave-uniform: records of the wave's spans
@@ -538,8 +506,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // tile's SX partial of line 63 (= its true SX_63).
   const uint32_t hb = a.filt_hb;
   uint64_t rootmax = 0;
-  auto seed_window = [&]() {
-    // the line just before the range's first tile: its tail bytes and its raw
+  {
+    // the line just before this wave's first tile: its tail bytes and its raw
     // CRC (= SX_63 of tile k0-1) seed the window; all lanes load it
     uint32_t pl[16];
     const bool has_prev = k0 > a.k_lo;  // the line before the resident range reads as zeros
@@ -555,7 +523,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       for (int j = 0; j < 4; j++) win[j] = has_prev ? pl[12 + j] : 0u;
       win[22] = has_prev ? cp : 0u;
     }
-  };
+  }
 
   // first 8 bytes of tile k+1 (line 63's window) by a SCALAR load: the slow
   // loop must not touch a register of the vector prefetch ring, or the
@@ -735,7 +703,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const int lm = rs >> 6;
           const uint32_t hm = lm < 0 ? __builtin_amdgcn_readfirstlane(hxp) : __builtin_amdgcn_readlane(hx, lm & 63);
           const uint64_t r = wtotal + count;  // the record's index in the wave's region
-          if (r < rcap) {
+          if (r < a.wcap) {
             const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
             const uint32_t fl = REC_KIND | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
                                 (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
@@ -755,7 +723,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
               rq[9] = writelane_u32(s4, li, rq[9]);
               rvalid |= 1ull << (r - flushed);
             } else if (lane == 0) {
-              const uint64_t gi = rbase + r;
+              const uint64_t gi = w * a.wcap + r;
               a.c_m[gi] = m;
               a.c_rec[2 * gi] = u32x4{s2, s3, s0, s1};
               a.c_rec[2 * gi + 1] = u32x4{s4, hm, hs, fl};
@@ -788,11 +756,11 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const int lm = r >> 6;                             // m's line (-1: previous tile's line 63)
       const uint32_t hm0 = __shfl(hx, lm & 63);
       const uint32_t hm = lm < 0 ? hxp : hm0;
-      if (FULL ? count + __popcll(cm) > a.cap : wtotal + count + __popcll(cm) > rcap) ovf = true;
+      if (FULL ? count + __popcll(cm) > a.cap : wtotal + count + __popcll(cm) > a.wcap) ovf = true;
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
-        if (FULL ? idx < a.cap : wtotal + idx < rcap) {
-          const uint64_t gi = FULL ? span * a.cap + idx : rbase + wtotal + idx;
+        if (FULL ? idx < a.cap : wtotal + idx < a.wcap) {
+          const uint64_t gi = FULL ? span * a.cap + idx : w * a.wcap + wtotal + idx;
           const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
           const uint32_t fl = (tomb ? F_TOMB : 0u) | ((r & 63) == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT) |
                               (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) | ((js & 63) < 32 ? F_SUF_LO : 0u);
@@ -819,8 +787,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint64_t pend = wtotal + count - flushed;  // records pending (lanes [0, min(pend, 64)))
       const bool fl = span_end && (pend >= FLUSH_AT || k + 1 == k1);  // uniform
       const bool wr = fl && ((rvalid >> lane) & 1);
-      const uint64_t rb = rbase + flushed;  // lane 0's record
-      const uint32_t rn = (uint32_t)min<uint64_t>(rcap - min(flushed, rcap), 64);  // slots left (OOB past)
+      const uint64_t rb = w * a.wcap + flushed;  // lane 0's record
+      const uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + rb, rn * 8),
                                             wr ? 8u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
@@ -853,6 +821,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // Loads are clamped, never skipped (tiles up to n_tiles+1 are readable).
   // kt = the first tail tile (flen - kt*TILE < TILE + 64)
   const uint64_t kt = flen >= (uint64_t)TILE + 64 ? (flen - TILE - 64) / TILE + 1 : 0;
+  const uint64_t km = min(k1, max(k0, kt));  // ring part: [k0, km)
+  const uint32_t nk = (uint32_t)(km - k0);
   const std::false_type body{};
   uint32_t A[16], Bv[16], Cv[16];
   // vmcnt counts loads and stores in issue order, and the compiler's wait
@@ -869,113 +839,48 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     for (uint32_t i = 0; i < NST; i++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, out_rsrc(a.tile, 256), OOB_OFF - 64u * (NST * g + i), 0, 0);
   };
-  for (;;) {
-    if (nostart) {
-      const uint64_t sa = k0 / SPAN_TILES, sb = (k1 + SPAN_TILES - 1) / SPAN_TILES;
-      for (uint64_t sp = sa + lane; sp < sb; sp += 64) {
-        a.span_count[sp] = 0;
-        a.span_first[sp] = 0;
-      }
-      k0 = k1 = a.k_lo;
-    }
-    count = 0;
-    wtotal = 0;
-    ovf = false;
-    flushed = 0;
-    rvalid = 0;
-    rootmax = 0;
-    seed_window();
-    const uint64_t km = min(k1, max(k0, kt));  // ring part: [k0, km)
-    const uint32_t nk = (uint32_t)(km - k0);
-    // Whole rounds of 3 tiles only: a break between the tiles of a round
-    // reaches the loop latch, and that (never taken) latch -> header path
-    // would shorten the compiler's wait counts as well.  The <= 2 remaining
-    // ring tiles run in the unpipelined loop below with the file's tail tiles.
-    const uint32_t nfull = nk / 3;
-    load_tile(k0, A);
-    pad_stores(0);
-    load_tile(k0 + 1, Bv);
-    pad_stores(1);
-    for (uint32_t i = 0; i < nfull; i++) {
-      const uint32_t j = 3 * i;
-      // priority from the tile's prefetch loads through its CRC (process()
-      // drops it after the lookups): -1.6 % same-box A/B over priority on the
-      // CRC alone
-      __builtin_amdgcn_s_setprio(3);
-      load_tile(k0 + min(j + 2, nk), Cv);
-      process(k0 + j, A, body);
-      __builtin_amdgcn_s_setprio(3);
-      load_tile(k0 + min(j + 3, nk), A);
-      process(k0 + j + 1, Bv, body);
-      __builtin_amdgcn_s_setprio(3);
-      load_tile(k0 + min(j + 4, nk), Bv);
-      process(k0 + j + 2, Cv, body);
-    }
-    const uint64_t kr = k0 + 3ull * nfull;
-    // the ring's remainder and the file's last <= 2 tiles (masked: a tail
-    // tile's bytes past file_len read as 0; a no-op on the others)
-    for (uint64_t k = kr; k < k1; k++) {
-      load_tile(k, A);
-      process(k, A, std::true_type{});
-    }
-
-    // the range's results (the last block to finish reduces them)
-    if (lane == 0) {
-      a.wave_total[rgn] = wtotal | (ovf ? (1ull << 63) : 0ull);
-      a.wave_root[rgn] = rootmax;  // wave-uniform already
-    }
-#ifdef SRD_WAVE_STAMPS
-    const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
-    const uint64_t dbg_w = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
-    if (lane == 0 && dbg_w < 4096) {
-      if (rgn < (uint64_t)gridDim.x * SCAN_WAVES_V2) { g_wave_dbg[4 * dbg_w] = dbg_t0; g_wave_dbg[4 * dbg_w + 1] = 0; g_wave_dbg[4 * dbg_w + 2] = 0; }
-      else g_wave_dbg[4 * dbg_w + 1] += 1;
-    }
-#endif
-    // the next chunk: this XCD's pool first (blocks go to the 8 XCDs
-    // round-robin; placement only affects speed), then a pool with chunks
-    // left -- all pool counts in one load round (lanes 0-7; a stale count
-    // only costs balance, never a chunk: claims are atomic)
-    uint32_t c = ~0u;
-    if (a.part.n_dyn) {
-      const uint32_t own = blockIdx.x % SCAN_DYN_POOLS;
-      uint32_t pool = own;
-      for (int attempt = 0; attempt < 4; attempt++) {
-        uint32_t j = 0;
-        if (lane == 0) j = atomicAdd(&a.dyn_next[pool * SCAN_DYN_STRIDE], 1u);
-        j = __builtin_amdgcn_readfirstlane(j);
-        const uint64_t cc = (uint64_t)j * SCAN_DYN_POOLS + pool;  // pool p holds chunks p, p + 8, ...
-        if (cc < a.part.n_dyn) { c = (uint32_t)cc; break; }
-        const uint32_t cnt = lane < (int)SCAN_DYN_POOLS
-                                 ? __hip_atomic_load(&a.dyn_next[lane * SCAN_DYN_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : 0u;
-        const uint64_t m = __ballot(lane < (int)SCAN_DYN_POOLS && (uint64_t)cnt * SCAN_DYN_POOLS + lane < a.part.n_dyn);
-        if (!m) break;
-        const uint32_t rot = (uint32_t)(((m >> own) | (m << (SCAN_DYN_POOLS - own))) & 0xffu);
-        pool = (own + (uint32_t)__builtin_ctz(rot)) % SCAN_DYN_POOLS;
-      }
-    }
-#ifdef SRD_WAVE_STAMPS
-    if (lane == 0 && dbg_w < 4096) g_wave_dbg[4 * dbg_w + 2] += __builtin_amdgcn_s_memrealtime() - dbg_t0;
-#endif
-    if (c == ~0u) break;
-    rgn = (uint64_t)gridDim.x * SCAN_WAVES_V2 + c;
-    rbase = part_region_base(a.part, rgn);
-    rcap = part_region_cap(a.part, rgn);
-    uint64_t r0, r1;
-    part_chunk_range(a.part, c, &r0, &r1);
-    set_range(r0, r1);
+  // Whole rounds of 3 tiles only: a break between the tiles of a round
+  // reaches the loop latch, and that (never taken) latch -> header path
+  // would shorten the compiler's wait counts as well.  The <= 2 remaining
+  // ring tiles run in the unpipelined loop below with the file's tail tiles.
+  const uint32_t nfull = nk / 3;
+  load_tile(k0, A);
+  pad_stores(0);
+  load_tile(k0 + 1, Bv);
+  pad_stores(1);
+  for (uint32_t i = 0; i < nfull; i++) {
+    const uint32_t j = 3 * i;
+    // priority from the tile's prefetch loads through its CRC (process()
+    // drops it after the lookups): -1.6 % same-box A/B over priority on the
+    // CRC alone
+    __builtin_amdgcn_s_setprio(3);
+    load_tile(k0 + min(j + 2, nk), Cv);
+    process(k0 + j, A, body);
+    __builtin_amdgcn_s_setprio(3);
+    load_tile(k0 + min(j + 3, nk), A);
+    process(k0 + j + 1, Bv, body);
+    __builtin_amdgcn_s_setprio(3);
+    load_tile(k0 + min(j + 4, nk), Bv);
+    process(k0 + j + 2, Cv, body);
   }
-#ifdef SRD_WAVE_STAMPS  // timing-only build (tools/wave_stamps.py): each wave's end, 100 MHz clock
-  {
-    const uint64_t w = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
-    if (lane == 0 && w < 8192) g_wave_stamp[w] = __builtin_amdgcn_s_memrealtime();
+  const uint64_t kr = k0 + 3ull * nfull;
+  // the ring's remainder and the file's last <= 2 tiles (masked: a tail
+  // tile's bytes past file_len read as 0; a no-op on the others)
+  for (uint64_t k = kr; k < k1; k++) {
+    load_tile(k, A);
+    process(k, A, std::true_type{});
   }
-#endif
 
-  // ---- epilogue: the last block to finish reduces the region results
+  // ---- epilogue: per-wave results; the last block to finish reduces them
   // (cdna guide: plain stores, vmcnt(0), barrier, lane-0 agent release, add;
   // the last block acquires before reading) ----
+  if (lane == 0) {
+    a.wave_total[w] = wtotal | (ovf ? (1ull << 63) : 0ull);
+    a.wave_root[w] = rootmax;  // wave-uniform already
+#ifdef SRD_WAVE_STAMPS  // timing-only build (tools/wave_stamps.py): each wave's end, 100 MHz clock
+    if (w < 8192) g_wave_stamp[w] = __builtin_amdgcn_s_memrealtime();
+#endif
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint32_t& s_last = lds.s_last;
   __syncthreads();
@@ -989,37 +894,36 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // exclusive prefix of the region counts: thread t owns regions
-  // [t*q, (t+1)*q).  q <= QR (the host keeps part_regions() <= 16 Ki): the
-  // thread's regions are loaded together into registers (one round trip
-  // instead of 2q dependent ones: the last block's epilogue is on the
-  // critical path of every call)
-  constexpr int QR = 16;
+  // exclusive prefix of the wave counts: thread t owns waves [t*q, (t+1)*q).
+  // q <= 4 (up to 256 blocks): the thread's waves are loaded together into
+  // registers (one round trip instead of 2q dependent ones: the last block's
+  // epilogue is on the critical path of every call)
+  constexpr int QR = 4;
   uint64_t* s_wsum = (uint64_t*)lds.tab;  // the CRC tables are dead now
   uint64_t* s_root = lds.s_root;
   uint64_t* s_ovf = lds.s_ovf;
   const uint32_t T = blockDim.x, t = threadIdx.x;
-  const uint64_t q = (total_regions + T - 1) / T;
+  const uint64_t q = (total_waves + T - 1) / T;
   uint64_t sum = 0, rmax = 0, o = 0;
   uint64_t vt[QR];
   if (q <= QR) {
     uint64_t vr[QR];
 #pragma unroll
     for (int j = 0; j < QR; j++) {
-      const uint64_t i = min(t * q + j, total_regions - 1);
+      const uint64_t i = min(t * q + j, total_waves - 1);
       vt[j] = a.wave_total[i];
       vr[j] = a.wave_root[i];
     }
 #pragma unroll
     for (int j = 0; j < QR; j++) {
-      const bool in = (uint64_t)j < q && t * q + j < total_regions;
+      const bool in = (uint64_t)j < q && t * q + j < total_waves;
       vt[j] = in ? vt[j] : 0ull;
       sum += vt[j] & ~(1ull << 63);
       o |= vt[j] >> 63;
       rmax = max(rmax, in ? vr[j] : 0ull);
     }
   } else {
-    for (uint64_t i = t * q; i < min((t + 1) * q, total_regions); i++) {
+    for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
       const uint64_t v = a.wave_total[i];
       sum += v & ~(1ull << 63);
       o |= v >> 63;
@@ -1043,13 +947,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   if (q <= QR) {
 #pragma unroll
     for (int j = 0; j < QR; j++) {
-      if ((uint64_t)j < q && t * q + j < total_regions) {
+      if ((uint64_t)j < q && t * q + j < total_waves) {
         a.wave_base[t * q + j] = run;
         run += vt[j] & ~(1ull << 63);
       }
     }
   } else {
-    for (uint64_t i = t * q; i < min((t + 1) * q, total_regions); i++) {
+    for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
       a.wave_base[i] = run;
       run += a.wave_total[i] & ~(1ull << 63);
     }
@@ -1062,7 +966,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     a.counters[1] = 0;
     a.counters[2] = oo;
     *a.done = 0;  // for the next launch on this context
-    for (uint32_t i = 0; i < SCAN_DYN_POOLS; i++) a.dyn_next[i * SCAN_DYN_STRIDE] = 0;
 #ifdef SRD_WAVE_STAMPS
     g_wave_stamp[8192 + 1023] = __builtin_amdgcn_s_memrealtime();
 #endif
