@@ -12,8 +12,14 @@ timeout -k 10 200 python tools/wave_stamps.py > gpurun_out/stamps_ab.json 2>&1 |
 tail -2 gpurun_out/stamps_ab.json
 fi
 for rep in 1 2 3; do
-for V in new prev; do
-  if [ $V = new ]; then unset SRD_LIB_PATH; else export SRD_LIB_PATH=$PWD/rust-simd-r-drive_amd/build/var/lib_prev.so; fi
+for V in ${VARIANTS:-new prev}; do
+  unset SRD_LIB_PATH SRD_SCAN_DYN
+  case $V in
+    prev) export SRD_LIB_PATH=$PWD/rust-simd-r-drive_amd/build/var/lib_prev.so ;;
+    nodyn) export SRD_SCAN_DYN=0 ;;
+    dyn5) export SRD_SCAN_DYN=5 ;;
+    dyn20) export SRD_SCAN_DYN=20 ;;
+  esac
   timeout -k 10 200 python bench.py --no-cpu ${BENCH_ARGS} > gpurun_out/bench_ab_$V.json 2> gpurun_out/bench_ab.err || { echo BENCH_FAIL; tail -30 gpurun_out/bench_ab.err; exit 1; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/bench_ab_$V.json').read().strip().splitlines()[-1])

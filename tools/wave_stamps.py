@@ -35,7 +35,16 @@ for rep in range(5):
     ld = (st[8192 + 256:8192 + 512].astype(np.int64) - t0) / 100.0
     bend_all = we.reshape(256, 16).max(1)
     epi = (int(st[8192 + 1023]) - t0) / 100.0
-    out.append({"block_start_us_max": round(float(bs.max()), 2),
+    dbg = None
+    if hasattr(L, "srd_debug_wave_dbg"):
+        dd = np.zeros(4096 * 4, np.uint64)
+        assert L.srd_debug_wave_dbg(C.c_void_p(dd.ctypes.data)) == 0
+        dd = dd.reshape(4096, 4).astype(np.int64)
+        send = (dd[:, 0] - t0) / 100.0
+        dbg = {"static_end_us_pct_0_50_100": [round(float(x), 1) for x in np.percentile(send, [0, 50, 100])],
+               "chunks_per_wave_mean_max": [round(float(dd[:, 1].mean()), 2), int(dd[:, 1].max())],
+               "claim_us_per_wave_mean_max": [round(float(dd[:, 2].mean() / 100.0), 2), round(float(dd[:, 2].max() / 100.0), 2)]}
+    out.append({"dbg": dbg, "block_start_us_max": round(float(bs.max()), 2),
                 "tables_loaded_us_pct_50_100": [round(float(np.percentile(ld, 50)), 2), round(float(ld.max()), 2)],
                 "block_end_us_pct_0_10_50_90_100": [round(float(x), 1) for x in np.percentile(bend_all, [0, 10, 50, 90, 100])],
                 "block_end_mean": round(float(bend_all.mean()), 1),
