@@ -387,9 +387,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)  # ~55 ms timed: host-side jitter of single calls averages out
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", choices=["c2", "c2torn", "c3", "c5", "ops"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c2torn", "c2full", "c3", "c5", "ops"], default="c2",
                     help="c2: 4 KiB entries (headline); c2torn: the C2 store + b'CORRUPT' (persistence_tests.rs:"
-                         "126-173: the torn-tail open, decided by the full pass); c3: Zipf-sized entries 64 B..1 MiB "
+                         "126-173: the torn-tail open; its start tail lies 7 bytes below file_len); c2full: the C2 "
+                         "store through the full pass (SRD_FLAG_FORCE_FULL: what a store the optimistic pass cannot "
+                         "prove costs); c3: Zipf-sized entries 64 B..1 MiB "
                          "(variable length); c5: checksum-on-append batch write of 1M x 4 KiB from pinned host memory")
     ap.add_argument("--entries-per-gpu", type=int, default=None)
     ap.add_argument("--payload", type=int, default=4096)
@@ -429,10 +431,11 @@ def main():
         return bench_ops(args, ctx, local)
     n, L = args.entries_per_gpu, args.payload
     torn = args.config == "c2torn"
-    if torn and world != 1:
-        sys.exit("bench.py: --config c2torn runs on one GPU")
+    full = args.config == "c2full"
+    if (torn or full) and world != 1:
+        sys.exit(f"bench.py: --config {args.config} runs on one GPU")
     if n is None:  # N=1: C2 (1M x 4 KiB); N>1: the C4 partition (2^21 per GPU; N=8 is C4)
-        n = (1 << 20 if world == 1 else 1 << 21) if args.config in ("c2", "c2torn") else 10_000_000
+        n = (1 << 20 if world == 1 else 1 << 21) if args.config in ("c2", "c2torn", "c2full") else 10_000_000
     lens, seed = None, 0x5EED0001
     if args.config == "c3":
         lens, seed = S.zipf_lens(n * world), 0x5EED0004
@@ -446,10 +449,12 @@ def main():
             store[size:flen].copy_(torch.frombuffer(bytearray(b"CORRUPT"), dtype=torch.uint8))
         span = (0, 0, size)
 
+        vflags = S.SRD_FLAG_FORCE_FULL if full else 0
+
         def step():
-            r = S.validate_index_device(store.data_ptr(), flen, 0, ctx)
+            r = S.validate_index_device(store.data_ptr(), flen, vflags, ctx)
             return r.final_len, r.n_chain, r.n_crc_bad, r.n_index, r.mode
-        expect = (size, n, 0, n, S.SRD_MODE_FULL if torn else S.SRD_MODE_OPTIMISTIC)
+        expect = (size, n, 0, n, S.SRD_MODE_FULL if full else S.SRD_MODE_OPTIMISTIC)
     else:
         import ctypes as C
         import srd_shard as SH
@@ -520,7 +525,7 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = bytes_total / dt * args.steps / 2**30
     scan_ms = scan_ms_sum / max(scan_n, 1)
-    if torn:  # both passes' scans per step (the optimistic pass fails, the full pass decides)
+    if full:  # the full pass's scan (one per step)
         scan_ms = scan_ms_sum / args.steps
     if multi is not None:  # the slowest shard's scan bounds the step
         shard_scan = [x / max(multi["n"], 1) for x in multi["scan_ms"]]
@@ -555,7 +560,9 @@ def main():
         "config": {
             "workload": (f"{args.config.upper()}: {n} x " + (f"{L} B" if lens is None else "Zipf 64 B..1 MiB") +
                          f" entries, {size} B store" + (" + the 7-byte torn tail b'CORRUPT' (recovered: final_len = "
-                                                        f"{size}, the full pass)" if torn else "") +
+                                                        f"{size}, the optimistic pass from the start tail 7 bytes "
+                                                        "below file_len)" if torn else "") +
+                         (" through the full pass (SRD_FLAG_FORCE_FULL)" if full else "") +
                          ", validate+index (recover_valid_chain + CRC-32 every payload + "
                          f"KeyIndexer::build)") if world == 1 else
                         ((f"C4 partition ({'= C4' if world == 8 else f'prefix of C4, {world} of its 8 shards'})"
@@ -573,7 +580,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "scan_kernel<false> + scan_kernel<true> (both passes)" if torn else "scan_kernel<false>",
+            "kernel": "scan_kernel<true> (the full pass)" if full else "scan_kernel<false>",
             "kernel_ms": round(scan_ms, 4),
             "kernel_timing": "HIP events stamped with the scan dispatch's own start / stop (hipExtLaunchKernel) "
                              "on the library stream, every timed step",

@@ -116,7 +116,7 @@ struct Ctx {
 enum BufId {
   B_TILE, B_SPAN_COUNT, B_SPAN_BASE,
   B_CM, B_CREC,
-  B_COUNTERS,  // [0]=max_root [1]=n_weak [2]=overflow [3]=best_g1 [4]=changed [5]=n_slow [6]=n_bad [7]=special
+  B_COUNTERS,  // [0]=max_root [1]=start tail (find_top) [2]=overflow [3]=best_g1 [4]=changed [5]=n_slow [6]=n_bad [7]=special
   B_DM, B_DPAR, B_DSLOT, B_DHEAD, B_RUNHEAD, B_INTS, B_WALK,
   B_ST, B_JMP, B_VFLAG, B_VLIST, B_NV, B_VPOS, B_VPAR, B_VHEAD, B_VSLOT,
   B_ONPATH, B_CPOS, B_CHAIN_G, B_CORE,
@@ -1065,6 +1065,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
           hp.n_index = (uint32_t)w[2];
           hp.n_bad = (uint32_t)w[3];
           hp.K = (uint32_t)w[4];
+          hp.top_gap = (uint32_t)w[5];
           hp.idx_alias = 1;
         }
       }
@@ -1091,7 +1092,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       if (!(hp.status & retry_bits) || (hp.status & ~retry_bits) || rounds >= 6) break;
     }
     out->n_candidates = hp.K;
-    out->n_weak = hp.n_weak;
+    out->n_weak = 0;
     if (hp.status & ST_OVERFLOW) {
       if (c->cap >= SPAN_BYTES) return 0;  // cannot happen (<= one candidate per byte); not provable here
       grow_cap(c, flen - span_off);
@@ -1102,7 +1103,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       continue;
     }
     if (hp.status) return 0;  // not provable here -> full pass (whole file) / unproven (span)
-    out->final_len = flen;
+    out->final_len = flen - hp.top_gap;  // find_top's start tail (a torn tail within TOP_WINDOW bytes: below flen)
     out->n_chain = hp.n_chain;
     out->n_crc_bad = hp.n_bad;
     out->n_index = hp.n_index;

@@ -50,7 +50,7 @@ struct Plan {
   uint64_t n_bad;      // chain entries whose CRC mismatches
   uint64_t n_slow;     // finalize entries handed to slow_kernel
   uint64_t chain_core; // core nodes (n_chain - 1 on success)
-  uint64_t max_root, n_weak, overflow;  // copies of the scan counters
+  uint64_t max_root, top_gap, overflow;  // the scan counters; top_gap = file_len - the start tail (find_top)
   uint64_t cap_need;   // K when it exceeds the dense capacity
   uint32_t status;     // ST_* bits; 0 = the optimistic result is final
   uint32_t nroot;      // core nodes linking to a root
@@ -296,8 +296,11 @@ struct ShapeArgs {
   uint32_t n_zero;
 };
 
+// the dense index of the node at the start tail find_top chose (the scan's
+// counters[1]; no candidate lies above it)
 __device__ __forceinline__ uint64_t start_node(const ShapeArgs& a, uint64_t K) {
-  return (K && a.c_m[a.d_slot[K - 1]] == a.flen - 20) ? K - 1 : NO_NODE;
+  const uint64_t t = a.counters[1];
+  return (K && t >= 21 && a.c_m[a.d_slot[K - 1]] == t - 20) ? K - 1 : NO_NODE;
 }
 
 // Core nodes of the current round: the start node, or a node some node of
@@ -442,7 +445,7 @@ constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
 // below IDX_TCAP, and an overflowing one sends the build to the global table)
 constexpr int IDX_BUCKET_AVG = 1280;
 constexpr uint64_t IDX_EMPTY = ~0ull;
-constexpr int PUB_WORDS = 5;  // flags, n_chain, n_index, n_bad, K
+constexpr int PUB_WORDS = 6;  // flags, n_chain, n_index, n_bad, K, top_gap
 
 struct IdxArgs {
   const uint64_t* kh;    // chain key hashes (o_kh)
@@ -661,9 +664,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   block_prefix_n<CHAIN_WAVES>(a.part, capk ? 0u : (uint32_t)CHAIN_BLOCKS, wsum, &before, &total);
   Plan* pl = a.plan;
   uint32_t st = pl->status;  // check_kernel's shape bits
-  // whole file only: file_len is itself a root tail (prev 0); flen >= 21 here
-  const bool troot = a.coff && ld_u64_unaligned(a.file, a.flen - 12) == 0;
-  const uint64_t root_t = troot ? a.flen : pl->root_t;
+  // whole file only: the start tail is itself a root tail (prev 0): one
+  // entry spans [0, t) (recover_valid_chain's walk ends at once)
+  const uint64_t top = a.counters[1];
+  const bool troot = a.coff && top >= 21 && ld_u64_unaligned(a.file, top - 12) == 0;
+  const uint64_t root_t = troot ? top : pl->root_t;
   if (capk) st |= ST_CAPK;
   if (a.counters[2]) st |= ST_OVERFLOW;
   const uint64_t start = capk ? NO_NODE : start_node(a, K);
@@ -674,13 +679,13 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     pl->K = K;
     pl->max_root = a.counters[0];
-    pl->n_weak = a.counters[1];
+    pl->top_gap = top ? a.flen - top : 0;
     pl->overflow = a.counters[2];
     pl->troot = troot;
-    if (troot) {  // file_len is itself a root tail: chain = that one entry
+    if (troot) {  // the start tail is itself a root tail: chain = that one entry
       pl->status = 0;
       pl->n_chain = 1;
-      pl->root_t = a.flen;
+      pl->root_t = top;
       pl->chain_core = 0;
     } else {
       if (capk) pl->cap_need = K;
@@ -941,7 +946,7 @@ __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
       const uint32_t fl = (pl->status & 0xffu) | (a.alias && nl_total == 0 ? 0x100u : 0u) |
                           (pl->idx_overflow ? 0x200u : 0u);
       const uint64_t w[PUB_WORDS] = {tag | fl, tag | (uint32_t)pl->n_chain, tag | (uint32_t)(n - nl_total),
-                                     tag | (uint32_t)pl->n_bad, tag | (uint32_t)pl->K};
+                                     tag | (uint32_t)pl->n_bad, tag | (uint32_t)pl->K, tag | (uint32_t)pl->top_gap};
 #pragma unroll
       for (int i = 0; i < PUB_WORDS; i++)
         __hip_atomic_store(a.pub + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

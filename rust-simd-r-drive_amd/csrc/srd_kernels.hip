@@ -128,7 +128,7 @@ struct ScanArgs {
   uint32_t* span_count;
   uint64_t* c_m;                   // [n_spans*cap] candidate metadata offsets
   u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
-  unsigned long long* counters;    // [0] max root tail, [1] unused, [2] overflow
+  unsigned long long* counters;    // [0] max root tail, [1] find_top's tail (optimistic pass), [2] overflow
   uint32_t filt_hb;               // (file_len-1) >> 32: bound of a node's p-byte 4 (p < file_len < 2^40)
   // span mode (entry-range shard): tiles [k_lo, n_tiles) are resident, k_lo a
   // multiple of SPAN_TILES; only nodes with m > m_lo are recorded (m_lo = the
@@ -394,23 +394,46 @@ __device__ __forceinline__ void crc_lane_bases(uint32_t (&R)[4], int lane) {
   for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
 }
 
-// The optimistic pass starts at the node whose metadata ends at file_len
-// (data_store.rs:388-479's first tail t = file_len): true when the 20 bytes
-// there fail recover_valid_chain's node test (:404-470) for a strong node
-// (p >= 20, p < m, a nonzero checksum field, the prepad / tombstone rule)
-// and are no root (p == 0: the whole file is one entry).  Every lane reads
-// the same words (one request per wave).
-__device__ __forceinline__ bool start_not_a_node(const uint8_t* file, uint64_t flen) {
-  const uint64_t m = flen - 20;
-  uint64_t kh, p;
-  uint32_t crc;
-  ld_meta(file, m, &kh, &p, &crc);
-  if (p == 0) return false;
-  const uint32_t bw = *(const uint32_t*)(file + ((m - 1) & ~3ull));
-  const bool zb = ((bw >> (8 * ((m - 1) & 3))) & 0xffu) == 0;
-  const uint64_t dp = m - p;
-  const bool node = p >= 20 && p < m && crc != 0 && (dp > prepad64(p) || (dp == 1 && zb));
-  return !node;
+// recover_valid_chain's outer loop (data_store.rs:388-479) walks the cursor t
+// down from file_len and skips every t whose metadata fails its first test,
+// entry_start < metadata_offset (:390-420; entry_start = prev + prepad(prev),
+// or prev for a tombstone, u64 wrapping).  The optimistic pass starts at the
+// largest t that passes it -- file_len itself for an intact store, file_len -
+// 7 after b"CORRUPT" was appended (persistence_tests.rs:126-173) -- searched
+// within TOP_WINDOW bytes below file_len (whole file; a shard's tail is
+// given: only t = file_len).  Returns t when its entry is a strong node (p >=
+// 20, p < m, a nonzero checksum field, the prepad / tombstone rule) or a root
+// (p == 0: one entry spans [0, t)); 0 otherwise, and the full pass decides.
+// Every candidate the scan records lies at or below t - 20: a strong node
+// above it would pass the same test.
+constexpr uint32_t TOP_WINDOW = 256;
+__device__ __forceinline__ uint64_t find_top(const uint8_t* file, uint64_t flen, bool search) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t steps = search ? TOP_WINDOW / 64 : 1;
+  for (uint32_t s = 0; s < steps; s++) {
+    const uint64_t d = (uint64_t)s * 64 + (uint64_t)lane;  // t = flen - d
+    const bool has = (search || lane == 0) && flen >= 21 + d;
+    const uint64_t m = (has ? flen - d : flen) - 20;      // flen >= 21 (the caller's guard)
+    uint64_t kh, p;
+    uint32_t crc;
+    ld_meta(file, m, &kh, &p, &crc);
+    const uint32_t bw = *(const uint32_t*)(file + ((m - 1) & ~3ull));
+    const bool zb = ((bw >> (8 * ((m - 1) & 3))) & 0xffu) == 0;  // byte m - 1: the tombstone byte when p == m - 1
+    const bool tomb = m > p && m - p == 1 && zb;
+    const uint64_t es = tomb ? p : p + prepad64(p);
+    const uint64_t pass = __ballot(has && es < m);
+    if (!pass) continue;
+    const int l = __builtin_ctzll(pass);  // the largest passing t of the step
+    // (readlane returns int: widen through uint32_t, or bit 31 sign-extends)
+    const uint64_t pl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(p >> 32), l) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)p, l);
+    const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane(crc, l);
+    const bool zl = __builtin_amdgcn_readlane((uint32_t)zb, l) != 0;
+    const uint64_t t = flen - ((uint64_t)s * 64 + (uint64_t)l), ml = t - 20, dp = ml - pl;
+    const bool strong = pl >= 20 && pl < ml && cl != 0 && (dp > prepad64(pl) || (dp == 1 && zl));
+    return (pl == 0 || strong) ? t : 0;
+  }
+  return 0;
 }
 
 // WIDE: stores above 2^40 bytes (prev offsets up to 48 bits, key_indexer.rs:12-15):
@@ -451,11 +474,11 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   uint64_t k1 = min((a.part.s_lo + r1) * SPAN_TILES, a.n_tiles);
   if (k0 >= k1) k0 = k1 = a.k_lo;  // no tiles (the loops below do nothing): the wave joins the epilogue
 
-  if (!FULL && start_not_a_node(file, flen)) {
-    // the optimistic pass needs a recorded node at file_len - 20; without
-    // one it cannot prove anything (a torn tail, b"CORRUPT" appended): the
-    // waves skip their tiles, record nothing (zero span counts) and the
-    // glue reports ST_NOSTART, so the full pass starts ~0.9 ms earlier
+  // the optimistic pass's start (find_top); none: the waves skip their tiles,
+  // record nothing (zero span counts) and the glue reports ST_NOSTART, so the
+  // full pass starts ~0.9 ms earlier
+  const uint64_t top = FULL ? 0 : find_top(file, flen, a.m_lo == 0);
+  if (!FULL && top == 0) {
     const uint64_t sa = k0 / SPAN_TILES, sb = (k1 + SPAN_TILES - 1) / SPAN_TILES;
     for (uint64_t sp = sa + lane; sp < sb; sp += 64) {
       a.span_count[sp] = 0;
@@ -963,7 +986,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     for (int i = 0; i < SCAN_WAVES_V2; i++) { mr = max(mr, s_root[i]); oo |= s_ovf[i]; tot += s_wsum[i]; }
     *a.k_total = tot;
     a.counters[0] = mr;
-    a.counters[1] = 0;
+    a.counters[1] = top;  // the optimistic pass's start tail (find_top; 0: none)
     a.counters[2] = oo;
     *a.done = 0;  // for the next launch on this context
 #ifdef SRD_WAVE_STAMPS

@@ -91,7 +91,9 @@ class HipBackend:
     def validate_span(self, buf: torch.Tensor, span_off: int, lo: int, hi: int, flags: int = 0):
         self._after_torch(buf)
         r = S.validate_span_device(buf.data_ptr(), span_off, lo, hi, flags, self.ctx)
-        proven = r.mode == S.SRD_MODE_OPTIMISTIC or (lo == 0 and r.final_len == hi)
+        # the chain reaches this shard's tail (lo == 0 is the whole-file rule:
+        # a torn tail's chain may end below hi in either mode)
+        proven = r.mode != S.SRD_MODE_SPAN_UNPROVEN and r.final_len == hi
         st = ShardStatus(bool(proven), lo, hi, int(r.n_chain), int(r.n_crc_bad))
         keys = S.device_view(r.index_key_hash, r.n_index, np.uint64, self.device)
         packed = S.device_view(r.index_packed, r.n_index, np.uint64, self.device)

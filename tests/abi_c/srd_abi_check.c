@@ -95,9 +95,15 @@ int main(int argc, char **argv) {
     if (i && off <= (r.index_packed[i - 1] & ((1ull << 48) - 1))) bad |= 128;  /* chain order */
     if (off >= r.final_len) bad |= 256;
   }
+  /* the multi-GPU form: which path decided (composed shards / neighbour retry / whole file) */
+  int path = -1;
+  if (nctx > 1) {
+    srd_multi_summary sm;
+    if (srd_ctx_multi_summary(ctx[0], &sm) == SRD_OK) path = (int)sm.path;
+  }
   printf("{\"final_len\": %" PRIu64 ", \"n_chain\": %" PRIu64 ", \"n_index\": %" PRIu64 ", \"n_crc_bad\": %" PRIu64
-         ", \"mode\": %u, \"n_ctx\": %d, \"bad\": %d}\n",
-         r.final_len, r.n_chain, r.n_index, r.n_crc_bad, r.mode, nctx, bad);
+         ", \"mode\": %u, \"path\": %d, \"n_ctx\": %d, \"bad\": %d}\n",
+         r.final_len, r.n_chain, r.n_index, r.n_crc_bad, r.mode, path, nctx, bad);
   srd_result_free(&r);
   for (int i = 0; i < nctx; i++) srd_ctx_destroy(ctx[i]);
   free(buf);

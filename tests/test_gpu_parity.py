@@ -182,6 +182,35 @@ def test_torn_and_corrupted(ctx):
         check_against_oracle(np.concatenate([store, np.frombuffer(b"CORRUPT", np.uint8)]), ctx, 0, "corrupt")
 
 
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_torn_tail_start_search(ctx, flags):
+    """recover_valid_chain walks the cursor down from file_len and skips every
+    t whose metadata fails entry_start < metadata_offset (data_store.rs:388-420).
+    The optimistic pass starts at the largest such t within 256 bytes of
+    file_len (find_top): b"CORRUPT" (persistence_tests.rs:126-173) and short
+    junk stay in the optimistic mode; trailing zeros make the whole file one
+    root entry (prev 0); a cut deep in the last entry, or junk longer than the
+    window, goes to the full pass.  Every case against the oracle."""
+    rnd = random.Random(17)
+    base = O.synth_store(30, 100)
+    lens = _zipf_lens(40, seed=3)
+    mixed = O.synth_store(len(lens), lens=lens)
+    tails = [b"CORRUPT", b"\x00", b"\x01" * 19, b"\x00" * 20, b"\x00" * 64, bytes(rnd.randrange(1, 256) for _ in range(100)),
+             bytes(rnd.randrange(1, 256) for _ in range(255)), bytes(rnd.randrange(1, 256) for _ in range(300)),
+             rnd.randbytes(64) + b"\x00" * 40]
+    for store in (base, mixed):
+        for i, tail in enumerate(tails):
+            data = np.concatenate([store, np.frombuffer(tail, np.uint8)])
+            check_against_oracle(data, ctx, flags, "tail%d" % i)
+            r = S.validate_index(data, flags, ctx)
+            want = O.recover_valid_chain(data)
+            if flags == 0 and want == store.size and len(tail) <= 256:
+                assert r.mode == S.SRD_MODE_OPTIMISTIC, ("tail%d" % i, r.mode)
+        # cuts inside the last entry (its metadata or payload): junk below the window -> either mode, same answer
+        for cut in (store.size - 1, store.size - 19, store.size - 21, store.size - 60, store.size - 300):
+            check_against_oracle(store[:cut], ctx, flags, "cut%d" % cut)
+
+
 def test_datastore_open_truncates_torn_tail(tmp_path, ctx):
     # persistence_tests.rs:126-173
     p = tmp_path / "store.bin"

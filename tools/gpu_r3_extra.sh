@@ -1,4 +1,4 @@
-# Round 3: extra bench configs (torn-tail full pass, e2e, C3, C5) -- each with its own limit
+# Round 3: extra bench configs (torn tail, forced full pass, e2e, C3, C5) -- each with its own limit
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -8,6 +8,7 @@ for cfg in ${CONFIGS:-c2torn e2e}; do
   case $cfg in
     e2e) args="--e2e --no-cpu --steps 10" ;;
     c2torn) args="--config c2torn --no-cpu --steps 20 --warmup 3" ;;
+    c2full) args="--config c2full --no-cpu --steps 20 --warmup 3" ;;
     c3) args="--config c3 --no-cpu --steps 10 --warmup 2" ;;
     c5) args="--config c5 --steps 5 --warmup 2" ;;
     ops) args="--config ops" ;;
