@@ -54,7 +54,9 @@ extern "C" {
 #define SRD_ERR_INTERNAL (-4)
 
 /* srd_device_result.mode */
-#define SRD_MODE_OPTIMISTIC 0      /* the chain from file_len was proven through recorded nodes */
+#define SRD_MODE_OPTIMISTIC 0      /* the chain was proven through recorded nodes from the largest tail
+                                      within 256 B of file_len that passes recover_valid_chain's first
+                                      test (file_len for an intact store, below it for a short torn tail) */
 #define SRD_MODE_FULL 1            /* full pass (torn tail / corrupt store / unusual structure) */
 #define SRD_MODE_SPAN_UNPROVEN 3   /* span mode: the shard's chain was not proven; use the whole-file path */
 
@@ -140,7 +142,9 @@ int srd_validate_index_device(srd_ctx *ctx, const uint8_t *d_file,
  * recover_valid_chain's byte-wise outer loop is global).  The shards' chains
  * compose to the whole file's chain when shard 0 has lo = 0 (whole-file rule)
  * and each shard's lo equals the previous shard's hi.  lo == 0 with
- * span_off == 0 is exactly srd_validate_index_device. */
+ * span_off == 0 is exactly srd_validate_index_device (the whole-file rule:
+ * final_len may lie below hi in any mode); a shard is proven iff
+ * final_len == hi and mode != SRD_MODE_SPAN_UNPROVEN. */
 int srd_validate_span_device(srd_ctx *ctx, const uint8_t *d_span,
                              uint64_t span_off, uint64_t lo, uint64_t hi,
                              uint32_t flags, srd_device_result *out);
