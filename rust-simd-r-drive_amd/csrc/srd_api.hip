@@ -93,6 +93,7 @@ struct Ctx {
   uint64_t last_n = 0;  // chain length of the previous call (index bucket sizing)
   Plan* h_plan = nullptr;  // pinned host copy
   uint64_t* h_pub = nullptr;  // pinned: idx_emit's published outcome (IdxArgs::pub)
+  uint64_t* h_small = nullptr;  // pinned: small device reads (counters, K, ...): async copies, one wait
   uint32_t pub_seq = 0;
   // batch writer (srd_batch_write): side copy stream, double-buffer events,
   // pinned entry tables and pinned bounce buffers (non-contiguous inputs)
@@ -130,7 +131,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
-  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED,
+  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN,
   B_COUNT_
 };
 
@@ -221,7 +222,7 @@ int ensure_cub(Ctx* c, uint64_t n) {
   size_t t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
   int nn = (int)std::min<uint64_t>(n + 1, 0x7fffffff);
   hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (uint32_t*)nullptr, (uint64_t*)nullptr, nn);
-  hipcub::DeviceScan::InclusiveScan(nullptr, t2, (uint64_t*)nullptr, (uint64_t*)nullptr, hipcub::Max(), nn);
+  hipcub::DeviceScan::InclusiveScan(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, hipcub::Max(), nn);
   hipcub::DeviceScan::ExclusiveSum(nullptr, t3, (uint32_t*)nullptr, (uint32_t*)nullptr, nn);
   hipcub::DeviceSelect::Flagged(nullptr, t4, hipcub::CountingInputIterator<uint64_t>(0), (uint32_t*)nullptr,
                                 (uint64_t*)nullptr, (uint64_t*)nullptr, nn);
@@ -306,9 +307,22 @@ static int wait_publish(Ctx* c, uint64_t* w) {
   }
 }
 
+// the 8 counters into pinned h_small[0..8) (no wait) / with the wait: the
+// counters and, if extra != nullptr, the n_extra words enqueued into
+// h_small[8..) before (one host wait for all of them; a copy into pageable
+// memory would wait by itself)
+static int enqueue_counters(Ctx* c) {
+  HIPCHK(hipMemcpyAsync(c->h_small, P<uint64_t>(c, B_COUNTERS), 8 * 8, hipMemcpyDeviceToHost, c->stream));
+  return 0;
+}
+static int enqueue_small(Ctx* c, const void* src, uint32_t word) {  // one u64 into h_small[8 + word]
+  HIPCHK(hipMemcpyAsync(c->h_small + 8 + word, src, 8, hipMemcpyDeviceToHost, c->stream));
+  return 0;
+}
 int read_counters(Ctx* c, uint64_t* h) {
-  HIPCHK(hipMemcpyAsync(h, P<uint64_t>(c, B_COUNTERS), 8 * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  TRY(enqueue_counters(c));
+  HIPCHK(spin_sync(c->stream));
+  memcpy(h, c->h_small, 64);
   return 0;
 }
 
@@ -317,26 +331,30 @@ int walk_and_mark(Ctx* c, const int64_t* par, const uint64_t* slot, uint64_t n, 
                   WalkState* hws) {
   WalkState* ws = P<WalkState>(c, B_WALK);
   uint8_t* core = P<uint8_t>(c, B_CORE);
-  uint64_t* key = P<uint64_t>(c, B_DHEAD);
+  uint32_t* key = P<uint32_t>(c, B_DHEAD);
   HIPCHK(hipMemsetAsync(core, 0, n, c->stream));
   child_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(par, n, core);
   KCHK(c, "child_kernel");
   core_key_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(core, ws, n, key);
   KCHK(c, "core_key_kernel");
   size_t tb = c->bufs[B_CUB_TMP].n;
-  HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint64_t>(c, B_RUNHEAD),
+  HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint32_t>(c, B_RUNHEAD),
                                            hipcub::Max(), (int)n, c->stream));
-  head_key_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(core, par, P<uint64_t>(c, B_RUNHEAD), n, key);
+  KCHK(c, "hipcub");
+  head_key_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(core, par, P<uint32_t>(c, B_RUNHEAD), n, key);
   KCHK(c, "head_key_kernel");
   tb = c->bufs[B_CUB_TMP].n;
-  HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint64_t>(c, B_RUNHEAD),
+  HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tb, key, P<uint32_t>(c, B_RUNHEAD),
                                            hipcub::Max(), (int)n, c->stream));
-  walk_kernel<<<1, 64, 0, c->stream>>>(par, P<uint64_t>(c, B_RUNHEAD), slot, P<u32x4>(c, B_CREC),
+  KCHK(c, "hipcub");
+  walk_kernel<<<1, 64, 0, c->stream>>>(par, P<uint32_t>(c, B_RUNHEAD), slot, P<u32x4>(c, B_CREC),
                                        P<uint64_t>(c, B_INTS), ws, n);
   KCHK(c, "walk_kernel");
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(hws, ws, sizeof(WalkState), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  static_assert(sizeof(WalkState) <= 64, "h_small[8..16)");
+  HIPCHK(hipMemcpyAsync(c->h_small + 8, ws, sizeof(WalkState), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(spin_sync(c->stream));
+  memcpy(hws, c->h_small + 8, sizeof(WalkState));
   if (hws->status != 1) return 0;
   mark_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_INTS), ws, n, core,
                                                      P<uint32_t>(c, B_ONPATH));
@@ -345,14 +363,14 @@ int walk_and_mark(Ctx* c, const int64_t* par, const uint64_t* slot, uint64_t n, 
   tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_ONPATH),
                                           P<uint32_t>(c, B_CPOS), (int)(n + 1), c->stream));
+  KCHK(c, "hipcub");
   scatter_chain_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(P<uint32_t>(c, B_ONPATH), P<uint32_t>(c, B_CPOS), n,
                                                               map, P<uint64_t>(c, B_CHAIN_G));
   KCHK(c, "scatter_chain_kernel");
   HIPCHK(hipGetLastError());
-  uint32_t on = 0;
-  HIPCHK(hipMemcpyAsync(&on, P<uint32_t>(c, B_CPOS) + n, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  hws->chain_len = 1 + (uint64_t)on;
+  HIPCHK(hipMemcpyAsync(c->h_small + 8, P<uint32_t>(c, B_CPOS) + n, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(spin_sync(c->stream));
+  hws->chain_len = 1 + (uint64_t)(uint32_t)c->h_small[8];
   return 0;
 }
 
@@ -400,6 +418,7 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   HIPCHK(hipHostMalloc((void**)&c->h_plan, sizeof(Plan), hipHostMallocDefault));
   HIPCHK(hipHostMalloc((void**)&c->h_pub, 64, hipHostMallocCoherent));  // fine-grained: the device's system-scope stores land here
   memset(c->h_pub, 0, 64);
+  HIPCHK(hipHostMalloc((void**)&c->h_small, 256, hipHostMallocDefault));
   c->stage_workers = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
@@ -419,6 +438,7 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
     if (e) hipEventDestroy(e);
   if (c->h_plan) hipHostFree(c->h_plan);
   if (c->h_pub) hipHostFree(c->h_pub);
+  if (c->h_small) hipHostFree(c->h_small);
   if (c->h_out) hipHostFree(c->h_out);
   for (int i = 0; i < 2; i++) {
     if (c->pin_ent[i]) hipHostFree(c->pin_ent[i]);
@@ -502,8 +522,8 @@ static int alloc_dense(Ctx* c, uint64_t K) {
   TRY(ensure(c, B_DM, K * 8));
   TRY(ensure(c, B_DPAR, K * 8));
   TRY(ensure(c, B_DSLOT, K * 8));
-  TRY(ensure(c, B_DHEAD, K * 8));
-  TRY(ensure(c, B_RUNHEAD, K * 8));
+  TRY(ensure(c, B_DHEAD, K * 4));    // run keys / heads: g + 1 in 32 bits (K < 2^32 - 1: run_scan)
+  TRY(ensure(c, B_RUNHEAD, K * 4));
   TRY(ensure(c, B_INTS, K * 16 + 16));
   TRY(ensure(c, B_ONPATH, (K + 1) * 4));
   TRY(ensure(c, B_CPOS, (K + 1) * 4));
@@ -583,6 +603,7 @@ static int index_global(Ctx* c, uint64_t n, uint64_t* n_index, const uint64_t* k
   size_t tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_LATEST),
                                           P<uint32_t>(c, B_IPOS), (int)(n + 1), c->stream));
+  KCHK(c, "hipcub");
   if (n) {
     index_emit_kernel<<<blocks(n, 256), 256, 0, c->stream>>>(kh, mo, P<uint32_t>(c, B_LATEST), P<uint32_t>(c, B_IPOS),
                                                              n, okey, opacked);
@@ -591,7 +612,7 @@ static int index_global(Ctx* c, uint64_t n, uint64_t* n_index, const uint64_t* k
   }
   uint32_t nidx = 0;
   HIPCHK(hipMemcpyAsync(&nidx, P<uint32_t>(c, B_IPOS) + n, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   *n_index = nidx;
   return 0;
 }
@@ -656,11 +677,14 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
     }
   }
   // ---- KeyIndexer::build (bucketed; the global table if a bucket overflows) ----
+  // the counters (n_bad: final after finalize / slow) ride on the build's wait
+  TRY(enqueue_counters(c));
   uint64_t nidx = 0;
   TRY(index_build_sep(c, P<uint64_t>(c, B_O_KH), P<uint64_t>(c, B_O_MO), n, P<uint64_t>(c, B_IKEY),
                       P<uint64_t>(c, B_IPACKED), &nidx));
+  if (!n) HIPCHK(spin_sync(c->stream));  // index_build_sep waited only for n > 0
   uint64_t h[8];
-  TRY(read_counters(c, h));
+  memcpy(h, c->h_small, 64);
   out->n_index = nidx;
   out->n_crc_bad = h[6];
   out->n_chain = n;
@@ -709,8 +733,11 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     size_t tb = c->bufs[B_CUB_TMP].n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_SPAN_COUNT),
                                             P<uint64_t>(c, B_SPAN_BASE), (int)(n_spans + 1), c->stream));
-    HIPCHK(hipMemcpyAsync(K, P<uint64_t>(c, B_SPAN_BASE) + n_spans, 8, hipMemcpyDeviceToHost, c->stream));
+    KCHK(c, "hipcub");
+    TRY(enqueue_small(c, P<uint64_t>(c, B_SPAN_BASE) + n_spans, 0));
     TRY(read_counters(c, h));
+    *K = c->h_small[8];
+    if (*K >= 0xFFFFFFFFull) { set_err("more than 2^32 - 2 chain-node candidates (full pass)"); return SRD_ERR_ALLOC; }
     if (n_spans && c->timing >= SRD_TIMING_SCAN) {
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
@@ -735,7 +762,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     l.d_m = P<uint64_t>(c, B_DM);
     l.d_par = P<int64_t>(c, B_DPAR);
     l.d_slot = P<uint64_t>(c, B_DSLOT);
-    link_kernel<<<blocks(n_spans, 64), 256, 0, c->stream>>>(l);
+    link_kernel<<<blocks(n_spans, 256 / LINK_LANES), 256, 0, c->stream>>>(l);
     KCHK(c, "link_kernel");
     HIPCHK(hipGetLastError());
   } else {
@@ -744,9 +771,23 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
   return 0;
 }
 
-__global__ void vpos_kernel(const uint64_t* vl, uint64_t n, uint64_t* vp) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) vp[vl[i]] = i;
+__global__ void walk_start_kernel(WalkState* ws, const uint64_t* vpos, uint64_t g) {
+  if (threadIdx.x == 0) {
+    WalkState w{};
+    w.start = vpos[g];
+    *ws = w;
+  }
+}
+__global__ void compact_valid_kernel(const uint32_t* vflag, const uint32_t* vscan, uint64_t K, uint64_t* vlist,
+                                     uint64_t* vpos, uint64_t* nv) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= K) return;
+  const uint32_t pos = vscan[g], f = vflag[g];
+  if (f) {
+    vlist[pos] = g;
+    vpos[g] = pos;
+  }
+  if (g == K - 1) *nv = (uint64_t)pos + (f ? 1 : 0);
 }
 
 static int set_single_root(Ctx* c, uint64_t t) {
@@ -1048,11 +1089,10 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
         HIPCHK(hipEventRecord(c->ev[3], c->stream));  // end of the device work (srd_ctx_timings)
         c->ev3_recorded = true;
       }
-      HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
       // the outcome idx_emit publishes to pinned memory when it starts; a
       // proven chain whose index aliases the chain arrays needs nothing else
-      // (the plan copy after it finishes on its own); anything else waits
-      // for the stream and reads the whole plan
+      // (no plan copy is enqueued: the next call's scan would queue behind
+      // it); anything else copies the whole plan and waits for the stream
       bool fast = false;
       if (!index_global_env() && !(c->timing >= SRD_TIMING_CALL)) {
         uint64_t w[PUB_WORDS];
@@ -1070,6 +1110,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
         }
       }
       if (!fast) {
+        HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(spin_sync(c->stream));
         hp = *c->h_plan;
       }
@@ -1143,7 +1184,7 @@ extern "C" int srd_validate_index_device(srd_ctx* c, const uint8_t* d_file, uint
       HIPCHK(hipEventRecord(c->ev[3], c->stream));
       HIPCHK(hipEventSynchronize(c->ev[3]));
     } else {
-      HIPCHK(hipStreamSynchronize(c->stream));
+      HIPCHK(spin_sync(c->stream));
     }
   }
   if (tcall) {
@@ -1189,7 +1230,7 @@ extern "C" int srd_validate_span_device(srd_ctx* c, const uint8_t* d_span, uint6
     HIPCHK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
     c->total_ms = ms;
   } else {
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(spin_sync(c->stream));
   }
   return r;
 }
@@ -1217,13 +1258,14 @@ static int partition_impl(Ctx* c, const uint64_t* keys, const uint64_t* vals, ui
   KCHK(c, "part_count_kernel");
   size_t tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, a.cnt, a.off, (int)nc, c->stream));
+  KCHK(c, "hipcub");
   part_scatter_kernel<<<GLUE_BLOCKS, 256, 0, c->stream>>>(a);
   KCHK(c, "part_scatter_kernel");
   part_counts_kernel<<<1, 64, 0, c->stream>>>(a);
   KCHK(c, "part_counts_kernel");
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(counts, a.counts, world * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   return 0;
 }
 
@@ -1255,7 +1297,7 @@ static int index_build_sep(Ctx* c, const uint64_t* keys, const uint64_t* vals, u
   KCHK(c, "set_u64_kernel");
   TRY(launch_index_bucketed(c, keys, vals, &pl->n_chain, &pl->status, log2_nbk, okeys, opacked, pl));
   HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   if (c->h_plan->idx_overflow) return index_global(c, n, n_index, keys, vals, okeys, opacked);
   *n_index = c->h_plan->n_index;
   return 0;
@@ -1330,8 +1372,8 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     const unsigned kb = blocks(K, 256);
     const int64_t* par = P<int64_t>(c, B_DPAR);
     uint8_t* core = P<uint8_t>(c, B_CORE);
-    uint64_t* key = P<uint64_t>(c, B_DHEAD);
-    uint64_t* chead = P<uint64_t>(c, B_RUNHEAD);
+    uint32_t* key = P<uint32_t>(c, B_DHEAD);
+    uint32_t* chead = P<uint32_t>(c, B_RUNHEAD);
     uint8_t* st = P<uint8_t>(c, B_ST);
     int64_t* jmp = P<int64_t>(c, B_JMP);
     HIPCHK(hipMemsetAsync(core, 0, K, c->stream));
@@ -1341,25 +1383,31 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     KCHK(c, "core_flag_key_kernel");
     size_t tbs = c->bufs[B_CUB_TMP].n;
     HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tbs, key, chead, hipcub::Max(), (int)K, c->stream));
+    KCHK(c, "hipcub");
     head_key_kernel<<<kb, 256, 0, c->stream>>>(core, par, chead, K, key);
     KCHK(c, "head_key_kernel");
     tbs = c->bufs[B_CUB_TMP].n;
     HIPCHK(hipcub::DeviceScan::InclusiveScan(P<void>(c, B_CUB_TMP), tbs, key, chead, hipcub::Max(), (int)K, c->stream));
+    KCHK(c, "hipcub");
     status_init_kernel<<<kb, 256, 0, c->stream>>>(par, core, chead, K, st, jmp);
     KCHK(c, "status_init_kernel");
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
     // pointer jumping over the core run heads: every round doubles how far
     // each unresolved head looks along its chain of runs, so ceil(log2 K) + 1
-    // rounds resolve every head; they run back to back and one more round,
-    // with the change flag cleared before it, proves convergence with a
-    // single host sync
+    // rounds resolve every head.  Rounds run back to back (a round after
+    // convergence exits at once) and one more round, with the change flag
+    // cleared before it, proves convergence with one host wait: first 12
+    // rounds (C2's chain of runs converges in ~10), then 8, 16, ... more
     int rounds = 1;
     while ((1ull << rounds) < K) rounds++;
     TRY(ensure(c, B_RFLAG, 4 * 72));
     unsigned int* rflag = P<unsigned int>(c, B_RFLAG);
+    int done_rounds = 0;
     for (int pass = 0; pass < 8; pass++) {
+      const int nr = std::max(1, std::min(pass ? 4 << pass : 12, rounds + 1 - done_rounds));
+      done_rounds += nr;
       HIPCHK(hipMemsetAsync(rflag, 0, 4 * 72, c->stream));
-      for (int r = 0; r <= (pass ? 0 : std::min(rounds, 70)); r++) {
+      for (int r = 0; r < std::min(nr, 70); r++) {
         // a fixed grid (grid-stride): a round after convergence exits at once
         status_round_kernel<<<std::min(kb, 1024u), 256, 0, c->stream>>>(K, core, chead, st, jmp, rflag + r,
                                                                        r ? rflag + r - 1 : nullptr);
@@ -1382,17 +1430,13 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     TRY(ensure(c, B_JMP, std::max<uint64_t>(K, vb) * 8));  // per-block maxima (the jump pointers are dead now)
     valid_max_kernel<<<vb, 256, 0, c->stream>>>(P<uint8_t>(c, B_ST), K, P<uint64_t>(c, B_JMP), P<uint32_t>(c, B_VFLAG));
     KCHK(c, "valid_max_kernel");
-    max_reduce_kernel<<<1, 1024, 0, c->stream>>>(P<uint64_t>(c, B_JMP), vb, (unsigned long long*)(cnt + 3));
+    max_reduce_kernel<<<1, 1024, 0, c->stream>>>(P<uint64_t>(c, B_JMP), vb, (unsigned long long*)(cnt + 3),
+                                                 P<uint64_t>(c, B_DM), (unsigned long long*)(cnt + 7));
     KCHK(c, "max_reduce_kernel");
     HIPCHK(hipGetLastError());
     TRY(read_counters(c, h));
     best_g1 = h[3];
-    if (best_g1) {
-      uint64_t bm;
-      HIPCHK(hipMemcpyAsync(&bm, P<uint64_t>(c, B_DM) + best_g1 - 1, 8, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
-      tlin = bm + 20;
-    }
+    if (best_g1) tlin = h[7] + 20;  // d_m[best_g1 - 1] + 20
   }
   const uint64_t final_len = std::max(tlin, max_root);
   out->final_len = final_len;
@@ -1407,28 +1451,30 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
   TRY(ensure(c, B_VPOS, K * 8));
   TRY(ensure(c, B_VPAR, K * 8));
   TRY(ensure(c, B_VSLOT, K * 8));
+  // valid nodes in dense order: an exclusive scan of the flags, then one
+  // scatter writes vlist[pos] = g, vpos[g] = pos and nv (no host wait before
+  // the remap: its grid covers K and stops at nv on the device)
+  TRY(ensure(c, B_VSCAN, K * 4));
   size_t tb = c->bufs[B_CUB_TMP].n;
-  HIPCHK(hipcub::DeviceSelect::Flagged(P<void>(c, B_CUB_TMP), tb, hipcub::CountingInputIterator<uint64_t>(0),
-                                       P<uint32_t>(c, B_VFLAG), P<uint64_t>(c, B_VLIST), P<uint64_t>(c, B_NV),
-                                       (int)K, c->stream));
-  uint64_t nv = 0;
-  HIPCHK(hipMemcpyAsync(&nv, P<uint64_t>(c, B_NV), 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  // vpos[vlist[i]] = i  (scatter via a tiny lambda kernel)
-  vpos_kernel<<<blocks(nv, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_VLIST), nv, P<uint64_t>(c, B_VPOS));
-  KCHK(c, "vpos_kernel");
-  remap_kernel<<<blocks(nv, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_VLIST), P<uint64_t>(c, B_NV),
-                                                       P<int64_t>(c, B_DPAR), P<uint64_t>(c, B_VPOS),
-                                                       P<int64_t>(c, B_VPAR), P<uint64_t>(c, B_VSLOT),
-                                                       P<uint64_t>(c, B_DSLOT));
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint32_t>(c, B_VFLAG), P<uint32_t>(c, B_VSCAN),
+                                          (int)K, c->stream));
+  KCHK(c, "hipcub");
+  compact_valid_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<uint32_t>(c, B_VFLAG), P<uint32_t>(c, B_VSCAN), K,
+                                                              P<uint64_t>(c, B_VLIST), P<uint64_t>(c, B_VPOS),
+                                                              P<uint64_t>(c, B_NV));
+  KCHK(c, "compact_valid_kernel");
+  remap_kernel<<<blocks(K, 256), 256, 0, c->stream>>>(P<uint64_t>(c, B_VLIST), P<uint64_t>(c, B_NV),
+                                                      P<int64_t>(c, B_DPAR), P<uint64_t>(c, B_VPOS),
+                                                      P<int64_t>(c, B_VPAR), P<uint64_t>(c, B_VSLOT),
+                                                      P<uint64_t>(c, B_DSLOT));
   KCHK(c, "remap_kernel");
+  // the walk starts at the best node's compacted position
+  walk_start_kernel<<<1, 64, 0, c->stream>>>(P<WalkState>(c, B_WALK), P<uint64_t>(c, B_VPOS), best_g1 - 1);
+  KCHK(c, "walk_start_kernel");
   HIPCHK(hipGetLastError());
-  uint64_t vstart = 0;
-  HIPCHK(hipMemcpyAsync(&vstart, P<uint64_t>(c, B_VPOS) + best_g1 - 1, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  WalkState w{};
-  w.start = vstart;
-  HIPCHK(hipMemcpyAsync(P<WalkState>(c, B_WALK), &w, sizeof w, hipMemcpyHostToDevice, c->stream));
+  TRY(enqueue_small(c, P<uint64_t>(c, B_NV), 0));
+  HIPCHK(spin_sync(c->stream));
+  const uint64_t nv = c->h_small[8];
   WalkState hw{};
   TRY(walk_and_mark(c, P<int64_t>(c, B_VPAR), P<uint64_t>(c, B_VSLOT), nv, P<uint64_t>(c, B_VLIST), &hw));
   if (hw.status != 1) { set_err("internal: valid walk did not reach a root"); return SRD_ERR_INTERNAL; }
@@ -1649,7 +1695,7 @@ extern "C" int srd_validate_index(srd_ctx* c, const uint8_t* file, uint64_t flen
     HIPCHK(hipMemcpyAsync(out->index_key_hash, r.index_key_hash, r.n_index * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(out->index_packed, r.index_packed, r.n_index * 8, hipMemcpyDeviceToHost, c->stream));
   }
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   return 0;
 }
 
@@ -2188,7 +2234,7 @@ extern "C" int srd_key_indexer_build(srd_ctx* c, const uint8_t* file, uint64_t t
     HIPCHK(hipMemcpyAsync(keys, r.index_key_hash, k * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(packed, r.index_packed, k * 8, hipMemcpyDeviceToHost, c->stream));
   }
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   return 0;
 }
 
@@ -2232,7 +2278,7 @@ static int batch_host(srd_ctx* c, const uint8_t* buf, uint64_t blen, const uint6
   }
   int r = launch((const uint8_t*)db, (const uint64_t*)dof, (const uint64_t*)dl, (OUT*)dout);
   if (!r && n) HIPCHK(hipMemcpyAsync(out, dout, n * sizeof(OUT), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   hipFree(db); hipFree(dof); hipFree(dl); hipFree(dout);
   return r;
 }
@@ -2290,7 +2336,7 @@ static int synth_launch(Ctx* c, uint8_t* d_abs, const std::vector<uint64_t>& off
       d_abs, (const uint64_t*)doff, (const uint64_t*)dl, fixed_len, n, seed, e0, clip_lo);
   KCHK(c, "synth_kernel");
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   hipFree(doff);
   if (dl) hipFree(dl);
   return 0;
@@ -2434,7 +2480,7 @@ extern "C" int srd_batch_write(srd_ctx* c, uint64_t tail, const uint8_t* keys, c
   }
   if (kh_out) HIPCHK(hipMemcpyAsync(kh_out, kh_dev, n * 8, hipMemcpyDeviceToHost, c->stream));
   if (mo_out) HIPCHK(hipMemcpyAsync(mo_out, mo_dev, n * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   return 0;
 }
 
@@ -2468,7 +2514,7 @@ extern "C" int srd_index_table_build_device(srd_ctx* c, const uint64_t* d_keys, 
     KCHK(c, "idx_table_insert_kernel");
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   return 0;
 }
 
@@ -2539,7 +2585,7 @@ extern "C" int srd_batch_read(srd_ctx* c, const void* d_table, uint64_t table_by
     HIPCHK(hipMemcpyAsync(start_out, ds, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(end_out, de, n * 8, hipMemcpyDeviceToHost, c->stream));
   }
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   cleanup();
   return r;
 }
@@ -2569,19 +2615,20 @@ static int iter_run(Ctx* c, const uint8_t* d_file, uint64_t flen, const uint64_t
   KCHK(c, "iter_flag_kernel");
   size_t tb = c->bufs[B_CUB_TMP].n;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, flag, pos, (int)n, c->stream));
+  KCHK(c, "hipcub");
   uint32_t last[2] = {0, 0};
   unsigned long long hk = 0;
   HIPCHK(hipMemcpyAsync(&last[0], pos + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(&last[1], flag + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(&hk, kept, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   const uint64_t nv = (uint64_t)last[0] + last[1];
   if (d_start && nv) {
     iter_emit_kernel<<<grid_for(n), 256, 0, c->stream>>>(d_file, d_packed, flag, pos, n, nv, P<uint64_t>(c, B_IT_ST),
                                                          P<uint64_t>(c, B_IT_EN), d_start, d_end, d_meta, d_kh);
     KCHK(c, "iter_emit_kernel");
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(spin_sync(c->stream));
   }
   *n_out = nv;
   if (kept_bytes) *kept_bytes = hk;
@@ -2631,12 +2678,14 @@ extern "C" int srd_compact_device(srd_ctx* c, const uint8_t* d_file, uint64_t fl
   TRY(ensure(c, B_IT_KEPT, 64));
   size_t tb = 0;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)nv));
+  KCHK(c, "hipcub");
   TRY(ensure(c, B_CUB_TMP, tb + 256));
   tb = c->bufs[B_CUB_TMP].n;
   compact_sizes_kernel<<<grid_for(nv), 256, 0, c->stream>>>(st, en, nv, P<uint64_t>(c, B_IT_RLEN));
   KCHK(c, "compact_sizes_kernel");
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(P<void>(c, B_CUB_TMP), tb, P<uint64_t>(c, B_IT_RLEN),
                                           P<uint64_t>(c, B_IT_PST), (int)nv, c->stream));
+  KCHK(c, "hipcub");
   uint64_t* d_new_len = P<uint64_t>(c, B_IT_KEPT) + 2;
   compact_entries_kernel<<<grid_for(nv), 256, 0, c->stream>>>(st, en, P<uint64_t>(c, B_IT_OKH), P<uint64_t>(c, B_IT_PST),
                                                              nv, P<srd_write_entry>(c, B_IT_ENT), d_new_len);
@@ -2644,7 +2693,7 @@ extern "C" int srd_compact_device(srd_ctx* c, const uint8_t* d_file, uint64_t fl
   HIPCHK(hipGetLastError());
   uint64_t tail = 0;
   HIPCHK(hipMemcpyAsync(&tail, d_new_len, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   *new_len = tail;
   if (!d_out) return 0;
   if (tail > out_cap) { set_err("out_cap too small for the compacted store"); return SRD_ERR_ARG; }
@@ -2657,7 +2706,7 @@ extern "C" int srd_compact_device(srd_ctx* c, const uint8_t* d_file, uint64_t fl
                    d_meta_off_out ? d_meta_off_out : P<uint64_t>(c, B_WMO), nullf));
   unsigned int hn = 0;
   HIPCHK(hipMemcpyAsync(&hn, nullf, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(spin_sync(c->stream));
   if (hn) {  // write_stream rejects NULL-only payloads (data_store.rs:792-797); compact() fails with it
     set_err("NULL-byte-only streams cannot be written directly.");
     return SRD_ERR_ARG;

@@ -302,6 +302,13 @@ __device__ __forceinline__ uint64_t start_node(const ShapeArgs& a, uint64_t K) {
   const uint64_t t = a.counters[1];
   return (K && t >= 21 && a.c_m[a.d_slot[K - 1]] == t - 20) ? K - 1 : NO_NODE;
 }
+// the dense arrays are incomplete: more candidates than the dense capacity
+// (ST_CAPK), or a record region overflowed (ST_OVERFLOW: link2 wrote no
+// parent / slot for the records past it) -- the shape kernels must not read
+// them; chain_finalize reports the status and the host retries larger
+__device__ __forceinline__ bool dense_incomplete(const ShapeArgs& a, uint64_t K) {
+  return K > a.capK || a.counters[2] != 0;
+}
 
 // Core nodes of the current round: the start node, or a node some node of
 // the previous round links to (has_child[g] == gen), whose own parent was
@@ -319,14 +326,14 @@ __device__ __forceinline__ bool is_core(const ShapeArgs& a, uint64_t g, uint64_t
 // the retry's round-0 marks: the nodes link2 claims were made on
 __global__ __launch_bounds__(256) void marks_from_claims_kernel(ShapeArgs a, uint32_t* marks_out) {
   const uint64_t K = *a.Kp;
-  if (K > a.capK) return;
+  if (dense_incomplete(a, K)) return;
   for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x)
     if ((a.childof[g] >> 32) == a.gen) marks_out[g] = a.gen;
 }
 
 __global__ __launch_bounds__(256) void prune_kernel(ShapeArgs a, uint32_t* marks_out, uint32_t gen_out) {
   const uint64_t K = *a.Kp;
-  if (K > a.capK) return;
+  if (dense_incomplete(a, K)) return;
   const uint64_t start = start_node(a, K);
   for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x) {
     const int64_t p = a.d_par[g];
@@ -337,7 +344,7 @@ __global__ __launch_bounds__(256) void prune_kernel(ShapeArgs a, uint32_t* marks
 __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_zero; i += gridDim.x * blockDim.x) a.zero[i] = 0;
   const uint64_t K = *a.Kp;
-  if (K > a.capK) return;
+  if (dense_incomplete(a, K)) return;
   const uint64_t start = start_node(a, K);
   // CR nodes per thread per pass: loads first (no store in between)
   constexpr int CR = 4;
@@ -378,7 +385,7 @@ __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
 __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
   __shared__ uint32_t wsum[CHAIN_WAVES];
   const uint64_t K = *a.Kp;
-  if (K > a.capK) return;
+  if (dense_incomplete(a, K)) return;
   const uint64_t start = start_node(a, K);
   const uint64_t tag = (uint64_t)a.gen << 32;
   const bool marks = a.has_child != nullptr;  // retry rounds
@@ -658,6 +665,18 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   __shared__ uint32_t slowq[CHAIN_THREADS * FIN_R];
   __shared__ uint32_t nslow;
   extern __shared__ uint32_t hist[];
+  // the LDS tables' words first, into registers: their loads overlap the
+  // plan's dependent ones below (one round trip instead of a load -> store
+  // loop after the plan)
+  static_assert(CHAIN_THREADS == 1024, "one word of each 1024-word table per thread");
+  const uint32_t ti = threadIdx.x;
+  const uint32_t r_tab = g_tabs.tab[ti >> 8][ti & 255], r_mx = (&g_tabs.mx64[0][0])[ti],
+                 r_m16k = (&g_tabs.m16k[0][0])[ti];
+  uint32_t r_inv[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) r_inv[j] = g_tabs.invpow[ti + 1024 * j];
+  const uint32_t r_inv_last = g_tabs.invpow[4096];
+  const uint32_t r_winit = g_tabs.winit[ti & 63], r_zc = g_tabs.zero_crc[ti & 63];
   const uint64_t K = *a.Kp;
   const bool capk = K > a.capK;
   uint64_t before = 0, total = 0;
@@ -671,7 +690,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   const uint64_t root_t = troot ? top : pl->root_t;
   if (capk) st |= ST_CAPK;
   if (a.counters[2]) st |= ST_OVERFLOW;
-  const uint64_t start = capk ? NO_NODE : start_node(a, K);
+  const uint64_t start = dense_incomplete(a, K) ? NO_NODE : start_node(a, K);
   if (start == NO_NODE) st |= ST_NOSTART;
   if (pl->nroot != 1) st |= ST_ROOTS;
   __syncthreads();  // this block has read pl->status / nroot / root_t before block 0 rewrites them
@@ -697,15 +716,15 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   }
   if (st && !troot) return;
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
-  for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
-    tab[i] = g_tabs.tab[i >> 8][i & 255];
-    mx[i] = (&g_tabs.mx64[0][0])[i];
-    lt.m16k[i] = (&g_tabs.m16k[0][0])[i];
-  }
-  for (uint32_t i = threadIdx.x; i < 4097; i += blockDim.x) lt.invpow[i] = g_tabs.invpow[i];
-  if (threadIdx.x < 64) {
-    lt.winit[threadIdx.x] = g_tabs.winit[threadIdx.x];
-    lt.zero_crc[threadIdx.x] = g_tabs.zero_crc[threadIdx.x];
+  tab[ti] = r_tab;
+  mx[ti] = r_mx;
+  lt.m16k[ti] = r_m16k;
+#pragma unroll
+  for (int j = 0; j < 4; j++) lt.invpow[ti + 1024 * j] = r_inv[j];
+  if (ti == 0) lt.invpow[4096] = r_inv_last;
+  if (ti < 64) {
+    lt.winit[ti] = r_winit;
+    lt.zero_crc[ti] = r_zc;
   }
   if (threadIdx.x == 0) nslow = 0;
   __syncthreads();

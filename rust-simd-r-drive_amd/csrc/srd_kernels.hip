@@ -1011,14 +1011,17 @@ struct LinkArgs {
   uint64_t* d_slot;
 };
 
-// 4 lanes per span, 64 spans per block (one 64-thread block per span left
-// most lanes idle and put 256K blocks through the dispatcher at C2)
+// LINK_LANES lanes per span, 256 / LINK_LANES spans per block: the full
+// pass records ~11 candidates per C2 span (the real node and the weak ones
+// its checksum bytes make), each a chain of dependent loads with a random
+// file read, so one record per lane (4 lanes and a loop: ~3 records each)
+constexpr uint32_t LINK_LANES = 16;
 __global__ __launch_bounds__(256) void link_kernel(LinkArgs a) {
-  const uint64_t sp = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  const uint64_t sp = (uint64_t)blockIdx.x * (256 / LINK_LANES) + (threadIdx.x / LINK_LANES);
   if (sp >= a.n_spans) return;
   const uint32_t n = min(a.span_count[sp], a.cap);
   const uint64_t gb = a.span_base[sp];
-  for (uint32_t i = threadIdx.x & 3; i < n; i += 4) {
+  for (uint32_t i = threadIdx.x % LINK_LANES; i < n; i += LINK_LANES) {
     const uint64_t gi = sp * a.cap + i;
     const u32x4 r0 = a.c_rec[2 * gi];
     const uint64_t m = a.c_m[gi], p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
@@ -1072,7 +1075,7 @@ struct WalkState {
 };
 
 // idx space: 0..n-1 ; par_of(i) gives par in the same space ; runhead[i]
-__global__ void walk_kernel(const int64_t* par, const uint64_t* runhead, const uint64_t* slot,
+__global__ void walk_kernel(const int64_t* par, const uint32_t* runhead, const uint64_t* slot,
                             const u32x4* c_rec, uint64_t* ints, WalkState* ws, uint64_t max_ints) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint64_t x = ws->start, n = 0, len = 1;
@@ -1105,22 +1108,24 @@ __global__ void child_kernel(const int64_t* par, uint64_t n, uint8_t* core) {
   int64_t p = par[g];
   if (p >= 0) core[p] = 1;
 }
-__global__ void core_key_kernel(uint8_t* core, const WalkState* ws, uint64_t n, uint64_t* key) {
+// run keys and heads are g + 1 in 32 bits (the host bounds the node count
+// below 2^32 - 1: half the bytes of the max-scans)
+__global__ void core_key_kernel(uint8_t* core, const WalkState* ws, uint64_t n, uint32_t* key) {
   uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;
   if (g == ws->start) core[g] = 1;
-  key[g] = core[g] ? g + 1 : 0;
+  key[g] = core[g] ? (uint32_t)(g + 1) : 0u;
 }
 // runs over core nodes: head if its parent is not the previous core node
-__global__ void head_key_kernel(const uint8_t* core, const int64_t* par, const uint64_t* cmax, uint64_t n,
-                                uint64_t* key) {
+__global__ void head_key_kernel(const uint8_t* core, const int64_t* par, const uint32_t* cmax, uint64_t n,
+                                uint32_t* key) {
   uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;
-  uint64_t k = 0;
+  uint32_t k = 0;
   if (core[g]) {
     const uint64_t prev1 = g ? cmax[g - 1] : 0;  // previous core index + 1
     const bool cont = prev1 && par[g] == (int64_t)(prev1 - 1);
-    k = cont ? 0 : g + 1;
+    k = cont ? 0u : (uint32_t)(g + 1);
   }
   key[g] = k;
 }
@@ -1160,7 +1165,7 @@ __global__ void scatter_chain_kernel(const uint32_t* onpath, const uint32_t* cpo
 // parent is the previous core node continues that one's run.  Runs share
 // their head's status and only heads jump (to the head of their parent's
 // run); a leaf then takes its parent's status.  A torn C2 store: one run.
-__global__ void status_init_kernel(const int64_t* par, const uint8_t* core, const uint64_t* chead, uint64_t n,
+__global__ void status_init_kernel(const int64_t* par, const uint8_t* core, const uint32_t* chead, uint64_t n,
                                    uint8_t* st, int64_t* jmp) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n || !core[g] || chead[g] != g + 1) return;  // core run heads only
@@ -1170,7 +1175,7 @@ __global__ void status_init_kernel(const int64_t* par, const uint8_t* core, cons
 }
 // prev (nullable): the previous round's change flag -- a round after one in
 // which no head jumped has nothing left to do (every head resolved)
-__global__ void status_round_kernel(uint64_t n, const uint8_t* core, const uint64_t* chead, uint8_t* st,
+__global__ void status_round_kernel(uint64_t n, const uint8_t* core, const uint32_t* chead, uint8_t* st,
                                     int64_t* jmp, unsigned int* changed, const unsigned int* prev) {
   if (prev && *prev == 0) return;
   for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x) {
@@ -1181,7 +1186,7 @@ __global__ void status_round_kernel(uint64_t n, const uint8_t* core, const uint6
     else { jmp[g] = jmp[j]; *changed = 1; }
   }
 }
-__global__ void status_spread_core_kernel(uint64_t n, const uint8_t* core, const uint64_t* chead, uint8_t* st) {
+__global__ void status_spread_core_kernel(uint64_t n, const uint8_t* core, const uint32_t* chead, uint8_t* st) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n && core[g] && chead[g] != g + 1) st[g] = st[chead[g] - 1];
 }
@@ -1191,9 +1196,9 @@ __global__ void status_spread_leaf_kernel(uint64_t n, const int64_t* par, const 
   const int64_t p = par[g];
   st[g] = p == PAR_ROOT ? 1 : (p == PAR_MISS ? 2 : st[p]);
 }
-__global__ void core_flag_key_kernel(const uint8_t* core, uint64_t n, uint64_t* key) {
+__global__ void core_flag_key_kernel(const uint8_t* core, uint64_t n, uint32_t* key) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) key[g] = core[g] ? g + 1 : 0;
+  if (g < n) key[g] = core[g] ? (uint32_t)(g + 1) : 0u;
 }
 
 // the largest valid node: a block maximum per block (same-address atomics
@@ -1210,7 +1215,11 @@ __global__ __launch_bounds__(256) void valid_max_kernel(const uint8_t* st, uint6
   __syncthreads();
   if (threadIdx.x == 0) bmax[blockIdx.x] = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
 }
-__global__ __launch_bounds__(1024) void max_reduce_kernel(const uint64_t* v, uint64_t n, unsigned long long* out) {
+// *out = max of the per-block maxima (best_g1 = 1 + the valid node with the
+// largest tail, 0 if none); *meta = d_m[best_g1 - 1], that node's metadata
+// offset (one host wait reads both)
+__global__ __launch_bounds__(1024) void max_reduce_kernel(const uint64_t* v, uint64_t n, unsigned long long* out,
+                                                          const uint64_t* d_m, unsigned long long* meta) {
   __shared__ uint64_t wm[16];
   uint64_t m = 0;
   for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) m = max(m, v[i]);
@@ -1220,6 +1229,7 @@ __global__ __launch_bounds__(1024) void max_reduce_kernel(const uint64_t* v, uin
   if (threadIdx.x == 0) {
     for (int w = 1; w < 16; w++) m = max(m, wm[w]);
     *out = m;
+    *meta = m ? d_m[m - 1] : 0ull;
   }
 }
 // remap parents into the compacted valid space
