@@ -130,7 +130,8 @@ def cpu_baseline(store_dev: torch.Tensor, size: int, bytes_alg: int, budget_s: f
 def e2e(store, size, bytes_alg, ctx, reps=3):
     """End to end from host memory (the path starts in the mmap'd file,
     data_store.rs:172-174): host bytes -> HBM -> validate+index -> host
-    result arrays (srd_validate_index).  Variants: a pinned host buffer; the
+    result arrays (srd_validate_index, the library call: its arrays left in
+    the context's pinned buffers).  Variants: a pinned host buffer; the
     store as a FILE in the page cache, mapped afresh each time (mmap ->
     srd_validate_index -> munmap, page faults included) under each staging
     mode, and with MAP_POPULATE; the same after posix_fadvise(DONTNEED) (a
@@ -144,7 +145,7 @@ def e2e(store, size, bytes_alg, ctx, reps=3):
     def row(dt, r=None):
         mode, st = ctx.stage_info()
         out = {"ms": round(dt * 1e3, 2), "GiBps": round(bytes_alg / dt / 2**30, 3), "staging": mode,
-               "stage_ms": round(st, 2)}
+               "stage_ms": round(st, 2), "after_stage_ms": round(dt * 1e3 - st, 2)}
         if r is not None:
             assert r.final_len == size and r.n_crc_bad == 0
         return out
@@ -152,11 +153,16 @@ def e2e(store, size, bytes_alg, ctx, reps=3):
     host = torch.empty(size, dtype=torch.uint8).pin_memory()
     host.copy_(store[:size])
     torch.cuda.synchronize()
-    S.validate_index(host.numpy(), 0, ctx)
+    S.validate_index_call(host.numpy(), 0, ctx)
     t0 = time.perf_counter()
     for _ in range(reps):
-        r = S.validate_index(host.numpy(), 0, ctx)
+        r = S.validate_index_call(host.numpy(), 0, ctx)
     res["pinned_buffer"] = row((time.perf_counter() - t0) / reps, r)
+    # the Python mirror's Result copies the ~77 MB of host arrays into numpy:
+    # its cost, apart from the library call
+    t0 = time.perf_counter()
+    S.Result(r)
+    res["python_result_copy_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
     del host
     d = tempfile.mkdtemp(prefix="srd_e2e_")
     path = os.path.join(d, "c2.store")
@@ -166,7 +172,7 @@ def e2e(store, size, bytes_alg, ctx, reps=3):
         try:
             mm = M.mmap(fd, 0, flags=M.MAP_SHARED | (M.MAP_POPULATE if populate else 0), prot=M.PROT_READ)
             v = np.frombuffer(mm, np.uint8)
-            r = S.validate_index(v, flags, ctx)
+            r = S.validate_index_call(v, flags, ctx)
             del v
             mm.close()
             return r

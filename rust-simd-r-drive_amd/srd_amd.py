@@ -300,6 +300,17 @@ def validate_index(file, flags: int = 0, ctx: Context | None = None) -> Result:
         lib().srd_result_free(C.byref(r))
 
 
+def validate_index_call(file, flags: int = 0, ctx: Context | None = None) -> DeviceResult:
+    """srd_validate_index alone: the result's arrays stay in the context-owned
+    pinned host buffers (valid until the next call on ctx; `Result(r)` copies
+    them into numpy).  The end-to-end timing of the library call."""
+    ctx = ctx or default_ctx()
+    a = _u8(file)
+    r = DeviceResult()
+    _check(lib().srd_validate_index(ctx.h, _ptr(a), a.size, flags, C.byref(r)))
+    return r
+
+
 def validate_index_multi(file, ctxs, flags: int = 0) -> Result:
     """DataStore::open's pass over one host store on len(ctxs) GPUs in one
     process (srd_validate_index_multi): entry-range shards, host composition,
