@@ -67,13 +67,31 @@ struct Buf {
   size_t n = 0;
 };
 
+// Candidate record slots per span; grow x4 on overflow and are remembered by
+// the context for stores of a similar size.  The optimistic pass starts at 8
+// (a C2 span holds ~4 records): its 4096 scan waves write their records into
+// regions of spans x cap slots, and with 64 slots the regions were 135 KiB
+// apart (a 604 MB record buffer for C2) -- on the first-allocated workspace of
+// a process that cost 6-8 % of the scan (same-box A/B, profiles/r03/
+// scan_record_regions_ab.txt); at 8 the regions are 17 KiB apart and every
+// placement runs at the fast rate.
+struct CandCap {
+  uint32_t cap;          // slots per span
+  uint32_t grown_cap;    // the cap the last overflow needed ...
+  uint64_t grown_bytes;  // ... for a store (span) of this many bytes
+  uint32_t floor;        // the default (a store of another size starts here again)
+};
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::vector<Buf> bufs;  // indexed by the enum below
-  uint32_t cap = 64;      // candidate slots per span (4 tiles); grows x4 on overflow
-  uint32_t grown_cap = 64;   // the cap the last overflow needed ...
-  uint64_t grown_bytes = 0;  // ... for a store (span) of this many bytes
+  // candidate slots per span (4 tiles) of the optimistic pass's scan and of
+  // the full pass's (CandCap): each scan wave's records are dense in a region
+  // of (its spans x cap) slots, so the cap sets how far apart the waves'
+  // record stores land -- see CandCap
+  CandCap copt{8, 8, 0, 8};
+  CandCap cfull{32, 32, 0, 32};
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
   uint32_t scan_wq[4] = {0, 0, 0, 0};  // ScanPart::wq (scan_weights())
   srd_device_result res{};
@@ -458,20 +476,17 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
 
 extern "C" void* srd_ctx_stream(srd_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-// Candidate slots per span grow x4 on overflow and are remembered by the
-// context; a store of another size starts lower again, so the records (40 B
-// per slot) stay within ~2x the store.  A store within 2x of the size whose
-// overflow grew the cap keeps that cap (a dense store would otherwise
-// overflow -- and rescan -- on every call).
-static void fit_cap(Ctx* c, uint64_t n_spans, uint64_t bytes) {
-  const bool similar = c->grown_bytes && bytes <= 2 * c->grown_bytes && 2 * bytes >= c->grown_bytes;
-  const uint32_t floor = similar ? c->grown_cap : 64;
-  while (c->cap > floor && (uint64_t)c->cap * 40 * n_spans > 2 * bytes + (64ull << 20)) c->cap /= 4;
+// A store of another size starts at the default again; a store within 2x of
+// the size whose overflow grew the cap keeps that cap (a dense store would
+// otherwise overflow -- and rescan -- on every call).
+static void fit_cap(CandCap& k, uint64_t bytes) {
+  const bool similar = k.grown_bytes && bytes <= 2 * k.grown_bytes && 2 * bytes >= k.grown_bytes;
+  k.cap = similar ? std::max(k.grown_cap, k.floor) : k.floor;
 }
-static void grow_cap(Ctx* c, uint64_t bytes) {
-  c->cap = (uint32_t)std::min<uint64_t>((uint64_t)c->cap * 4, SPAN_BYTES);
-  c->grown_cap = c->cap;
-  c->grown_bytes = bytes;
+static void grow_cap(CandCap& k, uint64_t bytes) {
+  k.cap = (uint32_t)std::min<uint64_t>((uint64_t)k.cap * 4, SPAN_BYTES);
+  k.grown_cap = k.cap;
+  k.grown_bytes = bytes;
 }
 
 static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g) {
@@ -506,8 +521,8 @@ static int scan_wave_args(Ctx* c, ScanArgs* a) {
   return 0;
 }
 
-static int alloc_scan(Ctx* c, uint64_t n_tiles, uint64_t n_spans) {
-  const uint64_t slots = n_spans * c->cap;
+static int alloc_scan(Ctx* c, uint64_t n_tiles, uint64_t n_spans, uint32_t cap) {
+  const uint64_t slots = n_spans * cap;
   TRY(ensure(c, B_TILE, n_tiles * 16));
   TRY(ensure(c, B_SPAN_COUNT, (n_spans + 1) * 4));
   TRY(ensure(c, B_SPAN_BASE, (n_spans + 1) * 8));
@@ -695,9 +710,9 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
 static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uint64_t* K, uint64_t* h) {
   const uint64_t n_tiles = (flen + TILE - 1) / TILE;
   const uint64_t n_spans = (n_tiles + SPAN_TILES - 1) / SPAN_TILES;
-  fit_cap(c, n_spans, flen);
+  fit_cap(c->cfull, flen);
   while (true) {
-    TRY(alloc_scan(c, n_tiles, n_spans));
+    TRY(alloc_scan(c, n_tiles, n_spans, c->cfull.cap));
     TRY(ensure_cub(c, n_spans + 1));
     uint64_t* cnt = P<uint64_t>(c, B_COUNTERS);
     HIPCHK(hipMemsetAsync(cnt, 0, 64, c->stream));
@@ -708,7 +723,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.flen = flen;
     a.n_tiles = n_tiles;
     a.n_spans = n_spans;
-    a.cap = c->cap;
+    a.cap = c->cfull.cap;
     a.tile = P<uint32_t>(c, B_TILE);
     a.span_count = P<uint32_t>(c, B_SPAN_COUNT);
     a.c_m = P<uint64_t>(c, B_CM);
@@ -745,8 +760,8 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
       c->scan_launches++;
     }
     if ((uint32_t)h[2] == 0) break;
-    if (c->cap >= SPAN_BYTES) { set_err("candidate overflow"); return SRD_ERR_INTERNAL; }
-    grow_cap(c, flen);
+    if (c->cfull.cap >= SPAN_BYTES) { set_err("candidate overflow"); return SRD_ERR_INTERNAL; }
+    grow_cap(c->cfull, flen);
   }
   if (*K) {
     TRY(alloc_dense(c, *K));
@@ -754,7 +769,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     l.file = d_file;
     l.flen = flen;
     l.n_spans = n_spans;
-    l.cap = c->cap;
+    l.cap = c->cfull.cap;
     l.span_count = P<uint32_t>(c, B_SPAN_COUNT);
     l.span_base = P<uint64_t>(c, B_SPAN_BASE);
     l.c_m = P<uint64_t>(c, B_CM);
@@ -918,7 +933,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
   const uint64_t k_lo = span_off / TILE, s_lo = k_lo / SPAN_TILES;
   const uint64_t nt_rel = n_tiles - k_lo, ns_rel = n_spans - s_lo;
   const uint32_t coff = lo ? 0u : 1u;
-  fit_cap(c, ns_rel, flen - span_off);
+  fit_cap(c->copt, flen - span_off);
   for (int attempt = 0; attempt < 6; attempt++) {
     if (!c->capK) c->capK = (flen - span_off) / 1024 + 4096;
     const uint64_t capK = c->capK;
@@ -934,10 +949,10 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const ScanPart part = scan_part(c, s_lo, ns_rel, g);
     const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
     const uint64_t spw = part_max_wave_spans(part);
-    const uint64_t wcap = spw * c->cap;
+    const uint64_t wcap = spw * c->copt.cap;
     // the glue's record slots are 32-bit (d_slot): stores above ~1 TiB take the full pass
     if (total_waves * wcap >= (1ull << 32)) return 0;
-    TRY(alloc_scan(c, nt_rel, std::max<uint64_t>(ns_rel, total_waves * spw)));
+    TRY(alloc_scan(c, nt_rel, std::max<uint64_t>(ns_rel, total_waves * spw), c->copt.cap));
     TRY(ensure(c, B_SPAN_FIRST, (ns_rel + 1) * 4));
     TRY(alloc_fast(c, capK, log2_nbk));
     if (c->gen >= 0xFFFFFFF0u || c->gen == 0) {  // tag wrap: clear the marks once
@@ -959,7 +974,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.flen = flen;
     a.n_tiles = n_tiles;
     a.n_spans = n_spans;
-    a.cap = c->cap;
+    a.cap = c->copt.cap;
     a.tile = P<uint32_t>(c, B_TILE) - 4 * k_lo;
     a.span_count = P<uint32_t>(c, B_SPAN_COUNT) - s_lo;
     a.c_m = P<uint64_t>(c, B_CM);  // wave regions, indexed by the wave of this launch
@@ -1135,8 +1150,8 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     out->n_candidates = hp.K;
     out->n_weak = 0;
     if (hp.status & ST_OVERFLOW) {
-      if (c->cap >= SPAN_BYTES) return 0;  // cannot happen (<= one candidate per byte); not provable here
-      grow_cap(c, flen - span_off);
+      if (c->copt.cap >= SPAN_BYTES) return 0;  // cannot happen (<= one candidate per byte); not provable here
+      grow_cap(c->copt, flen - span_off);
       continue;
     }
     if (hp.status & ST_CAPK) {
@@ -1342,7 +1357,7 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
   out->file_len = flen;
   if (flen < 21) {  // no tail can be valid (recover_valid_chain :384-386, t>=21)
     TRY(alloc_dense(c, 1));
-    TRY(alloc_scan(c, 1, 1));
+    TRY(alloc_scan(c, 1, 1, c->copt.cap));
     return finish(c, d_file, flen, 0, flags, out);
   }
   bool full = flags & SRD_FLAG_FORCE_FULL;
