@@ -35,6 +35,14 @@ S.synth_store_device(t.data_ptr(), n, 4096, None, seed=0x5EED0001, ctx=variants[
 torch.cuda.synchronize()
 print(f"store ptr {t.data_ptr():#x} bytes {t.numel()}", file=sys.stderr)
 reps = int(os.environ.get("REPS", 10))
+# BIND_ORDER=reverse|forward: a kernel on every context's stream (its HW queue binding) before any first call
+if os.environ.get("BIND_ORDER"):
+    keep = []
+    for name, ctx in (variants[::-1] if os.environ["BIND_ORDER"] == "reverse" else variants):
+        es = torch.cuda.ExternalStream(ctx.stream)
+        with torch.cuda.stream(es):
+            keep.append(torch.zeros(1024, device="cuda") + 1)
+        es.synchronize()
 # FIRST_ORDER=reverse: the contexts' first calls (their workspace allocations) in reverse order
 first = variants[::-1] if os.environ.get("FIRST_ORDER") == "reverse" else variants
 for name, ctx in first:
