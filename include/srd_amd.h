@@ -89,10 +89,11 @@ const char *srd_last_error(void);
 #define SRD_TIMING_CALL 2
 int srd_ctx_set_timing(srd_ctx *ctx, int level);
 
-/* HIP-event timings of the last srd_validate_index(_device) call on ctx,
- * measured on the context stream: summed duration of the streaming scan
- * kernel launches (ms), their count, and the device span of the whole call
- * (0 unless the timing level includes them). */
+/* HIP-event timings on the context stream: the summed duration (ms) and the
+ * count of the streaming scan kernel launches of every validate call since the
+ * previous srd_ctx_timings call (the scans' event pairs are read out here, not
+ * inside the calls), and the device span of the last call (0 unless the
+ * timing level includes them). */
 int srd_ctx_timings(srd_ctx *ctx, double *scan_ms, int *scan_launches,
                     double *total_ms);
 

@@ -99,11 +99,16 @@ struct Ctx {
   Buf file;
   // timing (HIP events on `stream`)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  // srd_ctx_set_timing: 0 none (default), 1 scan kernel (ev[0], ev[1]), 2 +
-  // whole call (ev[2], ev[3]); each event record costs ~11 us of the C2
-  // call's wall time (4 events: 1.104 ms, 2: 1.081, none: 1.070)
+  // srd_ctx_set_timing: 0 none (default), 1 scan kernel (a ring of start /
+  // stop pairs stamped by the scan dispatches), 2 + whole call (ev[2],
+  // ev[3]).  The scan pairs are read out when srd_ctx_timings asks (or when
+  // the ring wraps), not inside the calls: hipEventElapsedTime per call was
+  // host time on every call's critical path
   int timing = SRD_TIMING_NONE;
-  double scan_ms = 0, total_ms = 0;
+  static constexpr uint32_t kScanRing = 64;
+  hipEvent_t sev[2 * kScanRing] = {};
+  uint32_t sev_next = 0, sev_pending = 0;  // next pair, pairs not yet read out
+  double scan_ms = 0, total_ms = 0;  // scan_ms / scan_launches: since the last srd_ctx_timings
   int scan_launches = 0;
   // sync-free optimistic pass
   uint64_t capK = 0;    // dense candidate capacity (grows on ST_CAPK)
@@ -261,7 +266,11 @@ template <bool FULL>
 static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr) {
   const dim3 grid(g), block(SCAN_WAVES_V2 * 64);
-  static const bool marker = [] { const char* e = getenv("SRD_SCAN_MARKER_EVENTS"); return e && *e == '1'; }();
+#ifdef SRD_SCAN_MARKER_EVENTS  // timing A/B builds: marker events around a plain launch
+  constexpr bool marker = true;
+#else
+  constexpr bool marker = false;
+#endif
   if (e0 && marker) {  // timing A/B only: marker events around a plain launch
     (void)hipEventRecord(e0, s);
     launch_scan<FULL>(g, a, s);
@@ -453,6 +462,8 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
     if (b.p) hipFree(b.p);
   if (c->file.p) hipFree(c->file.p);
   for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  for (auto& e : c->sev)
     if (e) hipEventDestroy(e);
   if (c->h_plan) hipHostFree(c->h_plan);
   if (c->h_pub) hipHostFree(c->h_pub);
@@ -707,6 +718,31 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
   return 0;
 }
 
+// read out the oldest n pending scan event pairs (their launches completed
+// before the call that made them returned)
+static int drain_scan_events(Ctx* c, uint32_t n) {
+  for (; n && c->sev_pending; n--) {
+    const uint32_t i = (c->sev_next - c->sev_pending) % Ctx::kScanRing;
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->sev[2 * i], c->sev[2 * i + 1]));
+    c->scan_ms += ms;
+    c->scan_launches++;
+    c->sev_pending--;
+  }
+  return 0;
+}
+// the event pair for the next scan launch (none below SRD_TIMING_SCAN)
+static int next_scan_events(Ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
+  *e0 = *e1 = nullptr;
+  if (c->timing < SRD_TIMING_SCAN) return 0;
+  if (c->sev_pending == Ctx::kScanRing) TRY(drain_scan_events(c, 1));
+  const uint32_t i = c->sev_next++ % Ctx::kScanRing;
+  c->sev_pending++;
+  *e0 = c->sev[2 * i];
+  *e1 = c->sev[2 * i + 1];
+  return 0;
+}
+
 static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uint64_t* K, uint64_t* h) {
   const uint64_t n_tiles = (flen + TILE - 1) / TILE;
   const uint64_t n_spans = (n_tiles + SPAN_TILES - 1) / SPAN_TILES;
@@ -737,11 +773,12 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     if (n_spans) {
       unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
       a.part = scan_part(c, 0, n_spans, g);
-      hipEvent_t e0 = c->timing >= SRD_TIMING_SCAN ? c->ev[0] : nullptr;
+      hipEvent_t e0, e1;
+      TRY(next_scan_events(c, &e0, &e1));
       if (full)
-        launch_scan<true>(g, a, c->stream, e0, c->ev[1]);
+        launch_scan<true>(g, a, c->stream, e0, e1);
       else
-        launch_scan<false>(g, a, c->stream, e0, c->ev[1]);
+        launch_scan<false>(g, a, c->stream, e0, e1);
       KCHK(c, "scan_kernel");
       HIPCHK(hipGetLastError());
     }
@@ -753,12 +790,6 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     TRY(read_counters(c, h));
     *K = c->h_small[8];
     if (*K >= 0xFFFFFFFFull) { set_err("more than 2^32 - 2 chain-node candidates (full pass)"); return SRD_ERR_ALLOC; }
-    if (n_spans && c->timing >= SRD_TIMING_SCAN) {
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-      c->scan_ms += ms;
-      c->scan_launches++;
-    }
     if ((uint32_t)h[2] == 0) break;
     if (c->cfull.cap >= SPAN_BYTES) { set_err("candidate overflow"); return SRD_ERR_INTERNAL; }
     grow_cap(c->cfull, flen);
@@ -989,7 +1020,9 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.n_zero_words = (uint32_t)(sizeof(Plan) / 4);
     a.sentinel = nullptr;
     TRY(scan_wave_args(c, &a));
-    launch_scan<false>(g, a, c->stream, c->timing >= SRD_TIMING_SCAN ? c->ev[0] : nullptr, c->ev[1]);
+    hipEvent_t e0, e1;
+    TRY(next_scan_events(c, &e0, &e1));
+    launch_scan<false>(g, a, c->stream, e0, e1);
     KCHK(c, "scan_kernel");
     HIPCHK(hipGetLastError());
     Link2Args l{};
@@ -1020,7 +1053,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     uint32_t* marks = P<uint32_t>(c, B_HASCHILD);
     uint32_t* marks2 = P<uint32_t>(c, B_HASCHILD2);
     uint32_t mgen = c->gen;
-    bool timed = false;
     for (int rounds = 0;; rounds += 2) {
       if (rounds) HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));  // round 0: zeroed by the scan
       ShapeArgs sa{};
@@ -1136,13 +1168,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
                 (unsigned long)hp.n_index, (unsigned long)hp.n_bad, (unsigned long)hp.n_slow, hp.status, hp.nroot,
                 hp.troot, hp.idx_overflow, log2_nbk, (unsigned long)capK, rounds);
       }
-      if (!timed && c->timing >= SRD_TIMING_SCAN) {
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-        c->scan_ms += ms;
-        c->scan_launches++;
-        timed = true;
-      }
       // only a shape / root-count failure can be a false chain; at most 6 extra rounds
       const uint32_t retry_bits = ST_SHAPE | ST_ROOTS;
       if (!(hp.status & retry_bits) || (hp.status & ~retry_bits) || rounds >= 6) break;
@@ -1187,8 +1212,6 @@ extern "C" int srd_validate_index_device(srd_ctx* c, const uint8_t* d_file, uint
                                          srd_device_result* out) {
   if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
   HIPCHK(hipSetDevice(c->device));
-  c->scan_ms = 0;
-  c->scan_launches = 0;
   c->total_ms = 0;
   c->ev3_recorded = false;
   const bool tcall = c->timing >= SRD_TIMING_CALL;
@@ -1222,8 +1245,6 @@ extern "C" int srd_validate_span_device(srd_ctx* c, const uint8_t* d_span, uint6
     return SRD_ERR_ARG;
   }
   HIPCHK(hipSetDevice(c->device));
-  c->scan_ms = 0;
-  c->scan_launches = 0;
   memset(out, 0, sizeof *out);
   out->file_len = hi;
   c->total_ms = 0;
@@ -1336,15 +1357,23 @@ extern "C" int srd_index_build_device(srd_ctx* c, const uint64_t* d_pairs, uint6
 
 extern "C" int srd_ctx_set_timing(srd_ctx* c, int level) {
   if (!c || level < SRD_TIMING_NONE || level > SRD_TIMING_CALL) { set_err("bad argument"); return SRD_ERR_ARG; }
+  if (level >= SRD_TIMING_SCAN && !c->sev[0]) {
+    HIPCHK(hipSetDevice(c->device));
+    for (auto& e : c->sev) HIPCHK(hipEventCreateWithFlags(&e, hipEventReleaseToDevice));
+  }
   c->timing = level;
   return 0;
 }
 
 extern "C" int srd_ctx_timings(srd_ctx* c, double* scan_ms, int* scan_launches, double* total_ms) {
   if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
+  TRY(drain_scan_events(c, c->sev_pending));
   if (scan_ms) *scan_ms = c->scan_ms;
   if (scan_launches) *scan_launches = c->scan_launches;
   if (total_ms) *total_ms = c->total_ms;
+  c->scan_ms = 0;
+  c->scan_launches = 0;
   return 0;
 }
 

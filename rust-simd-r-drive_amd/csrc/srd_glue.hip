@@ -41,6 +41,13 @@
 
 namespace srd {
 
+// The glue's per-entry outputs (~100 MB per C2 call) are written with
+// nontemporal stores: kept as dirty lines in L2 / the Infinity Cache they were
+// written back while the NEXT call's scan streamed the store (same-process
+// A/B, three contexts each: scan -1 %, call -1 %, profiles/r03/
+// scan_record_regions_ab.txt)
+#define GST(ptr, val) __builtin_nontemporal_store((val), &(ptr))
+
 struct Plan {
   uint64_t K;          // dense candidates
   uint64_t n_chain;    // chain entries incl. the root entry
@@ -268,8 +275,8 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
         par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
       }
     }
-    a.d_par[g] = (int32_t)par;
-    a.d_slot[g] = (uint32_t)gi;
+    GST(a.d_par[g], (int32_t)par);
+    GST(a.d_slot[g], (uint32_t)gi);
     if (par >= 0 && (uint64_t)par < a.capK) atomicMax(&a.childof[par], ((unsigned long long)a.gen << 32) | g);
   }
 }
@@ -421,7 +428,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
       const int64_t p = par[r];
       const bool linked = marks ? hc[r] == a.gen : (cg[r] & ~0xffffffffull) == tag;
       const bool core = g[r] == start || (linked && (p >= 0 || p == PAR_ROOT));  // is_core(g)
-      a.flag[g[r]] = core;
+      GST(a.flag[g[r]], (uint8_t)core);
       if (!core) continue;
       cnt++;
       const bool plinked = marks ? hp[r] == a.gen : (cp[r] & ~0xffffffffull) == tag;
@@ -618,8 +625,8 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
     else if (j == 32) { sxm = e.t1[2]; pieces |= 2; }
   }
   const uint64_t len = mo - start;
-  a.o_start[c] = start;  // o_mo / o_kh / o_prev / o_crc_st: stored by the caller
-  a.o_len[c] = len;
+  GST(a.o_start[c], start);  // o_mo / o_kh / o_prev / o_crc_st: stored by the caller
+  GST(a.o_len[c], len);
   if (a.no_crc) { a.o_crc[c] = 0; a.o_ok[c] = 0; return false; }
   uint32_t crc;
   if (tomb) {
@@ -650,8 +657,8 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
       crc = ~(mulp(t.invpow[(k1 + 1) * TILE - mo], y) ^ tail);
     }
   }
-  a.o_crc[c] = crc;
-  a.o_ok[c] = crc == e.crc_st;
+  GST(a.o_crc[c], crc);
+  GST(a.o_ok[c], (uint8_t)(crc == e.crc_st));
   if (crc != e.crc_st) atomicAdd(a.n_bad, 1ull);
   return false;
 }
@@ -793,11 +800,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       for (int r = 0; r < FIN_R; r++) {
         if (!fl[r]) continue;
         const uint64_t c = run + rank[r];
-        f.o_mo[c] = e[r].mo;
-        f.o_kh[c] = kh[r];
-        f.o_packed[c] = ((kh[r] >> 48) << 48) | (e[r].mo & 0xFFFFFFFFFFFFull);  // key_indexer.rs:79-85
-        f.o_prev[c] = e[r].p;
-        f.o_crc_st[c] = e[r].crc_st;
+        GST(f.o_mo[c], e[r].mo);
+        GST(f.o_kh[c], kh[r]);
+        GST(f.o_packed[c], ((kh[r] >> 48) << 48) | (e[r].mo & 0xFFFFFFFFFFFFull));  // key_indexer.rs:79-85
+        GST(f.o_prev[c], e[r].p);
+        GST(f.o_crc_st[c], e[r].crc_st);
         atomicAdd(&hist[idx_bucket(kh[r], log2_nbk)], 1u);
       }
 #pragma unroll

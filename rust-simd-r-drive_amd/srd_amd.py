@@ -203,7 +203,8 @@ class Context:
         _check(lib().srd_ctx_set_timing(self.h, level))
 
     def timings(self):
-        """(scan_ms, scan_launches, total_ms) of the last validate call (HIP events)."""
+        """(scan_ms, scan_launches) summed over the validate calls since the last
+        read, and total_ms of the last call (HIP events; srd_ctx_timings)."""
         a, n, b = C.c_double(), C.c_int(), C.c_double()
         _check(lib().srd_ctx_timings(self.h, C.byref(a), C.byref(n), C.byref(b)))
         return a.value, n.value, b.value

@@ -374,6 +374,15 @@ def test_timing_levels_do_not_change_results():
                 assert launches == 1 and scan_ms > 0
                 assert (total_ms > 0) == (level == S.TIMING_CALL)
         assert all(o == (size, n, 0, n, S.SRD_MODE_OPTIMISTIC) for o in outs), outs
+        # the scan's event pairs are read out by srd_ctx_timings: summed over
+        # every call since the last read, also past the 64-pair ring
+        c.set_timing(S.TIMING_SCAN)
+        for calls in (3, 70):
+            for _ in range(calls):
+                S.validate_index_device(t.data_ptr(), size, 0, c)
+            scan_ms, launches, _ = c.timings()
+            assert launches == calls and scan_ms > 0
+            assert c.timings()[:2] == (0.0, 0)
         with pytest.raises(S.SrdError):
             c.set_timing(3)
     finally:

@@ -11,6 +11,11 @@ import torch
 import srd_amd as S
 
 L = S.lib()
+n = int(os.environ.get("N_ENTRIES", 1 << 20))
+size = S.synth_store_len(n, 4096, None)
+t = None
+if os.environ.get("STORE_FIRST"):  # the store allocated before any context exists
+    t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
 variants = []
 for spec in sys.argv[1:]:
     name, _, rest = spec.partition(":")
@@ -28,9 +33,8 @@ for spec in sys.argv[1:]:
         else:
             os.environ[k] = v
     variants.append((name, ctx))
-n = int(os.environ.get("N_ENTRIES", 1 << 20))
-size = S.synth_store_len(n, 4096, None)
-t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
+if t is None:
+    t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
 S.synth_store_device(t.data_ptr(), n, 4096, None, seed=0x5EED0001, ctx=variants[0][1])
 torch.cuda.synchronize()
 print(f"store ptr {t.data_ptr():#x} bytes {t.numel()}", file=sys.stderr)
