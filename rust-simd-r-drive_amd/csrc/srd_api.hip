@@ -93,7 +93,7 @@ struct Ctx {
   CandCap copt{8, 8, 0, 8};
   CandCap cfull{32, 32, 0, 32};
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
-  uint32_t scan_wq[4] = {0, 0, 0, 0};  // ScanPart::wq (scan_weights())
+  uint32_t scan_wq[16] = {};  // ScanPart::wq (scan_weights())
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -405,23 +405,52 @@ int walk_and_mark(Ctx* c, const int64_t* par, const uint64_t* slot, uint64_t n, 
 
 struct srd_ctx : Ctx {};
 
-// ScanPart::wq, the per-wave share of each age group (waves 4q..4q+3 of a
-// block).  Default: inverse to the finish times an even split gave on MI355X
-// (wave slots 0-3 / 4-7 / 8-11 / 12-15 ended at 1 : 1.069 : 1.125 : 1.179,
-// tools/wave_stamps.py); SRD_SCAN_WEIGHTS="a,b,c,d" sets relative shares
-// ("1,1,1,1" is the even split).
-static void scan_weights(uint32_t (&wq)[4]) {
-  double f[4] = {1.0, 1.0 / 1.069, 1.0 / 1.125, 1.0 / 1.179};
+// ScanPart::wq, the share of each wave slot of a block.  The SIMD's issue
+// arbitration favours its older waves (slots 0-3 are the oldest on each
+// SIMD, 12-15 the youngest), so an even split ended the slots at 1 : 1.069 :
+// 1.125 : 1.179 by age group (tools/wave_stamps.py).  Default: per-slot
+// shares from the wave stamps of per-age-group shares (1 : 1/1.069 : 1/1.125
+// : 1/1.179), each slot's share scaled by (mean end / its end)^1.5: -1.3 to
+// -1.6 % scan against the age-group shares, -0.8 % at power 1, -0.6 % at 2
+// (tools/weights_ab.py: every set inside the same contexts).
+// SRD_SCAN_WEIGHTS sets relative shares: 4 values (one per age group;
+// "1,1,1,1" is the even split) or 16 (one per slot).
+static void scan_weights(uint32_t (&wq)[16]) {
+  double f[16] = {1.0000, 0.9787, 0.9796, 0.9788, 0.9081, 0.9072, 0.9074, 0.8915,
+                  0.8432, 0.8324, 0.8337, 0.8314, 0.7726, 0.7701, 0.7712, 0.7590};
   if (const char* e = getenv("SRD_SCAN_WEIGHTS")) {
-    double g[4];
-    if (sscanf(e, "%lf,%lf,%lf,%lf", &g[0], &g[1], &g[2], &g[3]) == 4 && g[0] > 0 && g[1] > 0 && g[2] > 0 && g[3] > 0)
-      for (int q = 0; q < 4; q++) f[q] = g[q];
+    double g[16];
+    int n = 0;
+    for (const char* q = e; n < 16 && *q;) {
+      char* end = nullptr;
+      const double x = strtod(q, &end);
+      if (end == q || !(x > 0)) { n = 0; break; }
+      g[n++] = x;
+      q = *end == ',' ? end + 1 : end;
+      if (*end && *end != ',') { n = 0; break; }
+    }
+    if (n == 4)
+      for (int v = 0; v < 16; v++) f[v] = g[v / 4];
+    else if (n == 16)
+      for (int v = 0; v < 16; v++) f[v] = g[v];
   }
-  const double sum = f[0] + f[1] + f[2] + f[3];
+  double sum = 0;
+  for (double x : f) sum += x;
   uint32_t used = 0;
-  for (int q = 0; q < 3; q++) used += wq[q] = (uint32_t)(16384.0 * f[q] / sum);
-  wq[3] = 16384 - used;
+  for (int v = 0; v < 15; v++) used += wq[v] = (uint32_t)(65536.0 * f[v] / sum);
+  wq[15] = 65536 - used;
 }
+#ifdef SRD_DEBUG_API  // timing builds: A/B of scan partitions inside one context (one workspace)
+extern "C" int srd_debug_set_scan_weights(srd_ctx* c, const double* w, int n) {
+  if (!c || !w || (n != 4 && n != 16)) return SRD_ERR_ARG;
+  double f[16], sum = 0;
+  for (int v = 0; v < 16; v++) sum += f[v] = n == 4 ? w[v / 4] : w[v];
+  uint32_t used = 0;
+  for (int v = 0; v < 15; v++) used += c->scan_wq[v] = (uint32_t)(65536.0 * f[v] / sum);
+  c->scan_wq[15] = 65536 - used;
+  return 0;
+}
+#endif
 extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   if (!out) { set_err("null out"); return SRD_ERR_ARG; }
   int n = 0;
@@ -505,13 +534,13 @@ static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g) 
   p.s_lo = s_lo;
   p.ns = ns;
   p.g = g;
-  for (int q = 0; q < 4; q++) p.wq[q] = c->scan_wq[q];
+  for (int q = 0; q < 16; q++) p.wq[q] = c->scan_wq[q];
   return p;
 }
 // an upper bound on the spans of one wave
 static uint64_t part_max_wave_spans(const ScanPart& p) {
   if (!p.g) return 1;
-  const uint32_t wmax = std::max(std::max(p.wq[0], p.wq[1]), std::max(p.wq[2], p.wq[3]));
+  const uint32_t wmax = *std::max_element(p.wq, p.wq + 16);
   const uint64_t nb = (p.ns + p.g - 1) / p.g;
   return (nb * wmax + 65535) / 65536 + 1;
 }

@@ -80,21 +80,19 @@ __device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]
 // spans.  Waves of one SIMD do not progress equally: the SIMD issues for
 // its oldest waves first, so with an even split waves 0-3 (the oldest on
 // each SIMD) finished ~15% before waves 12-15 (tools/wave_stamps.py); the
-// per-age-group shares wq[q] (waves 4q..4q+3) even out the finish times.
+// per-slot shares wq[v] (by default per age group, waves 4q..4q+3) even out
+// the finish times.
 struct ScanPart {
   uint64_t s_lo;   // first resident span
   uint64_t ns;     // resident spans
   uint32_t g;      // scan blocks
-  uint32_t wq[4];  // per-wave share of age group q; 4 * (wq[0] + .. + wq[3]) == 65536
+  uint32_t wq[16];  // share of wave slot v of each block; wq[0] + .. + wq[15] == 65536
 };
 // cumulative share of the waves below v (v <= 16)
 __host__ __device__ __forceinline__ uint64_t part_cw(const ScanPart& p, uint32_t v) {
   uint64_t c = 0;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const int k = (int)v - 4 * q;
-    c += (uint64_t)(k <= 0 ? 0 : k >= 4 ? 4 : k) * p.wq[q];
-  }
+  for (uint32_t q = 0; q < 16; q++) c += q < v ? p.wq[q] : 0u;
   return c;
 }
 __host__ __device__ __forceinline__ uint64_t part_block_start(const ScanPart& p, uint64_t b) {
