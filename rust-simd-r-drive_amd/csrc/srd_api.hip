@@ -535,6 +535,7 @@ static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g) 
   p.ns = ns;
   p.g = g;
   for (int q = 0; q < 16; q++) p.wq[q] = c->scan_wq[q];
+  part_fill_cw(p);
   return p;
 }
 // an upper bound on the spans of one wave
@@ -1074,7 +1075,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     l.s_lo = s_lo;
     l.span_lo = lo;
     l.zero = index_zero_words(c, log2_nbk, &l.n_zero);  // chain_finalize claims the bucket fills
-    link2_kernel<<<blocks(ns_rel, 64), 256, 0, c->stream>>>(l);
+    link2_kernel<<<(unsigned)total_waves, 256, 0, c->stream>>>(l);  // one block per scan wave
     KCHK(c, "link2_kernel");
     // ---- shape check, chain, finalize, index; retried on device with more
     //      prune rounds when false candidates chained onto each other ----

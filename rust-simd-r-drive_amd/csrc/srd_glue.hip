@@ -203,9 +203,11 @@ struct Link2Args {
   uint32_t n_zero;
 };
 
-// 4 lanes per span.  The scan wrote each wave's records densely in file
-// order: record i of span sp lives at slot w*wcap + span_first[sp] + i and
-// has the dense index wave_base[w] + span_first[sp] + i.
+// One block per scan wave: the wave's records are dense in file order in its
+// region (record r at slot w*wcap + r, dense index wave_base[w] + r), so the
+// block walks them directly -- no per-span lanes, no span -> wave search
+// except in the parent-search fallback.  (4 lanes per span took 1.1 ms at
+// C3, whose 4.4M spans are mostly empty.)
 //
 // Every node with a parent claims it: childof[p] = max((gen << 32) | g).
 // check_kernel reads a node's core flag (someone links to it) and the claim
@@ -218,14 +220,12 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
     for (uint32_t i = t; i < a.n_zero; i += nt) a.zero[i] = 0;
   }
-  const uint64_t sp = a.s_lo + (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
-  if (sp >= a.n_spans) return;
-  const uint64_t w = part_span_wave(a.part, sp - a.s_lo);
-  const uint32_t n = a.span_count[sp], first = a.span_first[sp];
-  const uint64_t gw = w * a.wcap, gb = a.wave_base[w] + first;
-  for (uint32_t i = threadIdx.x & 3; i < n; i += 4) {
-    if ((uint64_t)first + i >= a.wcap) return;  // wave overflow: scatter_plan reports ST_OVERFLOW
-    const uint64_t gi = gw + first + i, g = gb + i;
+  const uint64_t w = blockIdx.x;
+  // records past wcap were not stored (wave overflow: chain_finalize reports ST_OVERFLOW)
+  const uint64_t nrec = min(a.wave_total[w] & ~(1ull << 63), a.wcap);
+  const uint64_t gw = w * a.wcap, gb = a.wave_base[w];
+  for (uint64_t r = threadIdx.x; r < nrec; r += blockDim.x) {
+    const uint64_t gi = gw + r, g = gb + r;
     if (g >= a.capK) return;  // chain_finalize reports ST_CAPK
     const uint64_t m = a.c_m[gi];
     const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     // the previous wave's last record
     uint64_t mprev = 0;
     bool hp = true;
-    if (first + i > 0) {
+    if (r > 0) {
       mprev = a.c_m[gi - 1];
     } else {
       const uint64_t wt = w ? (a.wave_total[w - 1] & ~(1ull << 63)) : 0;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     // In a store without garbage the parent is the previous record in file
     // order: one load instead of a binary search.
     int64_t par = hp && mprev == mp ? (int64_t)(g - 1) : PAR_MISS;
-    if (par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
+    if (node && par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
       const uint64_t w2 = part_span_wave(a.part, sp2 - a.s_lo);
       const uint32_t f2 = a.span_first[sp2];
       const uint32_t n2 = (uint32_t)min<uint64_t>(a.span_count[sp2], a.wcap - min<uint64_t>(f2, a.wcap));

@@ -87,14 +87,14 @@ struct ScanPart {
   uint64_t ns;     // resident spans
   uint32_t g;      // scan blocks
   uint32_t wq[16];  // share of wave slot v of each block; wq[0] + .. + wq[15] == 65536
+  uint32_t cw[17];  // cumulative: cw[v] = wq[0] + .. + wq[v-1] (part_fill_cw)
 };
-// cumulative share of the waves below v (v <= 16)
-__host__ __device__ __forceinline__ uint64_t part_cw(const ScanPart& p, uint32_t v) {
-  uint64_t c = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < 16; q++) c += q < v ? p.wq[q] : 0u;
-  return c;
+__host__ __device__ __forceinline__ void part_fill_cw(ScanPart& p) {
+  p.cw[0] = 0;
+  for (int v = 0; v < 16; v++) p.cw[v + 1] = p.cw[v] + p.wq[v];
 }
+// cumulative share of the waves below v (v <= 16)
+__host__ __device__ __forceinline__ uint64_t part_cw(const ScanPart& p, uint32_t v) { return p.cw[v]; }
 __host__ __device__ __forceinline__ uint64_t part_block_start(const ScanPart& p, uint64_t b) {
   return b * p.ns / p.g;
 }

@@ -1,4 +1,5 @@
-"""Per-XCD block weights, A/B inside each context (timing tool; the SRD_DEBUG_API build): the weights learn
+"""(Experiment reverted: srd_debug_xcd is gone from the library; kept as the record of the measurement.)
+Per-XCD block weights, A/B inside each context (timing tool; the SRD_DEBUG_API build): the weights learn
 over LEARN calls (adaptive), then rounds alternate the learned weights and the even split, both held fixed."""
 import ctypes as C, json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
