@@ -11,7 +11,8 @@
 //   link2           4 lanes per span: node test of single-candidate records,
 //                   parent lookup (previous record, else a binary search in
 //                   the parent's span), 32-bit d_par / d_slot, and every node
-//                   claims its parent: childof[p] = max(gen:g); zeroes the
+//                   claims its parent (the earliest claimer wins, claim_word);
+//                   zeroes the
 //                   index bucket fills
 //   check           shape test from the claims alone: the core nodes (claimed
 //                   by someone, or the start node at file_len - 20) must form
@@ -182,6 +183,18 @@ __device__ uint64_t block_scan_partials(const uint32_t* part, uint32_t np, uint3
 }
 
 // --------------------------------------------------------------------------
+// A claim on a parent: the generation in the high word (stale words of
+// earlier calls lose any atomicMax), ~g in the low word, so the claimer with
+// the SMALLEST dense index holds the parent.  The real child of p is the
+// first node after p in file order; a false candidate that resolves to p
+// lies later (C3: a candidate 8 bytes past some metadata reads that entry's
+// CRC as its prev field, and one in ~7000 such CRCs equals a real tail below
+// 4 GiB) -- with the largest claimer winning it took the parent from the real
+// child, and every C3 call went through the retry rounds.
+__device__ __forceinline__ unsigned long long claim_word(uint32_t gen, uint64_t g) {
+  return ((unsigned long long)gen << 32) | (0xffffffffull - (g & 0xffffffffull));
+}
+
 struct Link2Args {
   const uint8_t* file;
   uint64_t flen, n_spans, capK;
@@ -209,7 +222,7 @@ struct Link2Args {
 // except in the parent-search fallback.  (4 lanes per span took 1.1 ms at
 // C3, whose 4.4M spans are mostly empty.)
 //
-// Every node with a parent claims it: childof[p] = max((gen << 32) | g).
+// Every node with a parent claims it: childof[p] = max(claim_word(gen, g)).
 // check_kernel reads a node's core flag (someone links to it) and the claim
 // on its parent from these words alone -- no separate marking pass.  A
 // parent claimed by two nodes keeps the larger; if the loser is a chain node
@@ -277,7 +290,7 @@ __global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
     }
     GST(a.d_par[g], (int32_t)par);
     GST(a.d_slot[g], (uint32_t)gi);
-    if (par >= 0 && (uint64_t)par < a.capK) atomicMax(&a.childof[par], ((unsigned long long)a.gen << 32) | g);
+    if (par >= 0 && (uint64_t)par < a.capK) atomicMax(&a.childof[par], claim_word(a.gen, g));
   }
 }
 
@@ -370,7 +383,7 @@ __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
       const uint64_t g = g0 + r * stride;
       if (g >= K) break;
       const int64_t p = par[r];
-      if (p >= 0 && (g == start || hc[r] == a.gen)) a.childof[p] = ((uint64_t)a.gen << 32) | g;  // is_core(g)
+      if (p >= 0 && (g == start || hc[r] == a.gen)) a.childof[p] = claim_word(a.gen, g);  // is_core(g)
     }
   }
 }
@@ -438,7 +451,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
         a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
       } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
         fail = true;  // dangling: the chain through g is broken (only the start node can get here)
-      } else if (cp[r] != (tag | g[r])) {
+      } else if (cp[r] != claim_word(a.gen, g[r])) {
         fail = true;  // branch: another node holds the claim on the same parent
       }
     }
