@@ -928,7 +928,7 @@ static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
 // zeroed here, idx_hist_kernel claims the ranges and idx_scatter_kernel fills them
 static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
                                  const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
-                                 Plan* pl, bool fused = false) {
+                                 Plan* pl, bool fused = false, const FinArgs* slow = nullptr) {
   TRY(next_lgen(c));
   IdxArgs ia = index_args(c, log2_nbk);
   ia.alias = fused ? 1u : 0u;
@@ -952,7 +952,9 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
     idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
     KCHK(c, "idx_scatter_kernel");
   }
-  idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia);
+  FinArgs fs{};  // n_slow == nullptr: no slow list
+  if (slow) fs = *slow;
+  idx_dedup_kernel<<<nbk, 512, 0, c->stream>>>(ia, fs);
   KCHK(c, "idx_dedup_kernel");
   idx_emit_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(ia);
   KCHK(c, "idx_emit_kernel");
@@ -1153,15 +1155,21 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.o_tail = P<uint32_t>(c, B_O_TAIL);
       f.o_ok = P<uint8_t>(c, B_O_OK);
       f.n_bad = (unsigned long long*)&pl->n_bad;
+      f.slow_list = P<uint64_t>(c, B_SLOW);       // entries that need a wave (idx_dedup runs them)
+      f.n_slow = (unsigned long long*)&pl->n_slow;  // zeroed with the plan
       f.o_packed = P<uint64_t>(c, B_O_PACKED);
       chain_finalize_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, (1u << log2_nbk) * 4, c->stream>>>(
           sa, f, index_args(c, log2_nbk), log2_nbk);
       KCHK(c, "chain_finalize_kernel");
       HIPCHK(hipGetLastError());
       // ---- KeyIndexer::build (bucketed; the global table in SRD_INDEX_GLOBAL timing builds) ----
-      if (!index_global_env())
+      if (!index_global_env()) {
         TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
-                                  P<uint64_t>(c, B_IPACKED), pl, true));
+                                  P<uint64_t>(c, B_IPACKED), pl, true, &f));
+      } else {  // timing builds without the bucketed index: the slow list by its own kernel
+        slow_kernel<<<2048 / SLOW_WAVES, SLOW_WAVES * 64, 0, c->stream>>>(f);
+        KCHK(c, "slow_kernel");
+      }
       if (c->timing >= SRD_TIMING_CALL) {
         HIPCHK(hipEventRecord(c->ev[3], c->stream));  // end of the device work (srd_ctx_timings)
         c->ev3_recorded = true;

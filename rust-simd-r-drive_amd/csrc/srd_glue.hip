@@ -828,8 +828,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       }
       __syncthreads();
       const uint32_t ns = nslow;
-      if (ns) {  // this pass's slow entries, one wave each
-        for (uint32_t q = threadIdx.x >> 6; q < ns; q += CHAIN_WAVES) slow_one(f, run + slowq[q], tab, mx);
+      if (ns) {  // this pass's slow entries go to the call's list (idx_dedup's blocks run them, one wave each)
+        __shared__ unsigned long long sbase;
+        if (threadIdx.x == 0) sbase = atomicAdd(f.n_slow, (unsigned long long)ns);
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < ns; q += CHAIN_THREADS) f.slow_list[sbase + q] = run + slowq[q];
         __syncthreads();
         if (threadIdx.x == 0) nslow = 0;
         __syncthreads();
@@ -837,7 +840,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       run += tot;
     }
   }
-  if (__syncthreads_or(root_slow) && threadIdx.x < 64) slow_one(f, 0, tab, mx);
+  if (root_slow) f.slow_list[atomicAdd(f.n_slow, 1ull)] = 0;  // (block 0, thread 0 only)
   __syncthreads();
   // KeyIndexer::build's scatter for this block's chain positions [clo, run)
   // (block 0 from 0: the root entry): claim the block's range of every
@@ -900,11 +903,31 @@ __global__ __launch_bounds__(256) void idx_scatter_kernel(IdxArgs a) {
   }
 }
 
-// one block per bucket: latest-wins dedup in LDS
-__global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a) {
+// one block per bucket: latest-wins dedup in LDS.  First, the chain entries
+// chain_finalize listed for a wave each (long entries, missing CRC pieces;
+// f.n_slow == nullptr: none) are spread over all the dedup blocks' waves --
+// balanced over the whole grid instead of queued behind their own
+// finalize block (C3: ~340K entries of 5-256 tiles)
+__global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a, FinArgs f) {
   __shared__ unsigned long long keys[IDX_TSLOTS];
   __shared__ uint32_t vals[IDX_TSLOTS];
   __shared__ uint32_t special;
+  if (f.n_slow) {
+    const unsigned long long ns = *f.n_slow;
+    constexpr uint32_t NW = 512 / 64;
+    if ((uint64_t)blockIdx.x * NW < ns) {
+      uint32_t* tab = (uint32_t*)keys;  // the tables in the hash table's LDS, before its use
+      uint32_t* mx = tab + 1024;
+      for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        tab[i] = g_tabs.tab[i >> 8][i & 255];
+        mx[i] = (&g_tabs.mx64[0][0])[i];
+      }
+      __syncthreads();
+      for (uint64_t q = (uint64_t)blockIdx.x * NW + (threadIdx.x >> 6); q < ns; q += (uint64_t)gridDim.x * NW)
+        slow_one(f, f.slow_list[q], tab, mx);
+      __syncthreads();
+    }
+  }
   if (*a.status) return;
   const uint32_t k = blockIdx.x;
   const uint32_t fill = a.bfill[k];
