@@ -916,15 +916,12 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a, FinArgs f) {
     const unsigned long long ns = *f.n_slow;
     constexpr uint32_t NW = 512 / 64;
     if ((uint64_t)blockIdx.x * NW < ns) {
-      uint32_t* tab = (uint32_t*)keys;  // the tables in the hash table's LDS, before its use
-      uint32_t* mx = tab + 1024;
-      for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-        tab[i] = g_tabs.tab[i >> 8][i & 255];
-        mx[i] = (&g_tabs.mx64[0][0])[i];
-      }
+      static_assert(sizeof(SlowLds) <= sizeof(keys), "the slow path's tables in the hash table's LDS");
+      SlowLds& L = *reinterpret_cast<SlowLds*>(keys);  // before the table's own use
+      load_slow_lds(L);
       __syncthreads();
       for (uint64_t q = (uint64_t)blockIdx.x * NW + (threadIdx.x >> 6); q < ns; q += (uint64_t)gridDim.x * NW)
-        slow_one(f, f.slow_list[q], tab, mx);
+        slow_one(f, f.slow_list[q], L);
       __syncthreads();
     }
   }

@@ -1502,36 +1502,103 @@ __device__ __forceinline__ uint32_t xpow8_any(uint64_t n) { return xpow8_dev(n);
 // metadata tile k1 combined by the 64 lanes of the calling wave: lane l
 // Horner-combines tiles k0+1+l, +65+l, ... with X^64 steps, weights its sum by
 // X^(distance of its last tile to tile k1-1), and the wave XOR-reduces.
+// mulp(a, b) for wave-uniform a, b, by the whole wave (every lane gets the
+// product): mulp adds b * x^(31 - i) for every set bit i of a; lane i < 32
+// builds its term from b with (31 - i) / 8 byte steps through the CRC table
+// R (crc8: v * x^8 = (v >> 8) ^ R[v & 0xff], LDS) and the remaining bit
+// steps, then the 32 terms are XOR-reduced -- ~45 instructions instead of
+// mulp's 32 dependent 7-instruction steps (the slow path runs four per entry)
+__device__ __forceinline__ uint32_t mulp_wave(uint32_t a, uint32_t b, const uint32_t* R) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane & 31;
+  const uint32_t e = 31u - (uint32_t)i;
+  uint32_t t = b;
+  for (uint32_t k = 0; k < (e >> 3); k++) t = (t >> 8) ^ R[t & 0xffu];
+  for (uint32_t r = 0; r < (e & 7u); r++) t = (t >> 1) ^ ((t & 1u) ? kPoly : 0u);
+  uint32_t v = ((a >> i) & 1u) ? t : 0u;
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o);
+  return v;  // lanes 32-63 reduce the same 32 terms
+}
+
+// the tables of the slow path in LDS: every input of an entry's combine is a
+// table word, and from global memory each was a dependent round trip
+// (latency, not arithmetic, set the slow path's time: ~10 us per entry)
+struct SlowLds {
+  uint32_t tab[1024];  // slice-by-4 CRC tables (tab[0..255]: the byte step R)
+  uint32_t mx[1024];   // v -> v * X^64 byte tables
+  uint32_t m16k[1024];  // v -> v * x^16384 byte tables (tile_T's lower-half fix)
+  uint32_t invpow[4097];
+  uint32_t xtile[65], xt64[65], winit[64], zero_crc[64];
+  uint32_t x32768;
+};
+__device__ __forceinline__ void load_slow_lds(SlowLds& L) {
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+    L.tab[i] = g_tabs.tab[i >> 8][i & 255];
+    L.mx[i] = (&g_tabs.mx64[0][0])[i];
+    L.m16k[i] = (&g_tabs.m16k[0][0])[i];
+  }
+  for (int i = threadIdx.x; i < 4097; i += blockDim.x) L.invpow[i] = g_tabs.invpow[i];
+  for (int i = threadIdx.x; i < 65; i += blockDim.x) {
+    L.xtile[i] = g_tabs.xtile[i];
+    L.xt64[i] = g_tabs.xt64[i];
+    if (i < 64) {
+      L.winit[i] = g_tabs.winit[i];
+      L.zero_crc[i] = g_tabs.zero_crc[i];
+    }
+  }
+  if (threadIdx.x == 0) L.x32768 = g_tabs.x32768;
+}
+
 __device__ uint32_t crc_from_pieces_wave(uint64_t s, uint64_t m, uint32_t suf, uint32_t sxm, uint32_t tail,
-                                         const uint32_t* tile, const uint32_t* mx64) {
+                                         const uint32_t* tile, const SlowLds& L) {
+  const uint32_t* mx64 = L.mx;
+  const uint32_t* R = L.tab;
   const int lane = threadIdx.x & 63;
   const uint64_t len = m - s;
-  if (len < 64) return tail ^ g_tabs.zero_crc[len];
+  if (len < 64) return tail ^ L.zero_crc[len];
   const uint64_t k0 = s / TILE, k1 = m / TILE;
   const uint32_t j0 = (uint32_t)((s % TILE) / 64);
-  uint32_t acc = suf ^ g_tabs.winit[j0];
+  uint32_t acc = suf ^ L.winit[j0];
   uint32_t y;
   if (k0 == k1) {
     y = acc ^ sxm;
   } else {
     const uint64_t n = k1 - k0 - 1;  // whole tiles between
+    // the last tile's values first (needed at the end), then the lane's
+    // tiles 4 at a time: their loads issued together, then the Horner steps
+    // (a dependent load chain per tile took ~10 us per C3 entry)
+    const uint32_t e0 = tile[4 * k1], e2 = tile[4 * k1 + 2];
     uint32_t h = 0;
     uint64_t jl = 0;
     bool any = false;
-    for (uint64_t j = lane; j < n; j += 64) {
-      h = mulfix(h, mx64) ^ tile_T(tile, k0 + 1 + j);  // h * X^64 by byte tables (LDS)
-      jl = j;
-      any = true;
+    for (uint64_t jb = lane; jb < n; jb += 256) {
+      uint32_t t0[4], t2[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint64_t j = jb + 64 * q, k = k0 + 1 + (j < n ? j : 0);
+        t0[q] = tile[4 * k];
+        t2[q] = tile[4 * k + 2];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint64_t j = jb + 64 * q;
+        if (j < n) {
+          h = mulfix(h, mx64) ^ mulfix(t0[q], L.m16k) ^ t2[q];  // h * X^64 ^ tile_T(k0 + 1 + j)
+          jl = j;
+          any = true;
+        }
+      }
     }
-    uint32_t v = any ? mulp(g_tabs.xtile[n - 1 - jl], h) : 0u;  // n-1-jl < 64
+    uint32_t v = any ? mulp(L.xtile[n - 1 - jl], h) : 0u;  // n-1-jl < 64
     for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
     // acc * X^n ^ mid, then one more tile step into k1
-    const uint32_t xn = n < 64 * 65 ? mulp(g_tabs.xt64[n >> 6], g_tabs.xtile[n & 63]) : xpow8_any(n * (uint64_t)TILE);
-    acc = mulp(xn, acc) ^ v;
-    y = mulp(g_tabs.x32768, acc) ^ tile_T(tile, k1) ^ sxm;
+    const uint32_t xn = n < 64 * 65 ? mulp_wave(L.xt64[n >> 6], L.xtile[n & 63], R) : xpow8_any(n * (uint64_t)TILE);
+    acc = mulp_wave(xn, acc, R) ^ v;
+    y = mulp_wave(L.x32768, acc, R) ^ (mulfix(e0, L.m16k) ^ e2) ^ sxm;
   }
   const uint64_t dd = (k1 + 1) * TILE - m;
-  return ~(mulp(g_tabs.invpow[dd], y) ^ tail);
+  return ~(mulp_wave(L.invpow[dd], y, R) ^ tail);
 }
 
 // one wave per slow entry (a piece of the combine was not recorded, or the
@@ -1542,13 +1609,14 @@ constexpr int SLOW_WAVES = 4;
 // one wave: chain entry c's CRC from its recorded inputs (o_start / o_mo /
 // o_pieces / o_suf / o_sxm / o_tail), recomputing missing pieces from the
 // file.  tab, mx: the CRC and X^64 byte tables in LDS.
-__device__ void slow_one(const FinArgs& a, uint64_t c, const uint32_t* tab, const uint32_t* mx) {
+__device__ void slow_one(const FinArgs& a, uint64_t c, const SlowLds& L) {
+  const uint32_t* tab = L.tab;
   const uint64_t s = a.o_start[c], m = a.o_mo[c];
   const uint32_t pieces = a.o_pieces[c], tail = a.o_tail[c];
   uint32_t suf = a.o_suf[c], sxm = a.o_sxm[c];
   if (!(pieces & 1)) suf = tile_probe_sx(a.file, a.flen, s / TILE, (uint32_t)((s % TILE) / 64), tab);
   if (!(pieces & 2)) sxm = tile_probe_sx(a.file, a.flen, m / TILE, (uint32_t)((m % TILE) / 64), tab);
-  const uint32_t crc = crc_from_pieces_wave(s, m, suf, sxm, tail, a.tile, mx);
+  const uint32_t crc = crc_from_pieces_wave(s, m, suf, sxm, tail, a.tile, L);
   if ((threadIdx.x & 63) == 0) {
     a.o_crc[c] = crc;
     a.o_ok[c] = crc == a.o_crc_st[c];
@@ -1556,18 +1624,14 @@ __device__ void slow_one(const FinArgs& a, uint64_t c, const uint32_t* tab, cons
   }
 }
 __global__ __launch_bounds__(SLOW_WAVES * 64) void slow_kernel(FinArgs a) {
-  __shared__ uint32_t tab[1024];
-  __shared__ uint32_t mx[1024];
+  __shared__ SlowLds L;
   const unsigned long long ns = *a.n_slow;
   if ((uint64_t)blockIdx.x * SLOW_WAVES >= ns) return;
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-    tab[i] = g_tabs.tab[i >> 8][i & 255];
-    mx[i] = (&g_tabs.mx64[0][0])[i];
-  }
+  load_slow_lds(L);
   __syncthreads();
   for (uint64_t w = (uint64_t)blockIdx.x * SLOW_WAVES + (threadIdx.x >> 6); w < ns;
        w += (uint64_t)gridDim.x * SLOW_WAVES)
-    slow_one(a, a.slow_list[w], tab, mx);
+    slow_one(a, a.slow_list[w], L);
 }
 
 // --------------------------------------------------------------------------
