@@ -8,12 +8,12 @@
 //   scan            (srd_kernels.hip) strong candidates only, each wave's
 //                   records dense in its region (ScanPart), wave bases by the
 //                   scan's last block; block 0 zeroes the plan
-//   link2           4 lanes per span: node test of single-candidate records,
-//                   parent lookup (previous record, else a binary search in
-//                   the parent's span), 32-bit d_par / d_slot, and every node
-//                   claims its parent (the earliest claimer wins, claim_word);
-//                   zeroes the
-//                   index bucket fills
+//   link2           one block per scan wave over its dense record region:
+//                   node test of single-candidate records, parent lookup
+//                   (previous record, else a binary search in the parent's
+//                   span), 32-bit d_par / d_slot, and every node claims its
+//                   parent (the earliest claimer wins, claim_word); zeroes
+//                   the index bucket fills
 //   check           shape test from the claims alone: the core nodes (claimed
 //                   by someone, or the start node at file_len - 20) must form
 //                   ONE chain from the start down to a root -- each core node's
@@ -27,15 +27,17 @@
 //                   result.
 //   chain_finalize  plan (every block derives it, block 0 publishes), the chain
 //                   rank of each core node, the per-entry outputs and CRC from
-//                   the scan's pieces (slow entries by one wave each), and
-//                   KeyIndexer::build's bucket claims + scatter
-//   idx_dedup       one block per XXH3 bucket: marks the non-latest entries
+//                   the scan's pieces (entries that need a wave go to the
+//                   call's slow list), and KeyIndexer::build's bucket claims +
+//                   scatter
+//   idx_dedup       the slow list (one wave per entry), then one block per
+//                   XXH3 bucket: marks the non-latest entries
 //                   (generation bytes); none marked -> the index aliases
 //                   (o_kh, o_packed)
 //   idx_emit        compacts the latest entries in chain order (or nothing,
 //                   aliased) and publishes the outcome (PUB_WORDS) to the host
 //
-// Generation tags (gen:g in one u64, lgen bytes for the non-latest marks)
+// Generation tags (claim_word: gen and ~g in one u64; lgen bytes for the non-latest marks)
 // make the per-node marks self-invalidating between calls, so no per-call
 // memsets are needed.
 #pragma once
@@ -680,7 +682,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
                                                                       uint32_t log2_nbk) {
   __shared__ uint32_t wsum[CHAIN_WAVES * FIN_R];
   __shared__ FinLds lt;
-  __shared__ uint32_t mx[1024];
   uint32_t* const tab = lt.tab;
   __shared__ uint32_t slowq[CHAIN_THREADS * FIN_R];
   __shared__ uint32_t nslow;
@@ -690,7 +691,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   // loop after the plan)
   static_assert(CHAIN_THREADS == 1024, "one word of each 1024-word table per thread");
   const uint32_t ti = threadIdx.x;
-  const uint32_t r_tab = g_tabs.tab[ti >> 8][ti & 255], r_mx = (&g_tabs.mx64[0][0])[ti],
+  const uint32_t r_tab = g_tabs.tab[ti >> 8][ti & 255],
                  r_m16k = (&g_tabs.m16k[0][0])[ti];
   uint32_t r_inv[4];
 #pragma unroll
@@ -737,7 +738,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   if (st && !troot) return;
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
   tab[ti] = r_tab;
-  mx[ti] = r_mx;
   lt.m16k[ti] = r_m16k;
 #pragma unroll
   for (int j = 0; j < 4; j++) lt.invpow[ti + 1024 * j] = r_inv[j];

@@ -80,7 +80,7 @@ __device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]
 // spans.  Waves of one SIMD do not progress equally: the SIMD issues for
 // its oldest waves first, so with an even split waves 0-3 (the oldest on
 // each SIMD) finished ~15% before waves 12-15 (tools/wave_stamps.py); the
-// per-slot shares wq[v] (by default per age group, waves 4q..4q+3) even out
+// per-slot shares wq[v] (scan_weights: fitted to the wave stamps) even out
 // the finish times.
 struct ScanPart {
   uint64_t s_lo;   // first resident span
