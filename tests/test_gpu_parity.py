@@ -387,3 +387,37 @@ def test_timing_levels_do_not_change_results():
             c.set_timing(3)
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("weights", ["1,1,1,1", "3,0.3,1,2", "per-slot-random", "1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,8",
+                                     "not,numbers"])
+def test_scan_wave_shares(weights):
+    """The scan's wave partition (ScanPart, SRD_SCAN_WEIGHTS: 4 or 16 shares, read at srd_ctx_create): any
+    shares give the same outputs -- link2 finds each span's records through the inverse of the same
+    partition.  A store large enough for the full 256-block grid, several spans per wave."""
+    if weights == "per-slot-random":
+        rng = random.Random(7)
+        weights = ",".join(f"{rng.uniform(0.3, 3.0):.3f}" for _ in range(16))
+    old = os.environ.get("SRD_SCAN_WEIGHTS")
+    os.environ["SRD_SCAN_WEIGHTS"] = weights
+    try:
+        c = S.Context(0)
+    finally:
+        if old is None:
+            os.environ.pop("SRD_SCAN_WEIGHTS", None)
+        else:
+            os.environ["SRD_SCAN_WEIGHTS"] = old
+    try:
+        check_against_oracle(_shares_store(), c, 0, f"shares {weights}")
+    finally:
+        c.close()
+
+
+_SHARES_STORE = []
+
+
+def _shares_store():
+    # 50K x 4 KiB = 206 MB: 12.6K spans, the full 256-block grid, ~3 spans per scan wave
+    if not _SHARES_STORE:
+        _SHARES_STORE.append(O.synth_store(50000))
+    return _SHARES_STORE[0]
