@@ -249,7 +249,8 @@ typedef struct {
   uint32_t n_shards;
   uint32_t merged;        /* 1: the index is summary->index_* on ctxs[0] */
   uint32_t shard_errors;  /* shards whose first validation failed with an error */
-  uint32_t reserved;
+  uint32_t peer_errors;   /* cross-device copies between GPUs without peer access
+                             (hipDeviceEnablePeerAccess refused: staged by the runtime) */
   double validate_ms;     /* host wall time of the slowest shard's validation(s) */
   double exchange_ms;     /* index exchange + builds */
   double total_ms;        /* the whole call */

@@ -9,8 +9,12 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cmath>
+#include <condition_variable>
 #include <cstdio>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -82,6 +86,50 @@ struct CandCap {
   uint32_t floor;        // the default (a store of another size starts here again)
 };
 
+// A context's persistent host thread (the multi-GPU open runs each shard's
+// work on its context's worker: no thread spawn / join per phase).  One job
+// at a time; post() then wait().
+struct Worker {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool has = false, stop = false;
+  Worker() {
+    th = std::thread([this] {
+      std::unique_lock<std::mutex> lk(mu);
+      for (;;) {
+        cv.wait(lk, [this] { return has || stop; });
+        if (!has) return;  // stop
+        lk.unlock();
+        job();
+        lk.lock();
+        has = false;
+        job = nullptr;
+        cv.notify_all();
+      }
+    });
+  }
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+  void post(std::function<void()> f) {
+    std::lock_guard<std::mutex> lk(mu);
+    job = std::move(f);
+    has = true;
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return !has; });
+  }
+};
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -135,6 +183,12 @@ struct Ctx {
   void* h_out = nullptr;  // pinned host result arrays (srd_validate_index / _multi)
   uint64_t h_out_n = 0;
   uint8_t lgen = 0;  // generation of the index build's non-latest marks (B_LATEST8)
+  // multi-GPU open: the context's persistent host worker (created on first
+  // use) and the event every cross-context copy out of this context's memory
+  // waits on (recorded on `stream` once the data it reads is enqueued)
+  Worker* worker = nullptr;
+  hipEvent_t ev_ready = nullptr;
+  bool ready_recorded = false;
 };
 
 enum BufId {
@@ -419,16 +473,20 @@ static void scan_weights(uint32_t (&wq)[16]) {
   double f[16] = {1.0000, 0.9787, 0.9796, 0.9788, 0.9081, 0.9072, 0.9074, 0.8915,
                   0.8432, 0.8324, 0.8337, 0.8314, 0.7726, 0.7701, 0.7712, 0.7590};
   if (const char* e = getenv("SRD_SCAN_WEIGHTS")) {
-    double g[16];
+    // 4 or 16 finite positive values whose sum is finite; anything else
+    // (unparsable, 'inf', 'nan', an overflowing sum) keeps the defaults
+    double g[16], gs = 0;
     int n = 0;
     for (const char* q = e; n < 16 && *q;) {
       char* end = nullptr;
       const double x = strtod(q, &end);
-      if (end == q || !(x > 0)) { n = 0; break; }
+      if (end == q || !(x > 0) || !std::isfinite(x)) { n = 0; break; }
       g[n++] = x;
+      gs += x;
       q = *end == ',' ? end + 1 : end;
       if (*end && *end != ',') { n = 0; break; }
     }
+    if (!std::isfinite(gs)) n = 0;
     if (n == 4)
       for (int v = 0; v < 16; v++) f[v] = g[v / 4];
     else if (n == 16)
@@ -444,7 +502,11 @@ static void scan_weights(uint32_t (&wq)[16]) {
 extern "C" int srd_debug_set_scan_weights(srd_ctx* c, const double* w, int n) {
   if (!c || !w || (n != 4 && n != 16)) return SRD_ERR_ARG;
   double f[16], sum = 0;
-  for (int v = 0; v < 16; v++) sum += f[v] = n == 4 ? w[v / 4] : w[v];
+  for (int v = 0; v < 16; v++) {
+    sum += f[v] = n == 4 ? w[v / 4] : w[v];
+    if (!(f[v] > 0) || !std::isfinite(f[v])) return SRD_ERR_ARG;
+  }
+  if (!std::isfinite(sum)) return SRD_ERR_ARG;
   uint32_t used = 0;
   for (int v = 0; v < 15; v++) used += c->scan_wq[v] = (uint32_t)(65536.0 * f[v] / sum);
   c->scan_wq[15] = 65536 - used;
@@ -471,6 +533,7 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   // event's system-scope release (an L2 write-back) put ~5 us into the
   // timeline at each record (four per call)
   for (auto& e : c->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventReleaseToDevice));
+  HIPCHK(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
   HIPCHK(hipHostMalloc((void**)&c->h_plan, sizeof(Plan), hipHostMallocDefault));
   HIPCHK(hipHostMalloc((void**)&c->h_pub, 64, hipHostMallocCoherent));  // fine-grained: the device's system-scope stores land here
   memset(c->h_pub, 0, 64);
@@ -486,7 +549,9 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
 
 extern "C" void srd_ctx_destroy(srd_ctx* c) {
   if (!c) return;
+  delete c->worker;  // idle between calls: joins at once
   hipSetDevice(c->device);
+  if (c->ev_ready) hipEventDestroy(c->ev_ready);
   for (auto& b : c->bufs)
     if (b.p) hipFree(b.p);
   if (c->file.p) hipFree(c->file.p);
@@ -1810,16 +1875,31 @@ extern "C" int srd_ctx_stage_info(srd_ctx* c, int* mode, double* stage_ms) {
 // shard indexes instead and builds the one merged index.
 // srd_validate_index_multi (host input) stages the spans and calls the same
 // implementation with the merged index, then copies the result to the host.
-static void enable_peer(int dev0, int dev) {
+//
+// Peer access of device dev0 to dev's memory, enabled once per pair and
+// process.  Returns false when it cannot be enabled (no xGMI path, or the
+// runtime refused): hipMemcpyPeerAsync still works then, staged through host
+// memory, and the call counts the pair in srd_multi_summary::peer_errors.
+static bool enable_peer(int dev0, int dev) {
   static std::mutex mu;
-  static uint64_t done[64] = {};
-  if (dev0 == dev || dev0 >= 64 || dev >= 64) return;
+  static uint8_t state[64][64] = {};  // 0 not tried, 1 enabled, 2 failed
+  if (dev0 == dev) return true;
+  if (dev0 < 0 || dev < 0 || dev0 >= 64 || dev >= 64) return false;
   std::lock_guard<std::mutex> lk(mu);
-  if (done[dev0] & (1ull << dev)) return;
-  int can = 0;
-  if (hipDeviceCanAccessPeer(&can, dev0, dev) == hipSuccess && can) (void)hipDeviceEnablePeerAccess(dev, 0);
-  (void)hipGetLastError();  // already enabled / unsupported: copies still work (staged)
-  done[dev0] |= 1ull << dev;
+  if (!state[dev0][dev]) {
+    int can = 0, cur = 0;
+    bool ok = hipDeviceCanAccessPeer(&can, dev0, dev) == hipSuccess && can;
+    if (ok && hipGetDevice(&cur) == hipSuccess && hipSetDevice(dev0) == hipSuccess) {
+      const hipError_t e = hipDeviceEnablePeerAccess(dev, 0);
+      ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+      (void)hipSetDevice(cur);
+    } else {
+      ok = false;
+    }
+    (void)hipGetLastError();
+    state[dev0][dev] = ok ? 1 : 2;
+  }
+  return state[dev0][dev] == 1;
 }
 
 // the same context twice would be driven by two host threads at once (its
@@ -1834,21 +1914,41 @@ static int check_ctxs(srd_ctx* const* ctxs, uint32_t nc) {
   return 0;
 }
 
-template <class F>
-static void parallel_for(uint32_t n, F&& f) {
-  std::vector<std::thread> th;
-  th.reserve(n);
-  for (uint32_t i = 1; i < n; i++) th.emplace_back(f, i);
+// Task i of n runs on the persistent worker of context on(i) (task 0 on the
+// calling thread); the contexts of one call are distinct (check_ctxs), so no
+// worker gets two tasks.  Replaces a std::thread per task per phase.
+template <class On, class F>
+static void parallel_for(uint32_t n, On&& on, F&& f) {
+  for (uint32_t i = 1; i < n; i++) {
+    Ctx* c = on(i);
+    if (!c->worker) c->worker = new Worker();
+    c->worker->post([&f, i] { f(i); });
+  }
   if (n) f(0);
-  for (auto& t : th) t.join();
+  for (uint32_t i = 1; i < n; i++) on(i)->worker->wait();
+}
+
+// Record, on the context's stream, that the device data a later cross-
+// context copy will read is enqueued (the copy's stream waits on it)
+static hipError_t mark_ready(Ctx* c) {
+  const hipError_t e = hipEventRecord(c->ev_ready, c->stream);
+  c->ready_recorded = e == hipSuccess;
+  return e;
 }
 
 // device copy into dst's memory on dst's stream (peer copy over xGMI when the
-// source lives on another GPU)
-static hipError_t copy_to(Ctx* dst, void* d, const Ctx* src, const void* s, uint64_t bytes) {
+// source lives on another GPU), ordered after the source context's last
+// mark_ready by an explicit event wait on dst's stream; *peer_fail counts the
+// copies between devices without peer access (staged by the runtime)
+static hipError_t copy_to(Ctx* dst, void* d, const Ctx* src, const void* s, uint64_t bytes,
+                          std::atomic<uint32_t>* peer_fail) {
   if (!bytes) return hipSuccess;
+  if (src != dst && src->ready_recorded) {
+    const hipError_t e = hipStreamWaitEvent(dst->stream, src->ev_ready, 0);
+    if (e != hipSuccess) return e;
+  }
   if (src->device == dst->device) return hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, dst->stream);
-  enable_peer(dst->device, src->device);
+  if (!enable_peer(dst->device, src->device) && peer_fail) peer_fail->fetch_add(1);
   return hipMemcpyPeerAsync(d, dst->device, s, src->device, bytes, dst->stream);
 }
 
@@ -1864,6 +1964,7 @@ struct MultiIn {
   const uint64_t* soff;
   const uint64_t* cuts;        // [nc + 1]: shard i holds [soff[i], cuts[i + 1]) when cuts[i] < cuts[i + 1]
   uint64_t flen;
+  std::atomic<uint32_t>* peer_fail;  // copies between devices without peer access
 };
 
 // file bytes [x, y) assembled in dst's B_GATHER buffer from the shards whose
@@ -1882,7 +1983,7 @@ static int gather_range(Ctx* dst, const MultiIn& in, uint64_t x, uint64_t y, con
       }
     if (best < 0) { set_err("internal: no shard holds file byte " + std::to_string(pos)); return SRD_ERR_INTERNAL; }
     const uint64_t e = std::min(y, reach);
-    HIPCHK(copy_to(dst, d + (pos - x), in.ctxs[best], in.span[best] + (pos - in.soff[best]), e - pos));
+    HIPCHK(copy_to(dst, d + (pos - x), in.ctxs[best], in.span[best] + (pos - in.soff[best]), e - pos, in.peer_fail));
     pos = e;
   }
   *out = d;
@@ -1929,6 +2030,7 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
     TRY(ensure(c, B_XVAL, std::max<uint64_t>(n, 1) * 8));
     if (n) TRY(partition_impl(c, s.r.index_key_hash, s.r.index_packed, n, nc, P<uint64_t>(c, B_XKEY), P<uint64_t>(c, B_XVAL), s.cnt));
     s.parted = true;
+    HIPCHK(mark_ready(c));  // the owners' pulls wait on it
     return 0;
   };
   auto validate = [&](uint32_t i, const uint8_t* d, uint64_t soff, uint64_t lo, uint64_t hi) {
@@ -1941,6 +2043,8 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
     if (!s.rc) {
       s.proven = s.r.final_len == hi && s.r.mode != SRD_MODE_SPAN_UNPROVEN;
       if (s.proven) s.rc = part(i);
+      // the merged gather reads the shard's result arrays from another stream
+      if (!s.rc && mark_ready(c) != hipSuccess) { set_err("hipEventRecord"); s.rc = SRD_ERR_HIP; }
     }
     if (s.rc) s.err = g_err;
     vms[i] += ms_since(t0);
@@ -1958,7 +2062,11 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
       }
   };
 
-  parallel_for(nc, [&](uint32_t i) { validate(i, in.span[i], in.soff[i], cuts[i], cuts[i + 1]); });
+  const auto on = [&](uint32_t i) -> Ctx* { return in.ctxs[i]; };
+  parallel_for(nc, on, [&](uint32_t i) {
+    if (hipSetDevice(in.ctxs[i]->device) != hipSuccess) { sh[i] = MShard{}; sh[i].rc = SRD_ERR_HIP; sh[i].err = "hipSetDevice"; return; }
+    validate(i, in.span[i], in.soff[i], cuts[i], cuts[i + 1]);
+  });
   bool composed = composes();
   note_errors();
   // shard 0 over the whole store IS the whole-file path (lo = 0)
@@ -1982,7 +2090,14 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
       // "proves" nothing; its cut may be the forged one)
       uint32_t a = i ? i - 1 : 0;
       while (a > floor && cuts[a] == cuts[a + 1]) a--;
-      runs.emplace_back(std::max(a, floor), b);
+      if (!runs.empty() && a <= floor && cuts[a] == cuts[a + 1]) {
+        // the walk reached the previous run through empty shards only: no
+        // shard between proves a tail, so this run joins the previous one
+        // (two runs would both start or end at the suspect cut)
+        runs.back().second = b;
+      } else {
+        runs.emplace_back(std::max(a, floor), b);
+      }
       floor = b + 1;
       i = b;
     }
@@ -1992,7 +2107,7 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
         sh[i] = MShard{};
         sh[i].proven = true;
       }
-    parallel_for((uint32_t)runs.size(), [&](uint32_t k) {
+    parallel_for((uint32_t)runs.size(), [&](uint32_t k) -> Ctx* { return in.ctxs[runs[k].first]; }, [&](uint32_t k) {
       const uint32_t a = runs[k].first;
       const uint64_t lo = cuts[a], hi = cuts[a + 1], x = lo - lo % SPAN_BYTES;
       const uint8_t* d = nullptr;
@@ -2067,8 +2182,8 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
     uint64_t acc = 0;
     for (uint32_t s = 0; s < nc && !r; s++) {
       const uint64_t n = sh[s].r.n_index;
-      if (copy_to(c0, P<uint64_t>(c0, B_GKEY) + acc, in.ctxs[s], sh[s].r.index_key_hash, n * 8) != hipSuccess ||
-          copy_to(c0, P<uint64_t>(c0, B_GVAL) + acc, in.ctxs[s], sh[s].r.index_packed, n * 8) != hipSuccess) {
+      if (copy_to(c0, P<uint64_t>(c0, B_GKEY) + acc, in.ctxs[s], sh[s].r.index_key_hash, n * 8, in.peer_fail) != hipSuccess ||
+          copy_to(c0, P<uint64_t>(c0, B_GVAL) + acc, in.ctxs[s], sh[s].r.index_packed, n * 8, in.peer_fail) != hipSuccess) {
         set_err("index gather: peer copy failed");
         r = SRD_ERR_HIP;
       }
@@ -2081,13 +2196,13 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
     mpacked = P<uint64_t>(c0, B_GOPACKED);
   } else {
     // by owner: the shards re-validated above partition now
-    parallel_for(nc, [&](uint32_t i) {
+    parallel_for(nc, on, [&](uint32_t i) {
       if (hipSetDevice(in.ctxs[i]->device) != hipSuccess) { erc[i] = SRD_ERR_HIP; return; }
       if ((erc[i] = part(i))) eerr[i] = g_err;
     });
     for (uint32_t i = 0; i < nc; i++)
       if (erc[i]) { set_err(eerr[i]); return erc[i]; }
-    parallel_for(nc, [&](uint32_t p) {
+    parallel_for(nc, on, [&](uint32_t p) {
       Ctx* c = in.ctxs[p];
       int& r = erc[p];
       if (hipSetDevice(c->device) != hipSuccess) { r = SRD_ERR_HIP; eerr[p] = "hipSetDevice"; return; }
@@ -2104,8 +2219,8 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
         for (uint32_t q = 0; q < p; q++) off += sh[s].cnt[q];
         const uint64_t n = sh[s].cnt[p];
         Ctx* cs = in.ctxs[s];
-        if (copy_to(c, P<uint64_t>(c, B_GKEY) + acc, cs, P<uint64_t>(cs, B_XKEY) + off, n * 8) != hipSuccess ||
-            copy_to(c, P<uint64_t>(c, B_GVAL) + acc, cs, P<uint64_t>(cs, B_XVAL) + off, n * 8) != hipSuccess) {
+        if (copy_to(c, P<uint64_t>(c, B_GKEY) + acc, cs, P<uint64_t>(cs, B_XKEY) + off, n * 8, in.peer_fail) != hipSuccess ||
+            copy_to(c, P<uint64_t>(c, B_GVAL) + acc, cs, P<uint64_t>(cs, B_XVAL) + off, n * 8, in.peer_fail) != hipSuccess) {
           set_err("index exchange: peer copy failed");
           r = SRD_ERR_HIP;
         }
@@ -2155,6 +2270,7 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
   S.n_shards = nc;
   S.merged = (merged || nc == 1) ? 1u : 0u;
   S.shard_errors = n_err;
+  S.peer_errors = in.peer_fail ? in.peer_fail->load() : 0u;
   for (double v : vms) S.validate_ms = std::max(S.validate_ms, v);
   S.exchange_ms = ex_ms;
   S.total_ms = ms_since(t_call);
@@ -2179,7 +2295,8 @@ extern "C" int srd_validate_index_multi_device(srd_ctx* const* ctxs, uint32_t nc
       return SRD_ERR_ARG;
     }
   }
-  MultiIn in{ctxs, nc, d_spans, span_offs, cuts, flen};
+  std::atomic<uint32_t> peer_fail{0};
+  MultiIn in{ctxs, nc, d_spans, span_offs, cuts, flen, &peer_fail};
   return multi_device_impl(in, flags, shards, summary);
 }
 
@@ -2222,7 +2339,8 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
   std::vector<const uint8_t*> span(nc, nullptr);
   std::vector<int> rc(nc, 0);
   std::vector<std::string> err(nc);
-  parallel_for(nc, [&](uint32_t i) {
+  const auto on = [&](uint32_t i) -> Ctx* { return ctxs[i]; };
+  parallel_for(nc, on, [&](uint32_t i) {
     srd_ctx* c = ctxs[i];
     const uint64_t lo = cuts[i], hi = cuts[i + 1];
     if (lo == hi) return;
@@ -2240,7 +2358,8 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
     if (rc[i]) { set_err(err[i]); return rc[i]; }
   std::vector<srd_device_result> sr(nc);
   srd_multi_summary sum{};
-  MultiIn in{ctxs, nc, span.data(), soff.data(), cuts.data(), flen};
+  std::atomic<uint32_t> peer_fail{0};
+  MultiIn in{ctxs, nc, span.data(), soff.data(), cuts.data(), flen, &peer_fail};
   TRY(multi_device_impl(in, (flags & ~kStageFlags) | SRD_FLAG_MERGE_INDEX, sr.data(), &sum));
 
   memset(out, 0, sizeof *out);
@@ -2250,7 +2369,7 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
   // index from ctxs[0]
   std::vector<uint64_t> cb(nc, 0);
   for (uint32_t i = 1; i < nc; i++) cb[i] = cb[i - 1] + sr[i - 1].n_chain;
-  parallel_for(nc, [&](uint32_t i) {
+  parallel_for(nc, on, [&](uint32_t i) {
     srd_ctx* c = ctxs[i];
     const uint64_t nk = i == 0 ? sum.n_index : 0;
     if (!sr[i].n_chain && !nk) return;

@@ -81,7 +81,7 @@ class MultiSummary(C.Structure):
         ("file_len", C.c_uint64), ("final_len", C.c_uint64), ("n_chain", C.c_uint64),
         ("n_index", C.c_uint64), ("n_crc_bad", C.c_uint64), ("n_candidates", C.c_uint64),
         ("mode", C.c_uint32), ("path", C.c_uint32), ("n_shards", C.c_uint32), ("merged", C.c_uint32),
-        ("shard_errors", C.c_uint32), ("reserved", C.c_uint32),
+        ("shard_errors", C.c_uint32), ("peer_errors", C.c_uint32),
         ("validate_ms", C.c_double), ("exchange_ms", C.c_double), ("total_ms", C.c_double),
         ("index_key_hash", C.c_void_p), ("index_packed", C.c_void_p),
     ]

@@ -165,7 +165,13 @@ def neighbour_runs(proven: list[bool], cuts: list[int]) -> list[tuple[int, int]]
         a = i - 1 if i else 0
         while a > floor and cuts[a] == cuts[a + 1]:
             a -= 1
-        runs.append((max(a, floor), b))
+        if runs and a <= floor and cuts[a] == cuts[a + 1]:
+            # only empty shards back to the previous run: no tail between them
+            # is proven, so this run joins that one (both would otherwise end
+            # or start at the suspect cut)
+            runs[-1] = (runs[-1][0], b)
+        else:
+            runs.append((max(a, floor), b))
         floor = b + 1
         i = b + 1
     return runs
@@ -248,11 +254,14 @@ def _retry_with_neighbours(backend, buf, span_off, lo, hi, file_len, group, prov
     dev = buf.device
     cd = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
     runs = neighbour_runs(proven, cuts)
+    # send / recv take GLOBAL ranks; the run plan speaks of ranks in `group`
+    glob = (lambda r: r) if group is None or group is dist.group.WORLD else (
+        lambda r: dist.get_global_rank(group, r))
     n_lo, n_hi, n_buf, n_off = lo, hi, buf, span_off
     for a, b in runs:
         if a < me <= b:  # a sender: its bytes go to rank a, its shard empties
             if hi > lo:
-                dist.send(buf[lo - span_off: hi - span_off].contiguous().to(cd), a, group=group)
+                dist.send(buf[lo - span_off: hi - span_off].contiguous().to(cd), glob(a), group=group)
             n_lo = n_hi = cuts[b + 1]
             n_buf = torch.empty(0, dtype=torch.uint8, device=dev)
             n_off = n_lo - n_lo % S.SPAN_ALIGN
@@ -261,14 +270,15 @@ def _retry_with_neighbours(backend, buf, span_off, lo, hi, file_len, group, prov
             for i in range(a + 1, b + 1):
                 if cuts[i + 1] > cuts[i]:
                     t = torch.empty(cuts[i + 1] - cuts[i], dtype=torch.uint8, device=cd)
-                    dist.recv(t, i, group=group)
+                    dist.recv(t, glob(i), group=group)
                     parts.append(t.to(dev))
             n_lo = cuts[a]
             n_hi = cuts[b + 1]
-            n_off = n_lo - n_lo % S.SPAN_ALIGN
-            # the merged bytes start at the neighbour's span, or -- an empty
+            # the merged bytes start at the neighbour's span (any 16 KiB
+            # multiple <= lo: the span keeps its offset), or -- an empty
             # neighbour -- at its cut (the bytes below a shard's lower tail
             # are never read as entries: zeros are fine there)
+            n_off = span_off if hi > lo else n_lo - n_lo % S.SPAN_ALIGN
             start = span_off if hi > lo else cuts[a + 1]
             merged = torch.cat([p.reshape(-1) for p in parts])
             n_buf = torch.zeros(S.padded_size(n_hi - n_off) if n_hi > n_lo else 1, dtype=torch.uint8, device=dev)

@@ -45,7 +45,7 @@ int main(int argc, char **argv) {
     F(srd_multi_summary, file_len); F(srd_multi_summary, final_len); F(srd_multi_summary, n_chain);
     F(srd_multi_summary, n_index); F(srd_multi_summary, n_crc_bad); F(srd_multi_summary, n_candidates);
     F(srd_multi_summary, mode); F(srd_multi_summary, path); F(srd_multi_summary, n_shards);
-    F(srd_multi_summary, merged); F(srd_multi_summary, shard_errors); F(srd_multi_summary, reserved);
+    F(srd_multi_summary, merged); F(srd_multi_summary, shard_errors); F(srd_multi_summary, peer_errors);
     F(srd_multi_summary, validate_ms); F(srd_multi_summary, exchange_ms); F(srd_multi_summary, total_ms);
     F(srd_multi_summary, index_key_hash); F(srd_multi_summary, index_packed);
     printf("\"sizeof(srd_result)\": %zu, \"sizeof(srd_write_entry)\": %zu, \"sizeof(srd_multi_summary)\": %zu}\n",

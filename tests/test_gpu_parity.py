@@ -390,7 +390,7 @@ def test_timing_levels_do_not_change_results():
 
 
 @pytest.mark.parametrize("weights", ["1,1,1,1", "3,0.3,1,2", "per-slot-random", "1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,8",
-                                     "not,numbers"])
+                                     "not,numbers", "inf,1,1,1", "nan,1,1,1", "1e308,1e308,1e308,1e308"])
 def test_scan_wave_shares(weights):
     """The scan's wave partition (ScanPart, SRD_SCAN_WEIGHTS: 4 or 16 shares, read at srd_ctx_create): any
     shares give the same outputs -- link2 finds each span's records through the inverse of the same

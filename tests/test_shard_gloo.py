@@ -286,9 +286,67 @@ def test_fake_tail_cut_is_refuted():
     ([False, True], [0, 5, 9], [(0, 0)]),
     ([True, True, False, False, True], [0, 1, 2, 3, 4, 5], [(1, 3)]),
     ([True, True, False], [0, 4, 4, 9], [(0, 2)]),  # the empty shard 1 is skipped
-    ([False, True, False], [0, 4, 4, 9], [(0, 0), (1, 2)]),  # the floor stops at the previous run's end
+    ([False, True, False], [0, 4, 4, 9], [(0, 2)]),  # only an empty shard between two runs: they merge
+    ([False, True, False], [0, 4, 6, 9], [(0, 0), (1, 2)]),  # a non-empty proven shard between: two runs
 ])
 def test_neighbour_runs(proven, cuts, want):
     sys.path[:0] = [os.path.join(ROOT, "rust-simd-r-drive_amd")]
     import srd_shard as SH
     assert SH.neighbour_runs(proven, cuts) == want
+
+
+def _forged_worker(rank, world, port, store_bytes, q, lower, members):
+    """sharded_validate_index on the forged-cut store over the ranks `members`
+    (a subgroup of the world; the others only join new_group), each member's
+    span starting `lower` alignment steps below span_of(lo)."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "rust-simd-r-drive_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = dist.new_group(members)
+        if rank in members:
+            import srd_amd as S
+            import srd_shard as SH
+            store = np.frombuffer(store_bytes, np.uint8)
+            gr = dist.get_rank(g)
+            lo, hi = SH.plan_byte_shards(store, len(members))[gr]
+            span_off = max(0, SH.span_of(lo) - lower * S.SPAN_ALIGN)
+            buf = torch.zeros(S.padded_size(hi - span_off) if hi > lo else 1, dtype=torch.uint8)
+            if hi > lo:
+                buf[: hi - span_off].copy_(torch.from_numpy(store[span_off:hi].copy()))
+            res = SH.sharded_validate_index(OracleBackend(store), buf, span_off, lo, hi, int(store.size), g)
+            q.put((gr, res.composed, res.retried, res.final_len, res.n_index,
+                   dict(zip(res.owner_keys.numpy().view(np.uint64).tolist(),
+                            res.owner_packed.numpy().view(np.uint64).tolist()))))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,members,lower", [(6, [0, 1, 2, 3, 4, 5], 1), (3, [1, 2], 0)])
+def test_neighbour_retry_lower_span_and_subgroup(world, members, lower):
+    """The retry with the lower neighbour (a forged cut) when the neighbour's
+    span starts below span_of(lo) (any 16 KiB multiple <= lo is allowed), and
+    inside a process subgroup (send / recv address global ranks).  Six
+    shards: the forged cut is cut 3, shards 2 and 3 (ending / starting at it)
+    are unproven, and the neighbour is shard 1, whose span lies above 0."""
+    import oracle as O
+    store, _ = fake_cut_store()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_forged_worker, args=(r, world, port, store.tobytes(), q, lower, members))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in members)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    want = O.key_indexer_build(store, store.size)
+    merged = {}
+    for gr, composed, retried, final_len, n_index, idx in out:
+        assert composed and retried and final_len == store.size and n_index == len(want)
+        assert not (merged.keys() & idx.keys())
+        merged.update(idx)
+    assert merged == want
