@@ -41,6 +41,7 @@ import torch  # noqa: E402
 import srd_amd as S  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SCAN_SAMPLE = 4  # event-stamp every 4th scan launch (roofline.kernel_ms)
 
 
 def kernel_sources_hash() -> str:
@@ -426,10 +427,13 @@ def main():
     devs = [local if same_dev else local + i for i in range(world)]
     torch.cuda.set_device(local)
     ctx = S.Context(local)
-    # the roofline's kernel time: HIP events around each scan launch on the
-    # library's stream, inside the timed region (the product default is no
-    # events: each record costs ~10 us of a call)
+    # the roofline's kernel time: HIP events stamped by the scan dispatch on
+    # the library's stream, inside the timed region, on every SCAN_SAMPLE-th
+    # launch (an event-stamped launch costs ~7 us more wall time than a plain
+    # one: a systematic sample keeps that off the other steps; the product
+    # default is no events)
     ctx.set_timing(S.TIMING_SCAN)
+    ctx.set_timing_every(SCAN_SAMPLE)
 
     if args.config == "c5":
         return bench_c5(args, ctx, local)
@@ -467,6 +471,7 @@ def main():
         ctxs = [ctx] + [S.Context(d) for d in devs[1:]]
         for c in ctxs:
             c.set_timing(S.TIMING_SCAN)
+            c.set_timing_every(SCAN_SAMPLE)
         spans, soffs, cuts, keep = [], [], [0], []
         for i, (first, cnt) in enumerate(SH.plan_entry_shards(n * world, world)):
             lo, hi = S.synth_span(None, 0, first, cnt, L, lens)
@@ -516,6 +521,7 @@ def main():
     # launch since its previous call)
     for c in (ctxs if multi is not None else [ctx]):
         c.timings()
+        c.set_timing_every(SCAN_SAMPLE)  # restarts the sample: timed steps 0, SCAN_SAMPLE, 2 SCAN_SAMPLE, ...
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -527,16 +533,15 @@ def main():
         torch.cuda.synchronize(d)
     dt = time.perf_counter() - t0
     scan_ms_sum, scan_n, _ = ctx.timings()
+    scan_each = sorted(ctx.scan_list())  # the sampled timed steps' scan durations (ms), one per launch
     if multi is not None:
-        multi["scan_ms"] = [scan_ms_sum] + [c.timings()[0] for c in ctxs[1:]]
+        multi["scan_ms"] = [(scan_ms_sum, scan_n)] + [c.timings()[:2] for c in ctxs[1:]]
 
     ms_per_step = dt / args.steps * 1e3
     value = bytes_total / dt * args.steps / 2**30
-    scan_ms = scan_ms_sum / max(scan_n, 1)
-    if full:  # the full pass's scan (one per step)
-        scan_ms = scan_ms_sum / args.steps
+    scan_ms = scan_ms_sum / max(scan_n, 1)  # (the full pass too: one scan per call)
     if multi is not None:  # the slowest shard's scan bounds the step
-        shard_scan = [x / max(multi["n"], 1) for x in multi["scan_ms"]]
+        shard_scan = [x / max(k, 1) for x, k in multi["scan_ms"]]
         scan_ms = max(shard_scan)
     achieved = bytes_alg / (scan_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
@@ -566,7 +571,9 @@ def main():
         "dtype": "u8",
         "data": "synthetic (counter-mode splitmix64 payloads, keys bench-key-{i}), generated in HBM",
         "config": {
-            "workload": (f"{args.config.upper()}: {n} x " + (f"{L} B" if lens is None else "Zipf 64 B..1 MiB") +
+            "workload": (("C4 partition at N=1 (the weak-scaling base: 2^21 x 4 KiB per GPU, as at N = 2/4/8)"
+                          if args.config == "c2" and n == 1 << 21 and L == 4096 else args.config.upper()) +
+                         f": {n} x " + (f"{L} B" if lens is None else "Zipf 64 B..1 MiB") +
                          f" entries, {size} B store" + (" + the 7-byte torn tail b'CORRUPT' (recovered: final_len = "
                                                         f"{size}, the optimistic pass from the start tail 7 bytes "
                                                         "below file_len)" if torn else "") +
@@ -590,8 +597,13 @@ def main():
             "bound": "hbm",
             "kernel": "scan_kernel<true> (the full pass)" if full else "scan_kernel<false>",
             "kernel_ms": round(scan_ms, 4),
+            # the distribution behind the mean (rocprof's kernel_stats for the same command: profiles/)
+            "kernel_ms_min": round(scan_each[0], 4) if scan_each else None,
+            "kernel_ms_median": round(scan_each[len(scan_each) // 2], 4) if scan_each else None,
+            "kernel_launches": len(scan_each),
             "kernel_timing": "HIP events stamped with the scan dispatch's own start / stop (hipExtLaunchKernel) "
-                             "on the library stream, every timed step (read out after the timed region)",
+                             f"on the library stream, every {SCAN_SAMPLE}th timed step (a systematic sample: a "
+                             "stamped launch costs ~7 us more wall time; read out after the timed region)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -88,6 +88,10 @@ const char *srd_last_error(void);
 #define SRD_TIMING_SCAN 1
 #define SRD_TIMING_CALL 2
 int srd_ctx_set_timing(srd_ctx *ctx, int level);
+/* With SRD_TIMING_SCAN: stamp only every n-th scan launch (n >= 1; 1 = every
+ * launch, the default).  The event-stamped launch costs ~7 us more wall time
+ * than a plain one; a systematic sample keeps that off most calls. */
+int srd_ctx_set_timing_every(srd_ctx *ctx, int n);
 
 /* HIP-event timings on the context stream: the summed duration (ms) and the
  * count of the streaming scan kernel launches of every validate call since the
@@ -96,6 +100,10 @@ int srd_ctx_set_timing(srd_ctx *ctx, int level);
  * timing level includes them). */
 int srd_ctx_timings(srd_ctx *ctx, double *scan_ms, int *scan_launches,
                     double *total_ms);
+/* The individual scan durations (ms) summed by the last srd_ctx_timings
+ * read, in launch order: copies up to cap of them to out and returns how
+ * many there were (< 0: error). */
+int srd_ctx_scan_list(srd_ctx *ctx, float *out, int cap);
 
 /* Result of one validate+index pass whose arrays live in DEVICE memory owned
  * by the context (valid until the next call on the same ctx). */

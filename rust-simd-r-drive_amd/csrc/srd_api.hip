@@ -142,6 +142,7 @@ struct Ctx {
   CandCap cfull{32, 32, 0, 32};
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
   uint32_t scan_wq[16] = {};  // ScanPart::wq (scan_weights())
+  uint32_t scan_variant = 0;  // ScanArgs::variant (srd_debug_set_scan_variant)
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -158,6 +159,10 @@ struct Ctx {
   uint32_t sev_next = 0, sev_pending = 0;  // next pair, pairs not yet read out
   double scan_ms = 0, total_ms = 0;  // scan_ms / scan_launches: since the last srd_ctx_timings
   int scan_launches = 0;
+  uint32_t timing_every = 1, timing_seq = 0;  // srd_ctx_set_timing_every
+  // the individual scan durations behind scan_ms (scan_list), and those of
+  // the last srd_ctx_timings read (scan_last: srd_ctx_scan_list)
+  std::vector<float> scan_list, scan_last;
   // sync-free optimistic pass
   uint64_t capK = 0;    // dense candidate capacity (grows on ST_CAPK)
   uint32_t gen = 0;     // generation tag of has_child / childof
@@ -329,6 +334,26 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
     (void)hipEventRecord(e0, s);
     launch_scan<FULL>(g, a, s);
     (void)hipEventRecord(e1, s);
+#ifdef SRD_DEBUG_API
+  } else if (a.variant == 1) {  // A/B variants (scan_kernel's V) inside one context
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 1>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 1>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 2) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 2>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 2>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 3) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 3>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 3>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 4) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 4>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 4>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 5) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 5>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 5>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 6) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 6>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 6>, grid, block, 0, s, e0, e1, 0, a);
+#endif
   } else if (e0) {
     if (a.flen > kWide)
       hipExtLaunchKernelGGL(scan_kernel<FULL, true>, grid, block, 0, s, e0, e1, 0, a);
@@ -498,7 +523,12 @@ static void scan_weights(uint32_t (&wq)[16]) {
   for (int v = 0; v < 15; v++) used += wq[v] = (uint32_t)(65536.0 * f[v] / sum);
   wq[15] = 65536 - used;
 }
-#ifdef SRD_DEBUG_API  // timing builds: A/B of scan partitions inside one context (one workspace)
+#ifdef SRD_DEBUG_API  // timing builds: A/B of scan variants inside one context (one workspace)
+extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
+  if (!c || v < 0 || v > 6) return SRD_ERR_ARG;
+  c->scan_variant = (uint32_t)v;
+  return 0;
+}
 extern "C" int srd_debug_set_scan_weights(srd_ctx* c, const double* w, int n) {
   if (!c || !w || (n != 4 && n != 16)) return SRD_ERR_ARG;
   double f[16], sum = 0;
@@ -822,6 +852,7 @@ static int drain_scan_events(Ctx* c, uint32_t n) {
     HIPCHK(hipEventElapsedTime(&ms, c->sev[2 * i], c->sev[2 * i + 1]));
     c->scan_ms += ms;
     c->scan_launches++;
+    if (c->scan_list.size() < (1u << 16)) c->scan_list.push_back(ms);
     c->sev_pending--;
   }
   return 0;
@@ -830,6 +861,7 @@ static int drain_scan_events(Ctx* c, uint32_t n) {
 static int next_scan_events(Ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
   *e0 = *e1 = nullptr;
   if (c->timing < SRD_TIMING_SCAN) return 0;
+  if (c->timing_seq++ % c->timing_every) return 0;  // srd_ctx_set_timing_every: a sampled launch only
   if (c->sev_pending == Ctx::kScanRing) TRY(drain_scan_events(c, 1));
   const uint32_t i = c->sev_next++ % Ctx::kScanRing;
   c->sev_pending++;
@@ -850,6 +882,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     // the scan writes every span's count; only the scan sentinel needs a zero
     HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT) + n_spans, 0, 4, c->stream));
     ScanArgs a{};
+    a.variant = c->scan_variant;
     a.file = d_file;
     a.flen = flen;
     a.n_tiles = n_tiles;
@@ -1097,6 +1130,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     // per-tile / per-span arrays hold the resident range only: their base
     // pointers are shifted so kernels index them by absolute tile / span
     ScanArgs a{};
+    a.variant = c->scan_variant;
     a.part = part;
     a.file = d_file;
     a.flen = flen;
@@ -1468,6 +1502,13 @@ extern "C" int srd_ctx_set_timing(srd_ctx* c, int level) {
   return 0;
 }
 
+extern "C" int srd_ctx_set_timing_every(srd_ctx* c, int n) {
+  if (!c || n < 1) { set_err("bad argument"); return SRD_ERR_ARG; }
+  c->timing_every = (uint32_t)n;
+  c->timing_seq = 0;
+  return 0;
+}
+
 extern "C" int srd_ctx_timings(srd_ctx* c, double* scan_ms, int* scan_launches, double* total_ms) {
   if (!c) { set_err("bad argument"); return SRD_ERR_ARG; }
   HIPCHK(hipSetDevice(c->device));
@@ -1477,7 +1518,16 @@ extern "C" int srd_ctx_timings(srd_ctx* c, double* scan_ms, int* scan_launches, 
   if (total_ms) *total_ms = c->total_ms;
   c->scan_ms = 0;
   c->scan_launches = 0;
+  c->scan_last.swap(c->scan_list);
+  c->scan_list.clear();
   return 0;
+}
+
+extern "C" int srd_ctx_scan_list(srd_ctx* c, float* out, int cap) {
+  if (!c || (cap > 0 && !out)) { set_err("bad argument"); return SRD_ERR_ARG; }
+  const int n = (int)std::min<size_t>(c->scan_last.size(), (size_t)std::max(cap, 0));
+  for (int i = 0; i < n; i++) out[i] = c->scan_last[i];
+  return (int)c->scan_last.size();
 }
 
 static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen, uint32_t flags,

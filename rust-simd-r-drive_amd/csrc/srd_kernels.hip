@@ -156,6 +156,9 @@ struct ScanArgs {
   // (the full pass keeps span*cap + slot)
   uint32_t* span_first;
   uint64_t wcap;
+  // host-side only: the scan variant to launch (0 = the build's default;
+  // SRD_DEBUG_API builds A/B the others inside one context)
+  uint32_t variant;
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -231,6 +234,11 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // ((pos*16+nib)*64 + l): every lane its own bank, conflict-free) and one
 // 24-dword window per wave for the cooperative candidate check.
 constexpr int SCAN_WAVES_V2 = 16;
+// scan_kernel's F1 (straight-line first flagged line) default
+#ifndef SRD_FLAG1
+#define SRD_FLAG1 0
+#endif
+constexpr bool kFlag1 = SRD_FLAG1 != 0;
 struct alignas(2048) ScanLds {
   // the last slice-by-4 step of 16-byte chain q (q < 3) with the chain's
   // join shift folded in: byte i of s -> (b << 8i) * x^(32 + 128 (3 - q)),
@@ -300,6 +308,28 @@ __device__ __forceinline__ uint32_t crc_line4(const uint32_t (&d)[16], const Sca
          tab_lookup(L, s[3], R[0], SEL3);
   return xor3(v[0], v[1], v[2]) ^ v[3];
 }
+// Two 32-byte chains (8 dependent LDS round trips instead of 4, but 4
+// lookups per line in the unreplicated shifted tables instead of 12):
+// raw(line) = a x^256 ^ b; chain a's last step reads ScanLds::last's chain-1
+// tables (shift x^(128 (3 - 1)) = x^256)
+__device__ __forceinline__ uint32_t crc_line2(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
+  constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
+  uint32_t s[2] = {d[0], d[8]};
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint32_t t3 = tab_lookup(L, s[q], R[3], SEL0), t2 = tab_lookup(L, s[q], R[2], SEL1);
+      const uint32_t t1 = tab_lookup(L, s[q], R[1], SEL2), t0 = tab_lookup(L, s[q], R[0], SEL3);
+      s[q] = xor3(xor3(t3, t2, d[8 * q + j + 1]), t1, t0);
+    }
+  }
+  const uint32_t* m = L.last + 1024 * 1;
+  const uint32_t v0 = xor3(m[s[0] & 0xff], m[256 + ((s[0] >> 8) & 0xff)], m[512 + ((s[0] >> 16) & 0xff)]) ^ m[768 + (s[0] >> 24)];
+  const uint32_t v1 = xor3(tab_lookup(L, s[1], R[3], SEL0), tab_lookup(L, s[1], R[2], SEL1), tab_lookup(L, s[1], R[1], SEL2)) ^
+                      tab_lookup(L, s[1], R[0], SEL3);
+  return v0 ^ v1;
+}
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
@@ -333,6 +363,51 @@ __device__ __forceinline__ uint32_t lds_off(const void* p) {
 }
 __device__ __forceinline__ uint32_t lds_ld(uint32_t off) {
   return *(const __attribute__((address_space(3))) uint32_t*)(uintptr_t)off;
+}
+// crc_line4 with each level's 16 lookups issued together: the scheduler
+// otherwise issues two chains' 8 lookups and drains them before the other
+// two chains' (8 dependent LDS round trips per line instead of 4).  Groups:
+// per level the 16 address VALU, the 16 LDS reads, then the XORs.
+__device__ __forceinline__ uint32_t crc_line4_wide(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
+  constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
+  uint32_t s[4] = {d[0], d[4], d[8], d[12]};
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    uint32_t t[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      t[q][3] = tab_lookup(L, s[q], R[3], SEL0);
+      t[q][2] = tab_lookup(L, s[q], R[2], SEL1);
+      t[q][1] = tab_lookup(L, s[q], R[1], SEL2);
+      t[q][0] = tab_lookup(L, s[q], R[0], SEL3);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) s[q] = xor3(xor3(t[q][3], t[q][2], d[4 * q + j + 1]), t[q][1], t[q][0]);
+    __builtin_amdgcn_sched_group_barrier(0x0002, 16, 0);  // the 16 lookup addresses
+    __builtin_amdgcn_sched_group_barrier(0x0100, 16, 0);  // the 16 LDS reads
+    __builtin_amdgcn_sched_group_barrier(0x0002, 8, 0);   // the XORs
+  }
+  // the last level: chains 0-2 through the shifted tables (ScanLds::last,
+  // byte i of s at word 1024 q + 256 i + byte), chain 3 through tab
+  const uint32_t lb = lds_off(L.last);
+  uint32_t t[4][4];
+#pragma unroll
+  for (int q = 0; q < 3; q++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) t[q][i] = lds_ld(lb + 4096u * q + 1024u * i + 4u * ((s[q] >> (8 * i)) & 0xffu));
+  t[3][3] = tab_lookup(L, s[3], R[3], SEL0);
+  t[3][2] = tab_lookup(L, s[3], R[2], SEL1);
+  t[3][1] = tab_lookup(L, s[3], R[1], SEL2);
+  t[3][0] = tab_lookup(L, s[3], R[0], SEL3);
+  uint32_t v[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) v[q] = xor3(t[q][0], t[q][1], t[q][2]) ^ t[q][3];
+  __builtin_amdgcn_sched_group_barrier(0x0002, 16, 0);
+  __builtin_amdgcn_sched_group_barrier(0x0100, 16, 0);
+  const uint32_t r = xor3(v[0], v[1], v[2]) ^ v[3];
+  __builtin_amdgcn_sched_barrier(0);
+  return r;
 }
 // lane_weight for the scan, whose nib table sits at a 2 KiB-aligned LDS
 // offset: the nibble's address bits (7-10) are OR-ed into the lane's base
@@ -436,9 +511,20 @@ __device__ __forceinline__ uint64_t find_top(const uint8_t* file, uint64_t flen,
 
 // WIDE: stores above 2^40 bytes (prev offsets up to 48 bits, key_indexer.rs:12-15):
 // the level-1 filter looks for the two zero bytes m+14, m+15 at any alignment
-template <bool FULL, bool WIDE>
+// V: the variant (0 = the product build; others are A/B'd inside one context
+// by SRD_DEBUG_API builds: 1 = F1 flipped, 2 = F1 flipped with its staging
+// and node test after the CRC at priority 2, 3 = the line CRC as two 32-byte
+// chains)
+template <bool FULL, bool WIDE, int V = 0>
 __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
+  constexpr bool F1 = (V == 1 || V == 2) ? !kFlag1 : kFlag1;
+  constexpr bool F1_AFTER = V == 2;  // F1's staging + test after the CRC, at priority 2
+  constexpr bool CRC2 = V == 3;
+  constexpr bool RING2 = V == 4 || V == 5;  // a 2-deep register ring (one tile in flight), 16 VGPRs fewer
+  constexpr bool WIDE16 = V == 5 || V == 6;  // crc_line4_wide: each level's 16 lookups issued together
   __shared__ ScanLds lds;
+  // lanes of the record queue rq: with F1 its lane 63 is scratch
+  constexpr uint64_t RQ_LANES = F1 ? 63 : 64;
   if (blockIdx.x == 0) {
     for (uint32_t i = threadIdx.x; i < a.n_zero_words; i += blockDim.x) a.zero_words[i] = 0;
     if (threadIdx.x == 0 && a.sentinel) *a.sentinel = 0;
@@ -527,6 +613,14 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // tile's SX partial of line 63 (= its true SX_63).
   const uint32_t hb = a.filt_hb;
   uint64_t rootmax = 0;
+  // the previous tile's SX_63 (F1; uniform -- without F1 the window's win[22])
+  uint32_t hxp_s = 0;
+  // lane-constant LDS addresses of the straight-line window test: lane b
+  // reads dwords (b + 2) / 4 .. + 5 and the tombstone dword (b + 1) / 4
+  const uint32_t win_lds = lds_off(win);
+  const uint32_t f1_wa = win_lds + 4u * (((uint32_t)lane + 2) >> 2), f1_ta = win_lds + 4u * (((uint32_t)lane + 1) >> 2);
+  const uint32_t f1_sh = (((uint32_t)lane + 2) & 3) * 8;
+  (void)f1_wa; (void)f1_ta; (void)f1_sh;
   {
     // the line just before this wave's first tile: its tail bytes and its raw
     // CRC (= SX_63 of tile k0-1) seed the window; all lanes load it
@@ -544,6 +638,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       for (int j = 0; j < 4; j++) win[j] = has_prev ? pl[12 + j] : 0u;
       win[22] = has_prev ? cp : 0u;
     }
+    hxp_s = __builtin_amdgcn_readfirstlane(has_prev ? cp : 0u);
   }
 
   // first 8 bytes of tile k+1 (line 63's window) by a SCALAR load: the slow
@@ -609,13 +704,86 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       }
       slow = __ballot(hz != 0);
     }
+    // ---- the tile's first flagged line (other than line 63), straight-line ----
+    // (optimistic pass) No loop and no branch: the loop's header had to drain
+    // every outstanding LDS read and the CRC's result before it, so the
+    // flagged line's LDS round trips ran after the CRC's instead of beside
+    // them.  Lane f stages the window by an exec-masked asm store here, before
+    // the CRC in program order; the window reads and the node test below
+    // interleave with the CRC's lookups; the record goes to the register
+    // queue once hx is known.  Line 63 (its window needs the next tile's
+    // head), further flagged lines and multi-candidate lines take the loop.
+    uint64_t f1_pm = 0;
+    uint32_t f1_f = 0, f1_f2 = 0, f1_f3 = 0, f1_f4 = 0, f1_s0 = 0, f1_s1 = 0, f1_tdw = 0;
+    uint32_t W[6] = {0, 0, 0, 0, 0, 0};
+    bool has0 = false;
+    // the node test of the staged line (lane b: m = B + 64 f + b - 14,
+    // data_store.rs:404-470's fields)
+    auto f1_test = [&]() {
+      f1_f2 = alignb(W[3], W[2], f1_sh);
+      f1_f3 = alignb(W[4], W[3], f1_sh);
+      f1_f4 = alignb(W[5], W[4], f1_sh);
+      f1_s0 = alignb(W[1], W[0], f1_sh);
+      f1_s1 = alignb(W[2], W[1], f1_sh);
+      const int r = 64 * (int)f1_f + lane - 14;  // m - B, in [-14, 4081]
+      const uint32_t u = (uint32_t)(r + 20);
+      const bool inrange = (u <= remu) && ((int64_t)B + r > (int64_t)a.m_lo);
+      f1_pm = __ballot(has0 && inrange && f1_f3 <= hb && (f1_f2 | f1_f3) != 0 && f1_f4 != 0);
+      // two or more possible nodes: the loop's general path takes the line
+      // (uniform selects, no branch)
+      const bool multi = (f1_pm & (f1_pm - 1)) != 0;
+      slow |= multi ? (1ull << f1_f) : 0ull;
+      f1_pm = multi ? 0ull : f1_pm;
+    };
+    auto f1_stage_test = [&]() {
+      // (room in the record queue for one more: else the loop takes the line)
+      const uint64_t s63 = slow & ~(1ull << 63);
+      has0 = s63 != 0 && wtotal + count - flushed < RQ_LANES - 1;  // uniform
+      f1_f = has0 ? (uint32_t)__builtin_ctzll(s63) : 0u;
+      slow = has0 ? (slow & ~(1ull << f1_f)) : slow;  // the loop's lines
+      const uint32_t p12 = dpp<DPP_WAVE_SHR1>(d[12]), p13 = dpp<DPP_WAVE_SHR1>(d[13]),
+                     p14 = dpp<DPP_WAVE_SHR1>(d[14]), p15 = dpp<DPP_WAVE_SHR1>(d[15]);
+      const uint32_t n0 = dpp<DPP_WAVE_SHL1>(d[0]), n1 = dpp<DPP_WAVE_SHL1>(d[1]);
+      // exec masks (SGPR pairs): the line + next head by lane f; the previous
+      // line's tail by lane f only when f > 0 (f == 0: win[0..3] holds the
+      // previous tile's line 63, carried below)
+      const uint64_t m1 = has0 ? (1ull << f1_f) : 0ull, m0 = f1_f ? m1 : 0ull;
+      uint64_t save;
+      asm volatile(
+          "s_mov_b64 %[sv], exec\n\t"
+          "s_mov_b64 exec, %[m0]\n\t"
+          "ds_write_b128 %[a], %[p]\n\t"
+          "s_mov_b64 exec, %[m1]\n\t"
+          "ds_write_b128 %[a], %[d0] offset:16\n\t"
+          "ds_write_b128 %[a], %[d1] offset:32\n\t"
+          "ds_write_b128 %[a], %[d2] offset:48\n\t"
+          "ds_write_b128 %[a], %[d3] offset:64\n\t"
+          "ds_write_b64 %[a], %[n] offset:80\n\t"
+          "s_mov_b64 exec, %[sv]"
+          : [sv] "=&s"(save)
+          : [m0] "s"(m0), [m1] "s"(m1), [a] "v"(win_lds), [p] "v"(u32x4{p12, p13, p14, p15}),
+            [d0] "v"(u32x4{d[0], d[1], d[2], d[3]}), [d1] "v"(u32x4{d[4], d[5], d[6], d[7]}),
+            [d2] "v"(u32x4{d[8], d[9], d[10], d[11]}), [d3] "v"(u32x4{d[12], d[13], d[14], d[15]}),
+            [n] "v"(u32x2{n0, n1})
+          : "memory");
+      // lane b's window dwords from its lane-constant address, in LDS issue
+      // order behind the stores (one wave: no wait between them)
+#pragma unroll
+      for (int i = 0; i < 6; i++) W[i] = lds_ld(f1_wa + 4 * i);
+      f1_tdw = lds_ld(f1_ta);
+      f1_test();
+    };
+    if constexpr (F1 && !F1_AFTER && !FULL) f1_stage_test();
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
     // Wave priority over the LDS-latency chains (the CRC's lookups here, the
     // flagged-line window below): a wave in them wins the issue arbitration,
     // so its next round of lookups goes out as soon as the last returns,
     // while the other waves fill the gaps (same-box A/B: -4 %)
-    __builtin_amdgcn_s_setprio(3);
-    const uint32_t c = crc_line4(d, lds, R);
+    // (F1: the ring loop raised the priority before the tile's loads already;
+    // a setprio here would split the scheduling region between the window
+    // test above and the CRC's lookups)
+    if (!F1 || F1_AFTER || tail_tile) __builtin_amdgcn_s_setprio(3);
+    const uint32_t c = CRC2 ? crc_line2(d, lds, R) : WIDE16 ? crc_line4_wide(d, lds, R) : crc_line4(d, lds, R);
     __builtin_amdgcn_s_setprio(0);
     const uint32_t hx = half_suffix_xor(lane_weight_or(c, nib_lane), lane);
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
@@ -639,6 +807,50 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint32_t lo2 = flush ? lo : 0u, n2 = flush ? 4u * t + 4u - lo : 0u;
       const uint32_t off = (uint32_t)lane - lo2 < n2 ? 4u * lane : OOB_OFF;
       __builtin_amdgcn_raw_buffer_store_b32(tacc, out_rsrc(a.tile + 4 * g, 256), off, 0, 0);
+    }
+
+    if constexpr (F1 && F1_AFTER && !FULL) {
+      __builtin_amdgcn_s_setprio(2);
+      f1_stage_test();
+    }
+    if constexpr (F1 && !FULL) {
+      // the first flagged line's record (at most one candidate: the node test
+      // is link2's, F_NT) into the register queue; lane 63 of rq is scratch
+      // (a tile without a record writes there), so the queue holds 63
+      const bool single = f1_pm != 0;  // uniform
+      const int bl = single ? __builtin_ctzll(f1_pm) : 0;
+      const int rs = 64 * (int)f1_f + bl - 14;
+      const uint64_t m = B + (int64_t)rs;
+      const uint32_t s2 = __builtin_amdgcn_readlane(f1_f2, bl), s3 = __builtin_amdgcn_readlane(f1_f3, bl);
+      const uint32_t s0 = __builtin_amdgcn_readlane(f1_s0, bl), s1 = __builtin_amdgcn_readlane(f1_s1, bl);
+      const uint32_t s4 = __builtin_amdgcn_readlane(f1_f4, bl);
+      const uint32_t os = (uint32_t)bl + 2;
+      const uint32_t stb = ((uint32_t)__builtin_amdgcn_readlane(f1_tdw, bl) >> (((os - 1) & 3) * 8)) & 0xffu;
+      const uint32_t us = (uint32_t)(rs + 20);
+      const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
+      const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
+      const int lm = rs >> 6;
+      const uint32_t hm = lm < 0 ? hxp_s : (uint32_t)__builtin_amdgcn_readlane(hx, lm & 63);
+      const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
+      const uint32_t fl = F_NT | (stb == 0 ? F_ZB : 0u) | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
+                          (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
+                          ((js & 63) < 32 ? F_SUF_LO : 0u);
+      const uint64_t rr = wtotal + count;  // the record's index in the wave's region
+      const bool inq = single && rr < a.wcap;  // room in the queue: checked before staging
+      const int li = inq ? (int)(rr - flushed) : (int)(RQ_LANES);
+      rq[0] = writelane_u32((uint32_t)m, li, rq[0]);
+      rq[1] = writelane_u32((uint32_t)(m >> 32), li, rq[1]);
+      rq[2] = writelane_u32(hm, li, rq[2]);
+      rq[3] = writelane_u32(hs, li, rq[3]);
+      rq[4] = writelane_u32(fl, li, rq[4]);
+      rq[5] = writelane_u32(s2, li, rq[5]);
+      rq[6] = writelane_u32(s3, li, rq[6]);
+      rq[7] = writelane_u32(s0, li, rq[7]);
+      rq[8] = writelane_u32(s1, li, rq[8]);
+      rq[9] = writelane_u32(s4, li, rq[9]);
+      rvalid |= inq ? (1ull << li) : 0ull;
+      ovf = ovf || (single && rr >= a.wcap);
+      count += single ? 1u : 0u;
     }
 
     // Re-define d by an empty asm once its loads have been consumed: a loop
@@ -686,7 +898,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 #pragma unroll
       for (int i = 0; i < 6; i++) W[i] = win[base + i];
       const uint32_t tdw = win[(o - 1) >> 2];
-      const uint32_t hxp = win[22];
+      const uint32_t hxp = F1 ? 0u : win[22];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -722,14 +934,15 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
           const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
           const int lm = rs >> 6;
-          const uint32_t hm = lm < 0 ? __builtin_amdgcn_readfirstlane(hxp) : __builtin_amdgcn_readlane(hx, lm & 63);
+          const uint32_t hm = lm < 0 ? (F1 ? hxp_s : (uint32_t)__builtin_amdgcn_readfirstlane(hxp))
+                                     : (uint32_t)__builtin_amdgcn_readlane(hx, lm & 63);
           const uint64_t r = wtotal + count;  // the record's index in the wave's region
           if (r < a.wcap) {
             const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
             const uint32_t fl = REC_KIND | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
                                 (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
                                 ((js & 63) < 32 ? F_SUF_LO : 0u);
-            if (r - flushed < 64) {
+            if (r - flushed < RQ_LANES) {
               // record r -> lane r - flushed of the record registers
               const int li = (int)(r - flushed);
               rq[0] = writelane_u32((uint32_t)m, li, rq[0]);
@@ -776,7 +989,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint32_t hs = __shfl(hx, (int)(js & 63));
       const int lm = r >> 6;                             // m's line (-1: previous tile's line 63)
       const uint32_t hm0 = __shfl(hx, lm & 63);
-      const uint32_t hm = lm < 0 ? hxp : hm0;
+      const uint32_t hm = lm < 0 ? (F1 ? hxp_s : hxp) : hm0;
       if (FULL ? count + __popcll(cm) > a.cap : wtotal + count + __popcll(cm) > a.wcap) ovf = true;
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
@@ -794,7 +1007,19 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
     __builtin_amdgcn_s_setprio(0);
     // carry the last line's tail and SX_63 into the next tile's window
-    if (lane == 63) {
+    if constexpr (F1) {
+      // lane 63's tail by an exec-masked asm store (no branch), SX_63 in an SGPR
+      uint64_t save;
+      asm volatile(
+          "s_mov_b64 %[sv], exec\n\t"
+          "s_mov_b64 exec, %[m]\n\t"
+          "ds_write_b128 %[a], %[p]\n\t"
+          "s_mov_b64 exec, %[sv]"
+          : [sv] "=&s"(save)
+          : [m] "s"(1ull << 63), [a] "v"(win_lds), [p] "v"(u32x4{d[12], d[13], d[14], d[15]})
+          : "memory");
+      hxp_s = __builtin_amdgcn_readlane(hx, 63);
+    } else if (lane == 63) {
 #pragma unroll
       for (int j = 0; j < 4; j++) win[j] = d[12 + j];
       win[22] = hx;
@@ -864,27 +1089,39 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // reaches the loop latch, and that (never taken) latch -> header path
   // would shorten the compiler's wait counts as well.  The <= 2 remaining
   // ring tiles run in the unpipelined loop below with the file's tail tiles.
-  const uint32_t nfull = nk / 3;
+  constexpr uint32_t RD = RING2 ? 2 : 3;  // ring depth
+  const uint32_t nfull = nk / RD;
   load_tile(k0, A);
   pad_stores(0);
-  load_tile(k0 + 1, Bv);
-  pad_stores(1);
+  if constexpr (!RING2) {
+    load_tile(k0 + 1, Bv);
+    pad_stores(1);
+  }
   for (uint32_t i = 0; i < nfull; i++) {
-    const uint32_t j = 3 * i;
+    const uint32_t j = RD * i;
     // priority from the tile's prefetch loads through its CRC (process()
     // drops it after the lookups): -1.6 % same-box A/B over priority on the
     // CRC alone
-    __builtin_amdgcn_s_setprio(3);
-    load_tile(k0 + min(j + 2, nk), Cv);
-    process(k0 + j, A, body);
-    __builtin_amdgcn_s_setprio(3);
-    load_tile(k0 + min(j + 3, nk), A);
-    process(k0 + j + 1, Bv, body);
-    __builtin_amdgcn_s_setprio(3);
-    load_tile(k0 + min(j + 4, nk), Bv);
-    process(k0 + j + 2, Cv, body);
+    if constexpr (RING2) {
+      __builtin_amdgcn_s_setprio(3);
+      load_tile(k0 + min(j + 1, nk), Bv);
+      process(k0 + j, A, body);
+      __builtin_amdgcn_s_setprio(3);
+      load_tile(k0 + min(j + 2, nk), A);
+      process(k0 + j + 1, Bv, body);
+    } else {
+      __builtin_amdgcn_s_setprio(3);
+      load_tile(k0 + min(j + 2, nk), Cv);
+      process(k0 + j, A, body);
+      __builtin_amdgcn_s_setprio(3);
+      load_tile(k0 + min(j + 3, nk), A);
+      process(k0 + j + 1, Bv, body);
+      __builtin_amdgcn_s_setprio(3);
+      load_tile(k0 + min(j + 4, nk), Bv);
+      process(k0 + j + 2, Cv, body);
+    }
   }
-  const uint64_t kr = k0 + 3ull * nfull;
+  const uint64_t kr = k0 + (uint64_t)RD * nfull;
   // the ring's remainder and the file's last <= 2 tiles (masked: a tail
   // tile's bytes past file_len read as 0; a no-op on the others)
   for (uint64_t k = kr; k < k1; k++) {

@@ -35,9 +35,31 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
   return v;
 }
-// v * x^32768 (one 4 KiB block) = two x^16384 byte-table steps
-__device__ __forceinline__ uint32_t mul_tile(uint32_t v) { return mul16k(mul16k(v, &g_tabs.m16k[0][0]), &g_tabs.m16k[0][0]); }
+// v * x^16384 for a wave-uniform v by SCALAR loads of the byte tables (the
+// table words are uniform too: no LDS, no vector memory)
+__device__ __forceinline__ uint32_t mul16k_u(uint32_t v) {
+  const __attribute__((address_space(4))) uint32_t* m =
+      (const __attribute__((address_space(4))) uint32_t*)&g_tabs.m16k[0][0];
+  return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
+}
+// v * x^32768 (one 4 KiB block) = two x^16384 steps
+__device__ __forceinline__ uint32_t mul_tile_u(uint32_t v) { return mul16k_u(mul16k_u(v)); }
 
+// 64 readable bytes for the lanes whose line is no whole in-bounds payload
+// line (their bytes are read one by one instead): the payload ring's loads
+// stay unconditional
+__device__ u32x4 g_wdummy[4];
+
+// One wave per entry, entries w, w + W, ... of the batch (W waves in the
+// grid).  The 4 KiB blocks of the wave's entries form one sequence; a 2-deep
+// register ring keeps the next block's loads in flight while the current
+// one is stored and checksummed.  Per block: each lane moves its 64-byte
+// line (4 x 16-byte loads and stores) and computes the line's raw CRC from
+// the same registers (crc_line4: four 16-byte slice-by-4 chains, LDS tables
+// as the scan's), weighted by lane (lane_weight_or) and XOR-reduced per half
+// (half_suffix_xor): raw CRC of the block = (lo * x^16384) ^ hi.  The key
+// hashes (XXH3-64, compute_hash.rs:25-27) are computed 64 at a time, one
+// entry per lane, not by one lane per entry.
 __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs a) {
   __shared__ ScanLds lds;
   load_crc_lds(lds);
@@ -45,78 +67,136 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t R[4];
   crc_lane_bases(R, lane);
-  uint64_t last_len = ~0ull;   // cache of ~(x^(8 len) * 0xFFFFFFFF) for runs of equal lengths
+  const uint32_t nib_lane = lds_off(lds.nib) + 4u * (lane & 31);
+  const uint64_t W = (uint64_t)gridDim.x * SCAN_WAVES_V2;
+  const uint64_t w = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
+  if (w >= a.n) return;
+  const bool pay_al = ((uintptr_t)a.pay & 15) == 0;
+  uint64_t last_len = ~0ull;  // cache of ~(x^(8 len) * 0xFFFFFFFF) for runs of equal lengths
   uint32_t last_fix = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv; i < a.n; i += (uint64_t)gridDim.x * SCAN_WAVES_V2) {
-    const srd_write_entry e = a.ent[i];
-    // key hash (lane 0; compute_hash.rs:25-27 = xxh3_64 with seed 0)
-    uint64_t kh = e.key_src;  // SRD_ENTRY_HASHED: batch_write_with_key_hashes / write_stream_with_key_hash
-    if (!(e.flags & SRD_ENTRY_HASHED) && lane == 0) kh = xxh3_64(a.keys + e.key_src, e.key_len);
-    kh = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(kh >> 32)) << 32) |
-         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)kh);
-    uint32_t crc;
-    uint64_t mo;
-    if (e.flags & SRD_ENTRY_TOMB) {
+
+  auto vec_line = [&](const srd_write_entry& e, uint64_t b) -> bool {
+    return !(e.flags & SRD_ENTRY_TOMB) && pay_al && (e.src & 15) == 0 && b * TILE + 64ull * lane + 64 <= e.len;
+  };
+  auto load_blk = [&](const srd_write_entry& e, uint64_t b, uint32_t (&o)[16]) {
+    const u32x4* q = vec_line(e, b) ? (const u32x4*)(a.pay + e.src + b * TILE + 64ull * lane) : g_wdummy;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const u32x4 v = q[j];
+      o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
+    }
+  };
+
+  uint64_t i = 0, b = 0, khl = 0, gend = 0;
+  srd_write_entry e;
+  uint32_t acc = 0, any = 0;
+  // one unit of the sequence: block b of entry i (a tombstone is one unit
+  // without a block); returns whether a next unit exists in the group (its
+  // loads went to nx)
+  auto step = [&](uint32_t (&d)[16], uint32_t (&nx)[16]) -> bool {
+    const bool tomb = e.flags & SRD_ENTRY_TOMB;
+    const uint64_t nb = tomb ? 1 : (e.len + TILE - 1) / TILE;
+    uint64_t i2 = i, b2 = b + 1;
+    srd_write_entry e2 = e;
+    if (b2 >= nb) {
+      i2 = i + W;
+      b2 = 0;
+      if (i2 < gend) e2 = a.ent[i2];
+    }
+    const bool more = i2 < gend;
+    load_blk(e2, b2, nx);  // (past the group: a block of this entry again, or the dummy -- harmless)
+    const int jl = (int)(((i - w) / W) % 64);  // the entry's lane in khl
+    const uint64_t kh = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(khl >> 32), jl) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)khl, jl);
+    bool done = false;
+    uint32_t crc = 0;
+    uint64_t mo = 0;
+    if (tomb) {
       // tombstone: the single NULL byte, no prepad (data_store.rs:864-897)
       if (lane == 0) a.out[e.tail - a.base] = 0;
       crc = 0xD202EF8Du;  // CRC32(b"\0")
       mo = e.tail + 1;
+      done = true;
     } else {
       const uint64_t pad = prepad64(e.tail), st = e.tail + pad;  // data_store.rs:907-914
-      if ((uint64_t)lane < pad) a.out[e.tail - a.base + lane] = 0;
-      const uint8_t* src = a.pay + e.src;
       uint8_t* dst = a.out + (st - a.base);  // 64-aligned when out is
-      const bool fast_src = ((uintptr_t)src & 15) == 0;
-      uint32_t acc = 0, any = 0;
-      const uint64_t nb = (e.len + TILE - 1) / TILE;
-      for (uint64_t b = 0; b < nb; b++) {
-        const uint64_t o = b * TILE + 64ull * lane;
+      if (b == 0) {
+        if ((uint64_t)lane < pad) a.out[e.tail - a.base + lane] = 0;
+        acc = 0;
+        any = 0;
+      }
+      const uint64_t o = b * TILE + 64ull * lane;
+      if (vec_line(e, b)) {
+        u32x4* q = (u32x4*)(dst + o);
+#pragma unroll
+        for (int j = 0; j < 4; j++) q[j] = u32x4{d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]};
+      } else {
+        // a partial (or unaligned) line: byte by byte, zero past the payload
         const uint32_t nl = o < e.len ? (uint32_t)min<uint64_t>(64, e.len - o) : 0u;
-        uint32_t d[16];
-        if (nl == 64 && fast_src) {
-          const u32x4* q = (const u32x4*)(src + o);
-          u32x4* w = (u32x4*)(dst + o);
+        const uint8_t* src = a.pay + e.src;
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const u32x4 v = q[j];
-            w[j] = v;
-            d[4 * j] = v[0]; d[4 * j + 1] = v[1]; d[4 * j + 2] = v[2]; d[4 * j + 3] = v[3];
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 16; j++) d[j] = 0;
-          for (uint32_t q = 0; q < nl; q++) {
-            const uint8_t v = src[o + q];
-            dst[o + q] = v;
-            d[q >> 2] |= (uint32_t)v << (8 * (q & 3));
-          }
+        for (int j = 0; j < 16; j++) d[j] = 0;
+        for (uint32_t q = 0; q < nl; q++) {
+          const uint8_t v = src[o + q];
+          dst[o + q] = v;
+          d[q >> 2] |= (uint32_t)v << (8 * (q & 3));
         }
+      }
 #pragma unroll
-        for (int j = 0; j < 16; j++) any |= d[j];
-        // raw CRC of this 4 KiB block (zero-padded past the payload)
-        const uint32_t u = lane_weight(crc_line1(d, lds, R), lds.nib, lane);
-        const uint32_t lo = wave_xor(lane < 32 ? u : 0u), hi = wave_xor(lane < 32 ? 0u : u);
-        const uint32_t raw = mul16k(lo, &g_tabs.m16k[0][0]) ^ hi;
-        acc = mul_tile(acc) ^ raw;
+      for (int j = 0; j < 16; j++) any |= d[j];
+      // raw CRC of this 4 KiB block (zero-padded past the payload)
+      const uint32_t hx = half_suffix_xor(lane_weight_or(crc_line4_wide(d, lds, R), nib_lane), lane);
+      const uint32_t lo = __builtin_amdgcn_readlane(hx, 0), hi = __builtin_amdgcn_readlane(hx, 32);
+      const uint32_t raw = mul16k_u(lo) ^ hi;
+      acc = b ? mul_tile_u(acc) ^ raw : raw;
+      if (b + 1 == nb) {
+        if (a.null_only && !__ballot(any != 0) && lane == 0) atomicOr(a.null_only, 1u);
+        const uint64_t z = nb * TILE - e.len;  // trailing zero padding of the last block, < 4096
+        if (z) acc = mulp(g_tabs.invpow[z], acc);
+        if (e.len != last_len) {
+          last_len = e.len;
+          last_fix = ~mulp(xpow8_dev(e.len), 0xFFFFFFFFu);
+        }
+        crc = acc ^ last_fix;  // crc32fast: init and xorout 0xFFFFFFFF
+        mo = st + e.len;
+        done = true;
       }
-      if (a.null_only && !__ballot(any != 0) && lane == 0) atomicOr(a.null_only, 1u);
-      const uint64_t z = nb * TILE - e.len;  // trailing zero padding of the last block, < 4096
-      if (z) acc = mulp(g_tabs.invpow[z], acc);
-      if (e.len != last_len) {
-        last_len = e.len;
-        last_fix = ~mulp(xpow8_dev(e.len), 0xFFFFFFFFu);
+    }
+    if (done) {
+      // EntryMetadata::serialize: key_hash LE, prev_offset LE, checksum LE
+      if (lane < 20) {
+        const uint64_t v = lane < 8 ? kh : lane < 16 ? e.tail : (uint64_t)crc;
+        a.out[mo - a.base + lane] = (uint8_t)(v >> (8 * (lane & 7)));
       }
-      crc = acc ^ last_fix;  // crc32fast: init and xorout 0xFFFFFFFF
-      mo = st + e.len;
+      if (lane == 0) {
+        a.kh_out[i] = kh;
+        a.mo_out[i] = mo;
+      }
     }
-    // EntryMetadata::serialize: key_hash LE, prev_offset LE, checksum LE
-    if (lane < 20) {
-      const uint64_t v = lane < 8 ? kh : lane < 16 ? e.tail : (uint64_t)crc;
-      a.out[mo - a.base + lane] = (uint8_t)(v >> (8 * (lane & 7)));
+    i = i2;
+    b = b2;
+    e = e2;
+    return more;
+  };
+  uint32_t cur[16], nxt[16];
+  // groups of 64 entries of the wave: their key hashes first (one per lane,
+  // outside the ring), then the ring over the group's blocks
+  for (uint64_t g0 = w; g0 < a.n; g0 += 64 * W) {
+    {
+      const uint64_t ij = g0 + (uint64_t)lane * W;
+      khl = 0;
+      if (ij < a.n) {
+        const srd_write_entry ej = a.ent[ij];
+        khl = (ej.flags & SRD_ENTRY_HASHED) ? ej.key_src : xxh3_64(a.keys + ej.key_src, ej.key_len);
+      }
     }
-    if (lane == 0) {
-      a.kh_out[i] = kh;
-      a.mo_out[i] = mo;
+    gend = min(a.n, g0 + 64 * W);
+    i = g0;
+    b = 0;
+    e = a.ent[i];
+    load_blk(e, 0, cur);
+    // the ring: two register blocks, the roles swapped every unit
+    while (step(cur, nxt) && step(nxt, cur)) {
     }
   }
 }

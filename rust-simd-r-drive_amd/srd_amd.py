@@ -59,7 +59,7 @@ EXPORTS = [
     "srd_batch_read_hashed_device", "srd_batch_read",
     "srd_iter_entries_device", "srd_estimate_compaction_savings_device", "srd_compact_device",
     "srd_shard_cuts", "srd_validate_index_multi", "srd_ctx_stage_info", "srd_index_hash_device",
-    "srd_validate_index_multi_device", "srd_ctx_multi_summary",
+    "srd_validate_index_multi_device", "srd_ctx_multi_summary", "srd_ctx_scan_list", "srd_ctx_set_timing_every",
 ]
 
 
@@ -118,6 +118,8 @@ def lib():
         L.srd_last_error.restype = C.c_char_p
         L.srd_ctx_timings.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double)]
         L.srd_ctx_set_timing.argtypes = [vp, C.c_int]
+        L.srd_ctx_scan_list.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
+        L.srd_ctx_set_timing_every.argtypes = [vp, C.c_int]
         L.srd_validate_index_device.argtypes = [vp, vp, u64, u32, C.POINTER(DeviceResult)]
         L.srd_validate_index.argtypes = [vp, vp, u64, u32, C.POINTER(DeviceResult)]
         L.srd_result_free.argtypes = [C.POINTER(DeviceResult)]
@@ -202,12 +204,25 @@ class Context:
         """HIP-event timing level: TIMING_NONE (default), TIMING_SCAN, TIMING_CALL."""
         _check(lib().srd_ctx_set_timing(self.h, level))
 
+    def set_timing_every(self, n: int):
+        """With TIMING_SCAN: stamp only every n-th scan launch (srd_ctx_set_timing_every)."""
+        _check(lib().srd_ctx_set_timing_every(self.h, n))
+
     def timings(self):
         """(scan_ms, scan_launches) summed over the validate calls since the last
         read, and total_ms of the last call (HIP events; srd_ctx_timings)."""
         a, n, b = C.c_double(), C.c_int(), C.c_double()
         _check(lib().srd_ctx_timings(self.h, C.byref(a), C.byref(n), C.byref(b)))
         return a.value, n.value, b.value
+
+    def scan_list(self) -> list[float]:
+        """The individual scan durations (ms) behind the last timings() read."""
+        n = lib().srd_ctx_scan_list(self.h, None, 0)
+        if n < 0:
+            _check(n)
+        buf = (C.c_float * max(n, 1))()
+        lib().srd_ctx_scan_list(self.h, buf, n)
+        return list(buf[:n])
 
     @property
     def stream(self) -> int:

@@ -212,3 +212,53 @@ def test_full_c5_write_equals_c2(ctx):
     r = S.validate_index_device(store.data_ptr(), size, 0, ctx)
     assert np.array_equal(S.device_to_numpy(r.index_key_hash, n), kh)
     assert np.array_equal(S.device_to_numpy(r.index_packed, n) & np.uint64((1 << 48) - 1), mo)
+
+
+def test_overflow_after_large_call_one_context():
+    """Regression test for the fault fixed in 46785b6: after a large call, a
+    store whose candidate records overflow their regions (and, later, the
+    dense candidate capacity capK the large call sized) made the shape
+    kernels read parents link2 never wrote.  All on ONE context: the full C2
+    store, the reference's storage_benchmark shape (1M x 8 B: ~256 records
+    per 16 KiB span against 8 slots, so the regions overflow and grow), a
+    5M x 8 B store (more candidates than C2's capK), then C2 again; each
+    compared with the oracle (C2 by its closed form)."""
+    import torch
+    c = S.Context(0)
+    try:
+        n2 = 1 << 20
+        size2 = S.synth_store_len(n2)
+        t = torch.empty(S.padded_size(size2), dtype=torch.uint8, device="cuda")
+        S.synth_store_device(t.data_ptr(), n2, 4096, ctx=c)
+        torch.cuda.synchronize()
+
+        def c2():
+            r = S.validate_index_device(t.data_ptr(), size2, 0, c)
+            assert (r.mode, r.final_len, r.n_chain, r.n_index, r.n_crc_bad) == (0, size2, n2, n2, 0)
+            ln = S.device_to_numpy(r.payload_len, n2, np.uint64)
+            assert np.all(ln == 4096)
+
+        c2()
+        for store in (_storage_benchmark_store(), None):
+            if store is None:  # 5M x 8 B, generated on the device: 320 MB, ~5M candidates > C2's capK (4.26M)
+                n = 5_000_000
+                size = S.synth_store_len(n, 8)
+                d = torch.zeros(S.padded_size(size), dtype=torch.uint8, device="cuda")
+                S.synth_store_device(d.data_ptr(), n, 8, ctx=c)
+                torch.cuda.synchronize()
+                store = d[:size].cpu().numpy()
+                del d
+            r = S.validate_index(store, 0, c)
+            ch = O.chain_arrays(store, store.size)
+            assert (r.final_len, r.n_chain, r.n_crc_bad) == (store.size, len(ch), 0)
+            for k in ("meta_off", "key_hash", "prev_offset", "payload_start", "payload_len", "crc_stored",
+                      "crc_computed", "crc_ok"):
+                assert np.array_equal(getattr(r, k).astype(np.uint64), ch[k].astype(np.uint64)), k
+            keys, packed = O.key_indexer_arrays(store, store.size)
+            o = np.argsort(r.index_key_hash, kind="stable")
+            assert np.array_equal(r.index_key_hash[o], keys) and np.array_equal(r.index_packed[o], packed)
+        c2()
+        del t
+        torch.cuda.empty_cache()
+    finally:
+        c.close()
