@@ -315,6 +315,9 @@ int ensure_cub(Ctx* c, uint64_t n) {
 // stores above 2^40 bytes take the WIDE scan (48-bit prev offsets)
 constexpr uint64_t kWide = 1ull << 40;
 constexpr uint64_t kMaxFile = 1ull << 48;  // packed offsets are 48-bit (key_indexer.rs:12-15, 79-85)
+#ifdef SRD_DEBUG_API
+constexpr uint32_t kDbgScanOnly = 1u << 30;  // SRD_DEBUG_API timing builds: the optimistic scan alone
+#endif
 // With timing events, the scan is launched by hipExtLaunchKernel, which
 // stamps the events with the kernel's own start and stop (the dispatch
 // packet's, as rocprofv3 sees them) instead of marker packets around it: a
@@ -353,6 +356,16 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
   } else if (a.variant == 6) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 6>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 6>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 7) {
+    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 7>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 8) {
+    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 8>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 9) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 9>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 9>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 10) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 10>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 10>, grid, block, 0, s, e0, e1, 0, a);
 #endif
   } else if (e0) {
     if (a.flen > kWide)
@@ -525,7 +538,7 @@ static void scan_weights(uint32_t (&wq)[16]) {
 }
 #ifdef SRD_DEBUG_API  // timing builds: A/B of scan variants inside one context (one workspace)
 extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
-  if (!c || v < 0 || v > 6) return SRD_ERR_ARG;
+  if (!c || v < 0 || v > 10) return SRD_ERR_ARG;
   c->scan_variant = (uint32_t)v;
   return 0;
 }
@@ -1156,6 +1169,13 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     launch_scan<false>(g, a, c->stream, e0, e1);
     KCHK(c, "scan_kernel");
     HIPCHK(hipGetLastError());
+#ifdef SRD_DEBUG_API
+    if (flags & kDbgScanOnly) {  // timing-only ablations: the scan alone, no result
+      HIPCHK(hipStreamSynchronize(c->stream));
+      *done = true;
+      return 0;
+    }
+#endif
     Link2Args l{};
     l.file = d_file;
     l.flen = flen;

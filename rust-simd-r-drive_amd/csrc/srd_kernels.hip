@@ -522,6 +522,16 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   constexpr bool CRC2 = V == 3;
   constexpr bool RING2 = V == 4 || V == 5;  // a 2-deep register ring (one tile in flight), 16 VGPRs fewer
   constexpr bool WIDE16 = V == 5 || V == 6;  // crc_line4_wide: each level's 16 lookups issued together
+  // timing-only ablations (wrong results; SRD_DEBUG_API's scan-only calls):
+  // 7 = the ring's loads alone (each tile XOR-folded), 8 = the whole tile
+  // body on two L1/L2-resident tiles per block (no HBM traffic)
+  constexpr bool MEMONLY = V == 7, NOHBM = V == 8;
+  // 9 = the previous tile's line-63 tail and SX_63 carried in SGPRs (no
+  // per-tile LDS store by lane 63; the f == 0 window takes them from there),
+  // 10 = 9 with the 16-wide CRC levels
+  constexpr bool SCARRY = V == 9 || V == 10;
+  constexpr bool WIDE16B = V == 10;
+  uint32_t memonly_acc = 0;
   __shared__ ScanLds lds;
   // lanes of the record queue rq: with F1 its lane 63 is scratch
   constexpr uint64_t RQ_LANES = F1 ? 63 : 64;
@@ -592,8 +602,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // (no loads under divergent/uniform branches, so the compiler's vmcnt
   // waits never have to drain the prefetch ring).  The tile's code (CRC,
   // lane weights, suffix XOR, filter) is one basic block.
+  const uint64_t nohbm_k = (a.part.s_lo + part_block_start(a.part, blockIdx.x)) * SPAN_TILES;
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
-    const u32x4* q = (const u32x4*)(file + k * (uint64_t)TILE + 64ull * lane);
+    const u32x4* q = (const u32x4*)(file + (NOHBM ? nohbm_k + (k & 1) : k) * (uint64_t)TILE + 64ull * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       // plain loads: this 64 B-per-lane pattern runs at ~3.8 TB/s with nt, ~6.1 without
@@ -615,6 +626,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   uint64_t rootmax = 0;
   // the previous tile's SX_63 (F1; uniform -- without F1 the window's win[22])
   uint32_t hxp_s = 0;
+  uint32_t carry_s[4] = {0, 0, 0, 0};  // SCARRY: the previous tile's line-63 tail (uniform)
   // lane-constant LDS addresses of the straight-line window test: lane b
   // reads dwords (b + 2) / 4 .. + 5 and the tombstone dword (b + 1) / 4
   const uint32_t win_lds = lds_off(win);
@@ -639,6 +651,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       win[22] = has_prev ? cp : 0u;
     }
     hxp_s = __builtin_amdgcn_readfirstlane(has_prev ? cp : 0u);
+#pragma unroll
+    for (int j = 0; j < 4; j++) carry_s[j] = __builtin_amdgcn_readfirstlane(has_prev ? pl[12 + j] : 0u);
   }
 
   // first 8 bytes of tile k+1 (line 63's window) by a SCALAR load: the slow
@@ -657,6 +671,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // under a branch inside the loop makes the compiler drain the whole
   // prefetch ring (vmcnt(0)) at the loop header.
   auto process = [&](uint64_t k, uint32_t (&d)[16], auto tail_c) {
+    if constexpr (MEMONLY) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) memonly_acc ^= d[j];
+      __builtin_amdgcn_s_setprio(0);
+      return;
+    }
     constexpr bool tail_tile = decltype(tail_c)::value;
     const uint64_t B = k * (uint64_t)TILE;
     const uint64_t span = k / SPAN_TILES;
@@ -783,7 +803,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     // a setprio here would split the scheduling region between the window
     // test above and the CRC's lookups)
     if (!F1 || F1_AFTER || tail_tile) __builtin_amdgcn_s_setprio(3);
-    const uint32_t c = CRC2 ? crc_line2(d, lds, R) : WIDE16 ? crc_line4_wide(d, lds, R) : crc_line4(d, lds, R);
+    const uint32_t c = CRC2 ? crc_line2(d, lds, R) : (WIDE16 || WIDE16B) ? crc_line4_wide(d, lds, R) : crc_line4(d, lds, R);
     __builtin_amdgcn_s_setprio(0);
     const uint32_t hx = half_suffix_xor(lane_weight_or(c, nib_lane), lane);
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
@@ -881,7 +901,10 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
         }
       }
       if (lane == f) {
-        if (f > 0) *(u32x4*)&win[0] = u32x4{p12, p13, p14, p15};
+        if constexpr (SCARRY)
+          *(u32x4*)&win[0] = f > 0 ? u32x4{p12, p13, p14, p15} : u32x4{carry_s[0], carry_s[1], carry_s[2], carry_s[3]};
+        else if (f > 0)
+          *(u32x4*)&win[0] = u32x4{p12, p13, p14, p15};
 #pragma unroll
         for (int j = 0; j < 4; j++) *(u32x4*)&win[4 + 4 * j] = u32x4{d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]};
         *(u32x2*)&win[20] = u32x2{n0, n1};
@@ -898,7 +921,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 #pragma unroll
       for (int i = 0; i < 6; i++) W[i] = win[base + i];
       const uint32_t tdw = win[(o - 1) >> 2];
-      const uint32_t hxp = F1 ? 0u : win[22];
+      const uint32_t hxp = (F1 || SCARRY) ? 0u : win[22];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -934,7 +957,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
           const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
           const int lm = rs >> 6;
-          const uint32_t hm = lm < 0 ? (F1 ? hxp_s : (uint32_t)__builtin_amdgcn_readfirstlane(hxp))
+          const uint32_t hm = lm < 0 ? ((F1 || SCARRY) ? hxp_s : (uint32_t)__builtin_amdgcn_readfirstlane(hxp))
                                      : (uint32_t)__builtin_amdgcn_readlane(hx, lm & 63);
           const uint64_t r = wtotal + count;  // the record's index in the wave's region
           if (r < a.wcap) {
@@ -989,7 +1012,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint32_t hs = __shfl(hx, (int)(js & 63));
       const int lm = r >> 6;                             // m's line (-1: previous tile's line 63)
       const uint32_t hm0 = __shfl(hx, lm & 63);
-      const uint32_t hm = lm < 0 ? (F1 ? hxp_s : hxp) : hm0;
+      const uint32_t hm = lm < 0 ? ((F1 || SCARRY) ? hxp_s : hxp) : hm0;
       if (FULL ? count + __popcll(cm) > a.cap : wtotal + count + __popcll(cm) > a.wcap) ovf = true;
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
@@ -1019,6 +1042,10 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           : [m] "s"(1ull << 63), [a] "v"(win_lds), [p] "v"(u32x4{d[12], d[13], d[14], d[15]})
           : "memory");
       hxp_s = __builtin_amdgcn_readlane(hx, 63);
+    } else if constexpr (SCARRY) {
+      hxp_s = __builtin_amdgcn_readlane(hx, 63);
+#pragma unroll
+      for (int j = 0; j < 4; j++) carry_s[j] = __builtin_amdgcn_readlane(d[12 + j], 63);
     } else if (lane == 63) {
 #pragma unroll
       for (int j = 0; j < 4; j++) win[j] = d[12 + j];
@@ -1129,6 +1156,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     process(k, A, std::true_type{});
   }
 
+  if constexpr (MEMONLY) {
+    if (memonly_acc == 0x12345678u) a.counters[3] = memonly_acc;  // (keeps the loads)
+  }
   // ---- epilogue: per-wave results; the last block to finish reduces them
   // (cdna guide: plain stores, vmcnt(0), barrier, lane-0 agent release, add;
   // the last block acquires before reading) ----

@@ -44,6 +44,17 @@ __device__ __forceinline__ uint32_t mul16k_u(uint32_t v) {
 }
 // v * x^32768 (one 4 KiB block) = two x^16384 steps
 __device__ __forceinline__ uint32_t mul_tile_u(uint32_t v) { return mul16k_u(mul16k_u(v)); }
+// a table word at a wave-uniform index, by a scalar load
+__device__ __forceinline__ uint32_t tab_u(const uint32_t* p) {
+  return *(const __attribute__((address_space(4))) uint32_t*)p;
+}
+// x^(8 n) mod P for a wave-uniform n (xpow8_dev with scalar table loads)
+__device__ __forceinline__ uint32_t xpow8_u(uint64_t n) {
+  uint32_t r = kX0;
+  for (int k = 0; n; k++, n >>= 1)
+    if (n & 1) r = mulp(tab_u(&g_tabs.pow8[k]), r);
+  return r;
+}
 
 // 64 readable bytes for the lanes whose line is no whole in-bounds payload
 // line (their bytes are read one by one instead): the payload ring's loads
@@ -89,6 +100,22 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
 
   uint64_t i = 0, b = 0, khl = 0, gend = 0;
   srd_write_entry e;
+  // the wave's entry descriptors by SCALAR loads (constant address space: the
+  // table is read-only here): as vector loads they joined the ring's vmcnt
+  // queue and their wait drained it -- the previous unit's stores included
+  auto ent_s = [&](uint64_t k) {
+    const __attribute__((address_space(4))) uint64_t* q =
+        (const __attribute__((address_space(4))) uint64_t*)(a.ent + k);
+    srd_write_entry x;
+    x.src = q[0];
+    x.len = q[1];
+    x.key_src = q[2];
+    x.tail = q[3];
+    const uint64_t kf = q[4];
+    x.key_len = (uint32_t)kf;
+    x.flags = (uint32_t)(kf >> 32);
+    return x;
+  };
   uint32_t acc = 0, any = 0;
   // one unit of the sequence: block b of entry i (a tombstone is one unit
   // without a block); returns whether a next unit exists in the group (its
@@ -101,37 +128,40 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
     if (b2 >= nb) {
       i2 = i + W;
       b2 = 0;
-      if (i2 < gend) e2 = a.ent[i2];
+      if (i2 < gend) e2 = ent_s(i2);
     }
     const bool more = i2 < gend;
     load_blk(e2, b2, nx);  // (past the group: a block of this entry again, or the dummy -- harmless)
     const int jl = (int)(((i - w) / W) % 64);  // the entry's lane in khl
     const uint64_t kh = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(khl >> 32), jl) << 32) |
                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)khl, jl);
-    bool done = false;
-    uint32_t crc = 0;
-    uint64_t mo = 0;
-    if (tomb) {
-      // tombstone: the single NULL byte, no prepad (data_store.rs:864-897)
-      if (lane == 0) a.out[e.tail - a.base] = 0;
-      crc = 0xD202EF8Du;  // CRC32(b"\0")
-      mo = e.tail + 1;
-      done = true;
-    } else {
-      const uint64_t pad = prepad64(e.tail), st = e.tail + pad;  // data_store.rs:907-914
+    // Every store of a unit is an UNCONDITIONAL buffer store whose unused
+    // lanes fall outside the descriptor's range (dropped by the hardware):
+    // stores under a branch made the count of memory ops between a block's
+    // loads and their wait path-dependent, and the ring's wait then also
+    // waited for the previous unit's stores to complete (the scan's rule)
+    const uint64_t pad = tomb ? 0 : prepad64(e.tail), st = e.tail + pad;  // data_store.rs:907-914
+    // the zero bytes before the payload: the prepad on an entry's first
+    // block, the single NULL byte of a tombstone (data_store.rs:864-897)
+    // (an entry's prepad is written by the wave of the batch's previous entry,
+    // with that entry's metadata -- one whole line instead of two partial
+    // ones from two waves; only the batch's first entry writes its own)
+    const uint32_t nz = tomb ? 1u : (b == 0 && i == 0 ? (uint32_t)pad : 0u);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, out_rsrc(a.out + (e.tail - a.base), nz), (uint32_t)lane, 0, 0);
+    bool done = tomb;
+    uint32_t crc = 0xD202EF8Du;  // CRC32(b"\0")
+    uint64_t mo = e.tail + 1;
+    if (!tomb) {
       uint8_t* dst = a.out + (st - a.base);  // 64-aligned when out is
       if (b == 0) {
-        if ((uint64_t)lane < pad) a.out[e.tail - a.base + lane] = 0;
         acc = 0;
         any = 0;
       }
       const uint64_t o = b * TILE + 64ull * lane;
-      if (vec_line(e, b)) {
-        u32x4* q = (u32x4*)(dst + o);
-#pragma unroll
-        for (int j = 0; j < 4; j++) q[j] = u32x4{d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]};
-      } else {
+      const bool vec = vec_line(e, b);
+      if (!vec) {
         // a partial (or unaligned) line: byte by byte, zero past the payload
+        // (extra memory ops on this path only: the ring's waits stay right)
         const uint32_t nl = o < e.len ? (uint32_t)min<uint64_t>(64, e.len - o) : 0u;
         const uint8_t* src = a.pay + e.src;
 #pragma unroll
@@ -141,6 +171,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
           dst[o + q] = v;
           d[q >> 2] |= (uint32_t)v << (8 * (q & 3));
         }
+      }
+      {
+        const __amdgpu_buffer_rsrc_t rb = out_rsrc(dst + b * TILE, TILE);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]}, rb,
+                                                 vec ? 64u * lane + 16u * j : OOB_OFF, 0, 0);
       }
 #pragma unroll
       for (int j = 0; j < 16; j++) any |= d[j];
@@ -152,26 +189,37 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
       if (b + 1 == nb) {
         if (a.null_only && !__ballot(any != 0) && lane == 0) atomicOr(a.null_only, 1u);
         const uint64_t z = nb * TILE - e.len;  // trailing zero padding of the last block, < 4096
-        if (z) acc = mulp(g_tabs.invpow[z], acc);
+        // (uniform values: scalar table loads, which leave the ring's vmcnt queue alone)
+        if (z) acc = mulp(tab_u(&g_tabs.invpow[z]), acc);
         if (e.len != last_len) {
           last_len = e.len;
-          last_fix = ~mulp(xpow8_dev(e.len), 0xFFFFFFFFu);
+          last_fix = ~mulp(xpow8_u(e.len), 0xFFFFFFFFu);
         }
         crc = acc ^ last_fix;  // crc32fast: init and xorout 0xFFFFFFFF
         mo = st + e.len;
         done = true;
       }
     }
-    if (done) {
-      // EntryMetadata::serialize: key_hash LE, prev_offset LE, checksum LE
-      if (lane < 20) {
-        const uint64_t v = lane < 8 ? kh : lane < 16 ? e.tail : (uint64_t)crc;
-        a.out[mo - a.base + lane] = (uint8_t)(v >> (8 * (lane & 7)));
+    // EntryMetadata::serialize: key_hash LE, prev_offset LE, checksum LE
+    // (bytes 0-19, one per lane), then the zero prepad of the batch's next
+    // entry up to its payload start (data_store.rs:907-914; a tombstone has
+    // none), so the line holding both is written whole by this wave; the
+    // (key_hash, metadata offset) pair
+    {
+      uint64_t next_start = mo + 20;
+      if (i + 1 < a.n) {
+        const srd_write_entry en = ent_s(i + 1);  // en.tail == mo + 20
+        next_start = (en.flags & SRD_ENTRY_TOMB) ? en.tail : en.tail + prepad64(en.tail);
       }
-      if (lane == 0) {
-        a.kh_out[i] = kh;
-        a.mo_out[i] = mo;
-      }
+      const uint32_t nb_meta = done ? (uint32_t)(next_start - mo) : 0u;  // 20 .. 83
+      const uint64_t v = lane < 8 ? kh : lane < 16 ? e.tail : (uint64_t)crc;
+      const __amdgpu_buffer_rsrc_t rm = out_rsrc(a.out + (mo - a.base), nb_meta);
+      __builtin_amdgcn_raw_buffer_store_b8(lane < 20 ? (uint8_t)(v >> (8 * (lane & 7))) : (uint8_t)0, rm, (uint32_t)lane, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rm, 64u + (uint32_t)lane, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)kh, (uint32_t)(kh >> 32)}, out_rsrc(a.kh_out + i, done ? 8u : 0u),
+                                            8u * lane, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)mo, (uint32_t)(mo >> 32)}, out_rsrc(a.mo_out + i, done ? 8u : 0u),
+                                            8u * lane, 0, 0);
     }
     i = i2;
     b = b2;
@@ -193,7 +241,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
     gend = min(a.n, g0 + 64 * W);
     i = g0;
     b = 0;
-    e = a.ent[i];
+    e = ent_s(i);
     load_blk(e, 0, cur);
     // the ring: two register blocks, the roles swapped every unit
     while (step(cur, nxt) && step(nxt, cur)) {
