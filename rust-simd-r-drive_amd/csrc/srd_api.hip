@@ -164,7 +164,6 @@ struct Ctx {
   // the last srd_ctx_timings read (scan_last: srd_ctx_scan_list)
   std::vector<float> scan_list, scan_last;
   // sync-free optimistic pass
-  uint64_t capK = 0;    // dense candidate capacity (grows on ST_CAPK)
   uint32_t gen = 0;     // generation tag of has_child / childof
   uint64_t last_n = 0;  // chain length of the previous call (index bucket sizing)
   Plan* h_plan = nullptr;  // pinned host copy
@@ -213,7 +212,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
-  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN,
+  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN, B_DEFER,
   B_COUNT_
 };
 
@@ -363,6 +362,11 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
   } else if (a.variant == 9) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 9>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 9>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 11) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 11>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 11>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 12) {
+    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 12>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 10) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 10>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 10>, grid, block, 0, s, e0, e1, 0, a);
@@ -538,7 +542,7 @@ static void scan_weights(uint32_t (&wq)[16]) {
 }
 #ifdef SRD_DEBUG_API  // timing builds: A/B of scan variants inside one context (one workspace)
 extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
-  if (!c || v < 0 || v > 10) return SRD_ERR_ARG;
+  if (!c || v < 0 || v > 12) return SRD_ERR_ARG;
   c->scan_variant = (uint32_t)v;
   return 0;
 }
@@ -1079,9 +1083,8 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
 // device; one host sync at the end.  *done=false sends the call to the full
 // pass (the check could not prove the chain from file_len).
 static int alloc_fast(Ctx* c, uint64_t capK, uint32_t log2_nbk) {
-  TRY(ensure(c, B_DM, capK * 8));
-  TRY(ensure(c, B_DPAR, capK * 8));
-  TRY(ensure(c, B_DSLOT, capK * 8));
+  TRY(ensure(c, B_DPAR, capK * 4));
+  TRY(ensure(c, B_DEFER, capK * 4));
   TRY(ensure_z(c, B_HASCHILD, capK * 4));
   TRY(ensure_z(c, B_HASCHILD2, capK * 4));
   TRY(ensure_z(c, B_CHILDOF, capK * 8));
@@ -1109,11 +1112,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
   const uint32_t coff = lo ? 0u : 1u;
   fit_cap(c->copt, flen - span_off);
   for (int attempt = 0; attempt < 6; attempt++) {
-    if (!c->capK) c->capK = (flen - span_off) / 1024 + 4096;
-    const uint64_t capK = c->capK;
-    // capacity exhausted (dense small-entry stores): not provable here, the
-    // full pass (whole file) decides / the span is reported unproven
-    if (capK >= (1ull << 31)) { c->capK = 0; return 0; }
     // index buckets: ~IDX_BUCKET_AVG chain entries per bucket
     const uint64_t n_est = std::max<uint64_t>(std::max<uint64_t>(c->last_n, (flen - span_off) / 4096), 1);
     const uint32_t log2_nbk = index_log2_buckets(n_est);
@@ -1124,8 +1122,12 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
     const uint64_t spw = part_max_wave_spans(part);
     const uint64_t wcap = spw * c->copt.cap;
-    // the glue's record slots are 32-bit (d_slot): stores above ~1 TiB take the full pass
-    if (total_waves * wcap >= (1ull << 32)) return 0;
+    // the glue works in slot space (slot = wave * wcap + record): its parent
+    // words are 31-bit; stores above ~1 TiB (or a denser cap) take the full pass
+    const uint64_t capK = total_waves * wcap;
+    if (capK >= (1ull << 31)) return 0;
+    const uint32_t wpb = (uint32_t)((total_waves + CHAIN_BLOCKS - 1) / CHAIN_BLOCKS);  // scan waves per chain block
+    if (wpb > BW_MAX) return 0;
     TRY(alloc_scan(c, nt_rel, std::max<uint64_t>(ns_rel, total_waves * spw), c->copt.cap));
     TRY(ensure(c, B_SPAN_FIRST, (ns_rel + 1) * 4));
     TRY(alloc_fast(c, capK, log2_nbk));
@@ -1163,6 +1165,14 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.zero_words = (uint32_t*)pl;
     a.n_zero_words = (uint32_t)(sizeof(Plan) / 4);
     a.sentinel = nullptr;
+    // the link phase (every node claims its parent) and the index bucket fills
+    // chain_finalize claims (zeroed by block 0)
+    a.d_par = P<int32_t>(c, B_DPAR);
+    a.childof = P<unsigned long long>(c, B_CHILDOF);
+    a.gen = c->gen;
+    a.span_lo = lo;
+    a.defer = P<uint32_t>(c, B_DEFER);
+    a.zero2 = index_zero_words(c, log2_nbk, &a.n_zero2);
     TRY(scan_wave_args(c, &a));
     hipEvent_t e0, e1;
     TRY(next_scan_events(c, &e0, &e1));
@@ -1176,28 +1186,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       return 0;
     }
 #endif
-    Link2Args l{};
-    l.file = d_file;
-    l.flen = flen;
-    l.n_spans = n_spans;
-    l.capK = capK;
-    l.gen = c->gen;
-    l.span_count = a.span_count;
-    l.span_first = a.span_first;
-    l.wave_base = a.wave_base;
-    l.wave_total = a.wave_total;
-    l.part = part;
-    l.wcap = wcap;
-    l.c_m = a.c_m;
-    l.c_rec = a.c_rec;
-    l.d_par = P<int32_t>(c, B_DPAR);
-    l.d_slot = P<uint32_t>(c, B_DSLOT);
-    l.childof = P<unsigned long long>(c, B_CHILDOF);
-    l.s_lo = s_lo;
-    l.span_lo = lo;
-    l.zero = index_zero_words(c, log2_nbk, &l.n_zero);  // chain_finalize claims the bucket fills
-    link2_kernel<<<(unsigned)total_waves, 256, 0, c->stream>>>(l);  // one block per scan wave
-    KCHK(c, "link2_kernel");
     // ---- shape check, chain, finalize, index; retried on device with more
     //      prune rounds when false candidates chained onto each other ----
     Plan hp{};
@@ -1209,13 +1197,16 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       ShapeArgs sa{};
       sa.file = d_file;
       sa.flen = flen;
-      sa.capK = capK;
       sa.Kp = a.k_total;
+      sa.wave_total = a.wave_total;
+      sa.wcap = wcap;
+      sa.n_waves = (uint32_t)total_waves;
+      sa.wpb = wpb;
+      sa.n_slots = capK;
       sa.coff = coff;
-      sa.c_m = l.c_m;
-      sa.d_par = l.d_par;
-      sa.d_slot = l.d_slot;
-      sa.c_rec = l.c_rec;
+      sa.c_m = a.c_m;
+      sa.d_par = a.d_par;
+      sa.c_rec = a.c_rec;
       sa.childof = P<uint64_t>(c, B_CHILDOF);
       sa.flag = P<uint8_t>(c, B_FLAG);
       sa.part = P<uint32_t>(c, B_PART);
@@ -1225,12 +1216,12 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       sa.plan = pl;
       sa.zero = index_zero_words(c, log2_nbk, &sa.n_zero);  // child2 zeroes the index's bucket fills
       if (rounds == 0) {
-        // round 0: link2's claims (every node claims its parent) are the
+        // round 0: the link phase's claims (every node claims its parent) are the
         // core flags and the branch test; no marks
         sa.has_child = nullptr;
         sa.gen = mgen;
       } else {
-        if (rounds == 2) {  // the retry's first marks: the nodes link2 claims were made on
+        if (rounds == 2) {  // the retry's first marks: the nodes the link claims were made on
           sa.gen = mgen;
           marks_from_claims_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa, marks);
           KCHK(c, "marks_from_claims_kernel");
@@ -1256,8 +1247,8 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       FinArgs f{};
       f.file = d_file;
       f.flen = flen;
-      f.c_m = l.c_m;
-      f.c_rec = l.c_rec;
+      f.c_m = a.c_m;
+      f.c_rec = a.c_rec;
       f.tile = a.tile;
       f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
       f.coff = coff;
@@ -1334,10 +1325,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     if (hp.status & ST_OVERFLOW) {
       if (c->copt.cap >= SPAN_BYTES) return 0;  // cannot happen (<= one candidate per byte); not provable here
       grow_cap(c->copt, flen - span_off);
-      continue;
-    }
-    if (hp.status & ST_CAPK) {
-      c->capK = hp.cap_need + hp.cap_need / 4 + 4096;
       continue;
     }
     if (hp.status) return 0;  // not provable here -> full pass (whole file) / unproven (span)

@@ -6,14 +6,16 @@
 // waits once, on the outcome idx_emit publishes to pinned host memory:
 //
 //   scan            (srd_kernels.hip) strong candidates only, each wave's
-//                   records dense in its region (ScanPart), wave bases by the
-//                   scan's last block; block 0 zeroes the plan
-//   link2           one block per scan wave over its dense record region:
-//                   node test of single-candidate records, parent lookup
-//                   (previous record, else a binary search in the parent's
-//                   span), 32-bit d_par / d_slot, and every node claims its
-//                   parent (the earliest claimer wins, claim_word); zeroes
-//                   the index bucket fills
+//                   records dense in its region (ScanPart); then every block
+//                   links its own records (link_record: node test of
+//                   single-candidate records, parent lookup -- the previous
+//                   record, else a binary search in the parent's span -- and
+//                   the claim on the parent, the earliest claimer winning,
+//                   claim_word) while slower blocks still scan; the last
+//                   block links the records that needed another block's
+//                   waves.  Slot space throughout: record r of wave w is
+//                   slot w*wcap + r.  Block 0 zeroes the plan and the index
+//                   bucket fills
 //   check           shape test from the claims alone: the core nodes (claimed
 //                   by someone, or the start node at file_len - 20) must form
 //                   ONE chain from the start down to a root -- each core node's
@@ -61,14 +63,13 @@ struct Plan {
   uint64_t n_slow;     // finalize entries handed to slow_kernel
   uint64_t chain_core; // core nodes (n_chain - 1 on success)
   uint64_t max_root, top_gap, overflow;  // the scan counters; top_gap = file_len - the start tail (find_top)
-  uint64_t cap_need;   // K when it exceeds the dense capacity
   uint32_t status;     // ST_* bits; 0 = the optimistic result is final
   uint32_t nroot;      // core nodes linking to a root
   uint32_t troot;      // file_len itself is a root tail
   uint32_t idx_overflow;
   uint32_t idx_alias;  // every chain entry is its key's latest: the index IS (o_kh, o_packed) (idx_emit)
 };
-constexpr uint32_t ST_NOSTART = 1, ST_SHAPE = 2, ST_ROOTS = 4, ST_CAPK = 8, ST_OVERFLOW = 16;
+constexpr uint32_t ST_NOSTART = 1, ST_SHAPE = 2, ST_ROOTS = 4, ST_OVERFLOW = 16;
 constexpr uint64_t NO_NODE = ~0ull;
 
 constexpr int GLUE_BLOCKS = 1024;  // chunked grid of the count/scatter kernels
@@ -184,126 +185,20 @@ __device__ uint64_t block_scan_partials(const uint32_t* part, uint32_t np, uint3
   return total;
 }
 
-// --------------------------------------------------------------------------
-// A claim on a parent: the generation in the high word (stale words of
-// earlier calls lose any atomicMax), ~g in the low word, so the claimer with
-// the SMALLEST dense index holds the parent.  The real child of p is the
-// first node after p in file order; a false candidate that resolves to p
-// lies later (C3: a candidate 8 bytes past some metadata reads that entry's
-// CRC as its prev field, and one in ~7000 such CRCs equals a real tail below
-// 4 GiB) -- with the largest claimer winning it took the parent from the real
-// child, and every C3 call went through the retry rounds.
-__device__ __forceinline__ unsigned long long claim_word(uint32_t gen, uint64_t g) {
-  return ((unsigned long long)gen << 32) | (0xffffffffull - (g & 0xffffffffull));
-}
-
-struct Link2Args {
-  const uint8_t* file;
-  uint64_t flen, n_spans, capK;
-  uint32_t gen;
-  const uint32_t* span_count;
-  const uint32_t* span_first;  // scan_kernel: span's first record inside its wave's region
-  const uint64_t* wave_base;   // scan_kernel's last block: dense index of each scan wave's first record
-  const uint64_t* wave_total;  // records per scan wave (bit 63: overflow)
-  ScanPart part;               // the scan's wave partition (span -> wave)
-  uint64_t wcap;               // record slots per scan wave
-  const uint64_t* c_m;
-  u32x4* c_rec;  // tombstone flags are set in place
-  int32_t* d_par;              // dense parent (PAR_ROOT / PAR_MISS)
-  uint32_t* d_slot;            // dense node -> record slot (< 2^32: the host checks)
-  unsigned long long* childof; // [capK] (gen << 32) | child: every node claims its parent (atomicMax)
-  uint64_t s_lo;     // first resident span (span mode)
-  uint64_t span_lo;  // span mode: the shard's lower tail (a node with p == span_lo is the shard's first entry); 0 = whole file
-  uint32_t* zero;    // zeroed here: the index's bucket fills (chain_finalize claims them)
-  uint32_t n_zero;
-};
-
-// One block per scan wave: the wave's records are dense in file order in its
-// region (record r at slot w*wcap + r, dense index wave_base[w] + r), so the
-// block walks them directly -- no per-span lanes, no span -> wave search
-// except in the parent-search fallback.  (4 lanes per span took 1.1 ms at
-// C3, whose 4.4M spans are mostly empty.)
-//
-// Every node with a parent claims it: childof[p] = max(claim_word(gen, g)).
-// check_kernel reads a node's core flag (someone links to it) and the claim
-// on its parent from these words alone -- no separate marking pass.  A
-// parent claimed by two nodes keeps the larger; if the loser is a chain node
-// the shape check fails and the retry rounds (prune + core-only claims)
-// decide, so the claim order never changes a result.
-__global__ __launch_bounds__(256) void link2_kernel(Link2Args a) {
-  {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
-    for (uint32_t i = t; i < a.n_zero; i += nt) a.zero[i] = 0;
-  }
-  const uint64_t w = blockIdx.x;
-  // records past wcap were not stored (wave overflow: chain_finalize reports ST_OVERFLOW)
-  const uint64_t nrec = min(a.wave_total[w] & ~(1ull << 63), a.wcap);
-  const uint64_t gw = w * a.wcap, gb = a.wave_base[w];
-  for (uint64_t r = threadIdx.x; r < nrec; r += blockDim.x) {
-    const uint64_t gi = gw + r, g = gb + r;
-    if (g >= a.capK) return;  // chain_finalize reports ST_CAPK
-    const uint64_t m = a.c_m[gi];
-    const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
-    // the previous record in file order: the slot before (same wave), else
-    // the previous wave's last record
-    uint64_t mprev = 0;
-    bool hp = true;
-    if (r > 0) {
-      mprev = a.c_m[gi - 1];
-    } else {
-      const uint64_t wt = w ? (a.wave_total[w - 1] & ~(1ull << 63)) : 0;
-      hp = wt > 0 && wt <= a.wcap;
-      if (hp) mprev = a.c_m[(w - 1) * a.wcap + wt - 1];
-    }
-    const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-    bool node = true;
-    if (r1[3] & F_NT) {
-      // single-candidate record, deferred node test (data_store.rs:404-470);
-      // F_ZB is the byte at m - 1, the tombstone byte when p == m - 1
-      const uint64_t dp = m - p;
-      const bool tomb = dp == 1 && (r1[3] & F_ZB);
-      node = p >= 20 && p < m && (tomb || dp > prepad64(p));
-      if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
-    }
-    const uint64_t mp = p - 20;  // p >= 20 for nodes
-    const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // scan_kernel: span s holds m in [16 KiB s - 14, +16 KiB)
-    // In a store without garbage the parent is the previous record in file
-    // order: one load instead of a binary search.
-    int64_t par = hp && mprev == mp ? (int64_t)(g - 1) : PAR_MISS;
-    if (node && par == PAR_MISS && sp2 >= a.s_lo && sp2 < a.n_spans) {
-      const uint64_t w2 = part_span_wave(a.part, sp2 - a.s_lo);
-      const uint32_t f2 = a.span_first[sp2];
-      const uint32_t n2 = (uint32_t)min<uint64_t>(a.span_count[sp2], a.wcap - min<uint64_t>(f2, a.wcap));
-      uint32_t lo = 0, hi = n2;
-      const uint64_t* cm = a.c_m + w2 * a.wcap + f2;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (cm[mid] < mp) lo = mid + 1; else hi = mid;
-      }
-      if (lo < n2 && cm[lo] == mp) par = (int64_t)(a.wave_base[w2] + f2 + lo);
-    }
-    if (!node) par = PAR_MISS;  // no parent, no root
-    else if (par == PAR_MISS) {
-      if (a.span_lo) {
-        if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
-      } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {
-        par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
-      }
-    }
-    GST(a.d_par[g], (int32_t)par);
-    GST(a.d_slot[g], (uint32_t)gi);
-    if (par >= 0 && (uint64_t)par < a.capK) atomicMax(&a.childof[par], claim_word(a.gen, g));
-  }
-}
-
 struct ShapeArgs {
   const uint8_t* file;
-  uint64_t flen, capK;
+  uint64_t flen;
   uint32_t gen;
-  const uint64_t* Kp;  // span_base + n_spans
-  const uint64_t* c_m;  // the records' metadata offsets (slot d_slot[g])
-  const int32_t* d_par;
-  const uint32_t* d_slot;
+  // slot space (scan_kernel's link phase): record r of scan wave w is slot
+  // w*wcap + r, r < min(wave_total[w], wcap); the chain blocks take the scan
+  // waves in order, wpb each (block_waves)
+  const uint64_t* Kp;  // [0] records, [1] 1 + the slot of the last record (0: none)
+  const uint64_t* wave_total;
+  uint64_t wcap;
+  uint32_t n_waves, wpb;
+  uint64_t n_slots;     // n_waves * wcap
+  const uint64_t* c_m;  // the records' metadata offsets
+  const int32_t* d_par;  // the parent's slot / PAR_ROOT / PAR_MISS
   const u32x4* c_rec;
   const uint32_t* has_child;  // retry rounds: the prune marks
   uint64_t* childof;
@@ -318,46 +213,74 @@ struct ShapeArgs {
   uint32_t n_zero;
 };
 
-// the dense index of the node at the start tail find_top chose (the scan's
-// counters[1]; no candidate lies above it)
-__device__ __forceinline__ uint64_t start_node(const ShapeArgs& a, uint64_t K) {
-  const uint64_t t = a.counters[1];
-  return (K && t >= 21 && a.c_m[a.d_slot[K - 1]] == t - 20) ? K - 1 : NO_NODE;
+// the slot of the node at the start tail find_top chose (the scan's
+// counters[1]; no candidate lies above it): the last record
+__device__ __forceinline__ uint64_t start_node(const ShapeArgs& a) {
+  const uint64_t t = a.counters[1], s1 = a.Kp[1];
+  return (s1 && t >= 21 && a.c_m[s1 - 1] == t - 20) ? s1 - 1 : NO_NODE;
 }
-// the dense arrays are incomplete: more candidates than the dense capacity
-// (ST_CAPK), or a record region overflowed (ST_OVERFLOW: link2 wrote no
-// parent / slot for the records past it) -- the shape kernels must not read
-// them; chain_finalize reports the status and the host retries larger
-__device__ __forceinline__ bool dense_incomplete(const ShapeArgs& a, uint64_t K) {
-  return K > a.capK || a.counters[2] != 0;
+// a record region overflowed (ST_OVERFLOW: the records past it were not
+// stored or linked) -- the shape kernels must not read the slot arrays;
+// chain_finalize reports the status and the host retries larger
+__device__ __forceinline__ bool dense_incomplete(const ShapeArgs& a) { return a.counters[2] != 0; }
+
+// Chain block b's records: scan waves [b*wpb, (b+1)*wpb) in file order,
+// flattened (s_pre: LDS[wpb + 1], the exclusive prefix of their record
+// counts); returns the block's record count.  slot_of maps a block index to
+// its slot.
+constexpr uint32_t BW_MAX = 64;  // wpb bound (the host checks)
+__device__ __forceinline__ uint32_t block_waves(const ShapeArgs& a, uint32_t* s_pre) {
+  const uint64_t w0 = (uint64_t)blockIdx.x * a.wpb;
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  if (t < 64) {
+    const uint64_t w = w0 + lane;
+    const uint32_t c = lane < a.wpb && w < a.n_waves ? (uint32_t)min(a.wave_total[w] & ~(1ull << 63), a.wcap) : 0u;
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    s_pre[lane + 1] = x;
+    if (lane == 0) s_pre[0] = 0;
+  }
+  __syncthreads();
+  return s_pre[a.wpb];
+}
+__device__ __forceinline__ uint64_t slot_of(const ShapeArgs& a, const uint32_t* s_pre, uint32_t i) {
+  uint32_t v = 0;  // the largest v < wpb with s_pre[v] <= i
+  for (uint32_t st = BW_MAX / 2; st; st >>= 1)
+    if (v + st < a.wpb && s_pre[v + st] <= i) v += st;
+  return ((uint64_t)blockIdx.x * a.wpb + v) * a.wcap + (i - s_pre[v]);
 }
 
 // Core nodes of the current round: the start node, or a node some node of
 // the previous round links to (has_child[g] == gen), whose own parent was
-// found (a record or the root rule).  Round 1's marks come from link2 (every
-// node with a found parent); each prune round keeps only the parents of the
-// previous round's core nodes, so a false chain of L candidates (a false
-// node whose "prev" happens to be another false node's tail) drops out after
-// L rounds, while an intact chain from the start node stays core throughout.
+// found (a record or the root rule).  Round 1's marks come from the link
+// phase's claims (every node with a found parent); each prune round keeps
+// only the parents of the previous round's core nodes, so a false chain of L
+// candidates (a false node whose "prev" happens to be another false node's
+// tail) drops out after L rounds, while an intact chain from the start node
+// stays core throughout.  The retry kernels run over every slot: a slot
+// without a record is never core (no claim or mark of this generation
+// reaches it -- parents are records), so its stale words are never used.
 __device__ __forceinline__ bool is_core(const ShapeArgs& a, uint64_t g, uint64_t start) {
   if (g == start) return true;
   const int64_t p = a.d_par[g];
   return a.has_child[g] == a.gen && (p >= 0 || p == PAR_ROOT);
 }
 
-// the retry's round-0 marks: the nodes link2 claims were made on
+// the retry's round-0 marks: the nodes the link phase's claims were made on
 __global__ __launch_bounds__(256) void marks_from_claims_kernel(ShapeArgs a, uint32_t* marks_out) {
-  const uint64_t K = *a.Kp;
-  if (dense_incomplete(a, K)) return;
-  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x)
+  if (dense_incomplete(a)) return;
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n_slots; g += (uint64_t)gridDim.x * blockDim.x)
     if ((a.childof[g] >> 32) == a.gen) marks_out[g] = a.gen;
 }
 
 __global__ __launch_bounds__(256) void prune_kernel(ShapeArgs a, uint32_t* marks_out, uint32_t gen_out) {
-  const uint64_t K = *a.Kp;
-  if (dense_incomplete(a, K)) return;
-  const uint64_t start = start_node(a, K);
-  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < K; g += (uint64_t)gridDim.x * blockDim.x) {
+  if (dense_incomplete(a)) return;
+  const uint64_t start = start_node(a);
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n_slots; g += (uint64_t)gridDim.x * blockDim.x) {
     const int64_t p = a.d_par[g];
     if (p >= 0 && is_core(a, g, start)) marks_out[p] = gen_out;
   }
@@ -365,9 +288,9 @@ __global__ __launch_bounds__(256) void prune_kernel(ShapeArgs a, uint32_t* marks
 
 __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_zero; i += gridDim.x * blockDim.x) a.zero[i] = 0;
-  const uint64_t K = *a.Kp;
-  if (dense_incomplete(a, K)) return;
-  const uint64_t start = start_node(a, K);
+  if (dense_incomplete(a)) return;
+  const uint64_t start = start_node(a);
+  const uint64_t K = a.n_slots;
   // CR nodes per thread per pass: loads first (no store in between)
   constexpr int CR = 4;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -402,44 +325,45 @@ __global__ __launch_bounds__(256) void child2_kernel(ShapeArgs a) {
 // start has a core child without a test of its own.  Leaves (false
 // candidates nobody links to) are ignored -- recover_valid_chain's walk only
 // follows back-pointers from file_len (data_store.rs:404-470).  Round 0
-// reads the claims link2 made (core: (childof[g] >> 32) == gen); the retry
+// reads the link phase's claims (core: (childof[g] >> 32) == gen); the retry
 // rounds, the prune marks and child2's core-only claims.
 __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
   __shared__ uint32_t wsum[CHAIN_WAVES];
-  const uint64_t K = *a.Kp;
-  if (dense_incomplete(a, K)) return;
-  const uint64_t start = start_node(a, K);
+  __shared__ uint32_t s_pre[BW_MAX + 1];
+  if (dense_incomplete(a)) return;
+  const uint64_t start = start_node(a);
   const uint64_t tag = (uint64_t)a.gen << 32;
   const bool marks = a.has_child != nullptr;  // retry rounds
-  uint64_t lo, hi;
-  chunk_of(K, &lo, &hi);
+  const uint32_t n = block_waves(a, s_pre);
   uint32_t cnt = 0;
   bool fail = false;
   // CR nodes per thread per pass, their loads issued level by level: the
   // node's own words (parent, claim), then its parent's
   constexpr int CR = 4;
-  for (uint64_t base = lo; base < hi; base += CR * CHAIN_THREADS) {
+  for (uint32_t base = 0; base < n; base += CR * CHAIN_THREADS) {
     uint64_t g[CR], cg[CR], cp[CR];
     int64_t par[CR], pp[CR];
     uint32_t hc[CR], hp[CR];
+    bool in[CR];
 #pragma unroll
     for (int r = 0; r < CR; r++) {
-      g[r] = base + (uint64_t)r * CHAIN_THREADS + threadIdx.x;
-      const uint64_t gg = g[r] < hi ? g[r] : lo;
-      par[r] = a.d_par[gg];
-      cg[r] = a.childof[gg];
-      hc[r] = marks ? a.has_child[gg] : 0u;
+      const uint32_t i = base + (uint32_t)r * CHAIN_THREADS + threadIdx.x;
+      in[r] = i < n;
+      g[r] = slot_of(a, s_pre, in[r] ? i : 0u);
+      par[r] = a.d_par[g[r]];
+      cg[r] = a.childof[g[r]];
+      hc[r] = marks ? a.has_child[g[r]] : 0u;
     }
 #pragma unroll
     for (int r = 0; r < CR; r++) {
-      const uint64_t q = par[r] >= 0 ? (uint64_t)par[r] : lo;
+      const uint64_t q = par[r] >= 0 ? (uint64_t)par[r] : g[r];
       pp[r] = a.d_par[q];
       cp[r] = a.childof[q];
       hp[r] = marks ? a.has_child[q] : 0u;
     }
 #pragma unroll
     for (int r = 0; r < CR; r++) {
-      if (g[r] >= hi) break;
+      if (!in[r]) break;
       const int64_t p = par[r];
       const bool linked = marks ? hc[r] == a.gen : (cg[r] & ~0xffffffffull) == tag;
       const bool core = g[r] == start || (linked && (p >= 0 || p == PAR_ROOT));  // is_core(g)
@@ -449,7 +373,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
       const bool plinked = marks ? hp[r] == a.gen : (cp[r] & ~0xffffffffull) == tag;
       if (p == PAR_ROOT) {
         atomicAdd(&a.plan->nroot, 1u);
-        const u32x4 r0 = a.c_rec[2 * (uint64_t)a.d_slot[g[r]]];
+        const u32x4 r0 = a.c_rec[2 * g[r]];
         a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
       } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
         fail = true;  // dangling: the chain through g is broken (only the start node can get here)
@@ -681,6 +605,7 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
 __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs a, FinArgs f, IdxArgs ia,
                                                                       uint32_t log2_nbk) {
   __shared__ uint32_t wsum[CHAIN_WAVES * FIN_R];
+  __shared__ uint32_t s_pre[BW_MAX + 1];
   __shared__ FinLds lt;
   uint32_t* const tab = lt.tab;
   __shared__ uint32_t slowq[CHAIN_THREADS * FIN_R];
@@ -698,10 +623,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   for (int j = 0; j < 4; j++) r_inv[j] = g_tabs.invpow[ti + 1024 * j];
   const uint32_t r_inv_last = g_tabs.invpow[4096];
   const uint32_t r_winit = g_tabs.winit[ti & 63], r_zc = g_tabs.zero_crc[ti & 63];
-  const uint64_t K = *a.Kp;
-  const bool capk = K > a.capK;
+  const uint64_t K = a.Kp[0];
+  const bool incomplete = dense_incomplete(a);
   uint64_t before = 0, total = 0;
-  block_prefix_n<CHAIN_WAVES>(a.part, capk ? 0u : (uint32_t)CHAIN_BLOCKS, wsum, &before, &total);
+  block_prefix_n<CHAIN_WAVES>(a.part, incomplete ? 0u : (uint32_t)CHAIN_BLOCKS, wsum, &before, &total);
   Plan* pl = a.plan;
   uint32_t st = pl->status;  // check_kernel's shape bits
   // whole file only: the start tail is itself a root tail (prev 0): one
@@ -709,9 +634,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   const uint64_t top = a.counters[1];
   const bool troot = a.coff && top >= 21 && ld_u64_unaligned(a.file, top - 12) == 0;
   const uint64_t root_t = troot ? top : pl->root_t;
-  if (capk) st |= ST_CAPK;
   if (a.counters[2]) st |= ST_OVERFLOW;
-  const uint64_t start = dense_incomplete(a, K) ? NO_NODE : start_node(a, K);
+  const uint64_t start = incomplete ? NO_NODE : start_node(a);
   if (start == NO_NODE) st |= ST_NOSTART;
   if (pl->nroot != 1) st |= ST_ROOTS;
   __syncthreads();  // this block has read pl->status / nroot / root_t before block 0 rewrites them
@@ -728,7 +652,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       pl->root_t = top;
       pl->chain_core = 0;
     } else {
-      if (capk) pl->cap_need = K;
       pl->start = start;
       pl->status = st;
       pl->chain_core = total;
@@ -758,31 +681,21 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   }
   uint64_t run = a.coff + before;  // this block's next chain position
   if (!troot) {
-    uint64_t lo, hi;
-    chunk_of(K, &lo, &hi);
+    const uint32_t n = block_waves(a, s_pre);
     const u32x4* t4 = (const u32x4*)f.tile;
-    for (uint64_t base = lo; base < hi; base += CHAIN_THREADS * FIN_R) {
+    for (uint32_t base = 0; base < n; base += CHAIN_THREADS * FIN_R) {
       bool fl[FIN_R];
-      uint64_t g[FIN_R], gi[FIN_R];
+      uint64_t gi[FIN_R], kh[FIN_R];
       int64_t par[FIN_R];
       FinIn e[FIN_R];
-      // level 1-2: core flag, parent, record slot (indices of idle lanes: 0)
+      // level 1: core flag, parent and the record itself, all at the record's
+      // slot (idle lanes: the block's first record)
 #pragma unroll
       for (int r = 0; r < FIN_R; r++) {
-        g[r] = base + (uint64_t)r * CHAIN_THREADS + threadIdx.x;
-        fl[r] = g[r] < hi && a.flag[g[r] < hi ? g[r] : lo];
-        if (!fl[r]) g[r] = 0;
-      }
-#pragma unroll
-      for (int r = 0; r < FIN_R; r++) {
-        par[r] = a.d_par[g[r]];
-        gi[r] = a.d_slot[g[r]];
-      }
-      // level 3: the records and the parent's record slot
-      uint64_t pgi[FIN_R], kh[FIN_R];
-#pragma unroll
-      for (int r = 0; r < FIN_R; r++) {
-        pgi[r] = a.d_slot[par[r] >= 0 ? (uint64_t)par[r] : 0];
+        const uint32_t i = base + (uint32_t)r * CHAIN_THREADS + threadIdx.x;
+        gi[r] = slot_of(a, s_pre, i < n ? i : 0u);
+        fl[r] = i < n && a.flag[gi[r]];
+        par[r] = a.d_par[gi[r]];
         e[r].mo = f.c_m[gi[r]];
         const u32x4 r0 = f.c_rec[2 * gi[r]], r1 = f.c_rec[2 * gi[r] + 1];
         e[r].p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
@@ -793,13 +706,13 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       }
       uint32_t rank[FIN_R];
       const uint32_t tot = block_rank_rounds<CHAIN_WAVES, FIN_R>(fl, wsum, rank);
-      // level 4: the parent's record, the tile values and table words.  k0
+      // level 2: the parent's record, the tile values and table words.  k0
       // (the entry's start tile) is resident: start >= p >= the span's lower
       // tail in span mode.  A root-linked candidate (par == PAR_ROOT) has no
       // parent record: its suffix comes from the per-tile values (start 0)
 #pragma unroll
       for (int r = 0; r < FIN_R; r++) {
-        const u32x4 pr1 = f.c_rec[2 * (par[r] >= 0 ? pgi[r] : 0) + 1];
+        const u32x4 pr1 = f.c_rec[2 * (fl[r] && par[r] >= 0 ? (uint64_t)par[r] : gi[r]) + 1];
         e[r].pfl = par[r] >= 0 ? pr1[3] : (3u << F_SUF_SHIFT);
         e[r].psuf = pr1[2];
         // idle lanes read the last tile's values (resident in span mode too)

@@ -48,7 +48,7 @@ constexpr int F_SUF_SHIFT = 3;        // 2 bits: 0 value, 1 next-tile T, 2 next-
 // the recorded sxm / suf value is a lower-half partial (line < 32): true value =
 // mul16k(v) ^ SX_32 of the tile holding m (sxm) or the entry start (suf kind 0) -- see lo_fix()
 constexpr uint32_t F_SXM_LO = 32u, F_SUF_LO = 64u;
-// single-candidate record of the optimistic scan: link2_kernel applies the
+// single-candidate record of the optimistic scan: link_record applies the
 // node test (F_NT); F_ZB = the byte at m - 1 is 0 (the tombstone rule's byte
 // when p == m - 1)
 constexpr uint32_t F_NT = 256u, F_ZB = 512u;
@@ -74,7 +74,7 @@ __device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]
                                                 // [8192 + 256 + b]: its tables loaded; [8192 + 1023]: the epilogue's end
 #endif
 
-// The scan's wave partition (both passes; link2 inverts it).  Block b of g
+// The scan's wave partition (both passes; link_record inverts it).  Block b of g
 // takes the resident spans [st(b), st(b+1)), st(b) = b*ns/g; inside a block
 // wave v takes the share [cw(v), cw(v+1)) (units of 1/65536) of the block's
 // spans.  Waves of one SIMD do not progress equally: the SIMD issues for
@@ -156,6 +156,18 @@ struct ScanArgs {
   // (the full pass keeps span*cap + slot)
   uint32_t* span_first;
   uint64_t wcap;
+  // optimistic pass (d_par != nullptr): every block links its own waves'
+  // records once its tiles are done (link_record, in slot space: record r of
+  // wave w is slot w*wcap + r), hidden under the other blocks' scan; a record
+  // that needs a wave of another block goes to defer[] (count: done[1]) and
+  // the last block links it.  k_total[1] = 1 + the slot of the last record (0: none)
+  int32_t* d_par;                  // [slots] the parent's slot, PAR_ROOT or PAR_MISS
+  unsigned long long* childof;     // [slots] claims on parents (claim_word)
+  uint32_t gen;                    // this call's claim generation
+  uint64_t span_lo;                // span mode: the shard's lower tail (0 = whole file)
+  uint32_t* defer;                 // [slots]
+  uint32_t* zero2;                 // zeroed by block 0 as well: the index's bucket fills
+  uint32_t n_zero2;
   // host-side only: the scan variant to launch (0 = the build's default;
   // SRD_DEBUG_API builds A/B the others inside one context)
   uint32_t variant;
@@ -179,6 +191,18 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* f, uint64_t 
   return v;
 }
 __device__ __forceinline__ uint64_t prepad64(uint64_t o) { return (64 - (o & 63)) & 63; }
+
+// A claim on a parent: the generation in the high word (stale words of
+// earlier calls lose any atomicMax), ~g in the low word, so the claimer with
+// the SMALLEST slot (file order) holds the parent.  The real child of p is
+// the first node after p in file order; a false candidate that resolves to p
+// lies later (C3: a candidate 8 bytes past some metadata reads that entry's
+// CRC as its prev field, and one in ~7000 such CRCs equals a real tail below
+// 4 GiB) -- with the largest claimer winning it took the parent from the real
+// child, and every C3 call went through the retry rounds.
+__device__ __forceinline__ unsigned long long claim_word(uint32_t gen, uint64_t g) {
+  return ((unsigned long long)gen << 32) | (0xffffffffull - (g & 0xffffffffull));
+}
 // the 20-byte metadata record at m (entry_metadata.rs:75-112), any alignment;
 // reads the dwords covering [m, m + 20) (the buffer is padded past file_len)
 __device__ __forceinline__ void ld_meta(const uint8_t* f, uint64_t m, uint64_t* kh, uint64_t* p, uint32_t* crc) {
@@ -515,6 +539,70 @@ __device__ __forceinline__ uint64_t find_top(const uint8_t* file, uint64_t flen,
 // by SRD_DEBUG_API builds: 1 = F1 flipped, 2 = F1 flipped with its staging
 // and node test after the CRC at priority 2, 3 = the line CRC as two 32-byte
 // chains)
+// Link record r of scan wave w (slot w*wcap + r; the optimistic pass, after
+// the scan): the deferred node test of a single-candidate record
+// (data_store.rs:404-470), its parent -- the previous record in file order
+// when that record's metadata sits at p - 20, else a binary search in the
+// parent's span -- and the claim on it (the earliest claimer wins).  Waves
+// [wlo, whi) are readable; false = the record needs another wave (nothing
+// was written: the caller defers it).
+__device__ bool link_record(const ScanArgs& a, uint64_t w, uint64_t r, uint64_t wlo, uint64_t whi) {
+  const uint64_t gi = w * a.wcap + r;
+  uint64_t gprev = 0;
+  bool hp = true;
+  if (r > 0) {
+    gprev = gi - 1;
+  } else if (w == 0) {
+    hp = false;  // the first resident record: nothing before it is resident
+  } else {
+    if (w - 1 < wlo) return false;
+    const uint64_t wt = a.wave_total[w - 1] & ~(1ull << 63);
+    hp = wt > 0 && wt <= a.wcap;  // an overflowed wave fails the pass anyway (ST_OVERFLOW)
+    gprev = (w - 1) * a.wcap + (hp ? wt - 1 : 0);
+  }
+  const uint64_t m = a.c_m[gi], mprev = hp ? a.c_m[gprev] : 0;
+  const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
+  const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+  bool node = true, tomb = false;
+  if (r1[3] & F_NT) {
+    // single-candidate record, deferred node test; F_ZB is the byte at m - 1,
+    // the tombstone byte when p == m - 1
+    const uint64_t dp = m - p;
+    tomb = dp == 1 && (r1[3] & F_ZB);
+    node = p >= 20 && p < m && (tomb || dp > prepad64(p));
+  }
+  const uint64_t mp = p - 20;  // p >= 20 for nodes
+  const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // span s holds m in [16 KiB s - 14, +16 KiB)
+  // in a store without garbage the parent is the previous record: one load
+  int64_t par = hp && mprev == mp ? (int64_t)gprev : PAR_MISS;
+  if (node && par == PAR_MISS && sp2 >= a.part.s_lo && sp2 < a.n_spans) {
+    const uint64_t w2 = part_span_wave(a.part, sp2 - a.part.s_lo);
+    if (w2 < wlo || w2 >= whi) return false;
+    const uint32_t f2 = a.span_first[sp2];
+    const uint32_t n2 = (uint32_t)min<uint64_t>(a.span_count[sp2], a.wcap - min<uint64_t>(f2, a.wcap));
+    uint32_t lo = 0, hi = n2;
+    const uint64_t* cm = a.c_m + w2 * a.wcap + f2;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (cm[mid] < mp) lo = mid + 1; else hi = mid;
+    }
+    if (lo < n2 && cm[lo] == mp) par = (int64_t)(w2 * a.wcap + f2 + lo);
+  }
+  if (!node) {
+    par = PAR_MISS;  // no parent, no root
+  } else if (par == PAR_MISS) {
+    if (a.span_lo) {
+      if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
+    } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {
+      par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
+    }
+  }
+  if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
+  a.d_par[gi] = (int32_t)par;
+  if (par >= 0) atomicMax(&a.childof[par], claim_word(a.gen, gi));
+  return true;
+}
+
 template <bool FULL, bool WIDE, int V = 0>
 __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
   constexpr bool F1 = (V == 1 || V == 2) ? !kFlag1 : kFlag1;
@@ -525,18 +613,22 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // timing-only ablations (wrong results; SRD_DEBUG_API's scan-only calls):
   // 7 = the ring's loads alone (each tile XOR-folded), 8 = the whole tile
   // body on two L1/L2-resident tiles per block (no HBM traffic)
-  constexpr bool MEMONLY = V == 7, NOHBM = V == 8;
+  constexpr bool MEMONLY = V == 7 || V == 12, NOHBM = V == 8;
   // 9 = the previous tile's line-63 tail and SX_63 carried in SGPRs (no
   // per-tile LDS store by lane 63; the f == 0 window takes them from there),
   // 10 = 9 with the 16-wide CRC levels
   constexpr bool SCARRY = V == 9 || V == 10;
   constexpr bool WIDE16B = V == 10;
+  // timing-only ablations (results not checked): 11 = coalesced tile loads
+  // (lane l, load j reads 16 B at 1024 j + 16 l), 12 = 11 memory-only
+  constexpr bool COAL = V == 11 || V == 12;
   uint32_t memonly_acc = 0;
   __shared__ ScanLds lds;
   // lanes of the record queue rq: with F1 its lane 63 is scratch
   constexpr uint64_t RQ_LANES = F1 ? 63 : 64;
   if (blockIdx.x == 0) {
     for (uint32_t i = threadIdx.x; i < a.n_zero_words; i += blockDim.x) a.zero_words[i] = 0;
+    for (uint32_t i = threadIdx.x; i < a.n_zero2; i += blockDim.x) a.zero2[i] = 0;
     if (threadIdx.x == 0 && a.sentinel) *a.sentinel = 0;
   }
 #ifdef SRD_WAVE_STAMPS
@@ -604,11 +696,11 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // lane weights, suffix XOR, filter) is one basic block.
   const uint64_t nohbm_k = (a.part.s_lo + part_block_start(a.part, blockIdx.x)) * SPAN_TILES;
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
-    const u32x4* q = (const u32x4*)(file + (NOHBM ? nohbm_k + (k & 1) : k) * (uint64_t)TILE + 64ull * lane);
+    const u32x4* q = (const u32x4*)(file + (NOHBM ? nohbm_k + (k & 1) : k) * (uint64_t)TILE + (COAL ? 16ull : 64ull) * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       // plain loads: this 64 B-per-lane pattern runs at ~3.8 TB/s with nt, ~6.1 without
-      const u32x4 v = q[j];
+      const u32x4 v = q[COAL ? 64 * j : j];
       o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
     }
   };
@@ -617,7 +709,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // m in [L-14, L+49] (L = B + 64 l): a node's zero bytes m+13..m+15 hold an
   // aligned zero halfword inside the lane's OWN line, so no lookahead is
   // needed.  Tile k covers [B-14, B+4082), span s covers
-  // [16 KiB s - 14, 16 KiB (s+1) - 14) -- link2_kernel looks parents up in
+  // [16 KiB s - 14, 16 KiB (s+1) - 14) -- link_record looks parents up in
   // span (m + 14) / 16 KiB.  The slow path stages the 22-dword window
   // [L-16, L+72) in LDS: win[0..3] the previous line's tail, win[4..19] the
   // line, win[20..21] the next line's head; win[22] holds the previous
@@ -835,7 +927,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
     if constexpr (F1 && !FULL) {
       // the first flagged line's record (at most one candidate: the node test
-      // is link2's, F_NT) into the register queue; lane 63 of rq is scratch
+      // is link_record's, F_NT) into the register queue; lane 63 of rq is scratch
       // (a tile without a record writes there), so the queue holds 63
       const bool single = f1_pm != 0;  // uniform
       const int bl = single ? __builtin_ctzll(f1_pm) : 0;
@@ -941,7 +1033,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
           // one possible node (the common case: one metadata record per
           // line): the record -- m, p, key_hash, crc, the two suffix values
           // only the scan has, and the position flags -- goes to lane `count`
-          // of the record registers; link2_kernel applies the node test
+          // of the record registers; link_record applies the node test
           // (data_store.rs:404-470) beside its parent lookup (F_NT).
           const int bl = __builtin_ctzll(pm);
           const int rs = 64 * f + bl - 14;
@@ -1159,19 +1251,44 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   if constexpr (MEMONLY) {
     if (memonly_acc == 0x12345678u) a.counters[3] = memonly_acc;  // (keeps the loads)
   }
-  // ---- epilogue: per-wave results; the last block to finish reduces them
-  // (cdna guide: plain stores, vmcnt(0), barrier, lane-0 agent release, add;
-  // the last block acquires before reading) ----
+  // ---- epilogue: per-wave results; the optimistic pass links the block's
+  // records; the last block to finish reduces the per-wave results and links
+  // the deferred records (cdna guide: plain stores, vmcnt(0), barrier, lane-0
+  // agent release, add; the last block acquires before reading) ----
+  const bool link = a.d_par != nullptr;  // uniform
+  uint32_t* s_pre = (uint32_t*)lds.s_ovf;  // [17] prefix of the block's wave record counts
   if (lane == 0) {
     a.wave_total[w] = wtotal | (ovf ? (1ull << 63) : 0ull);
     a.wave_root[w] = rootmax;  // wave-uniform already
+    if (link) s_pre[wv + 1] = (uint32_t)min<uint64_t>(wtotal, a.wcap);  // records past wcap were not stored
 #ifdef SRD_WAVE_STAMPS  // timing-only build (tools/wave_stamps.py): each wave's end, 100 MHz clock
     if (w < 8192) g_wave_stamp[w] = __builtin_amdgcn_s_memrealtime();
 #endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint32_t& s_last = lds.s_last;
   __syncthreads();
+  if (link) {
+    // the block's records in file order (its 16 waves' regions, flattened);
+    // their records and counts are visible to the whole block now
+    if (threadIdx.x == 0) {
+      s_pre[0] = 0;
+      for (int v = 0; v < SCAN_WAVES_V2; v++) s_pre[v + 1] += s_pre[v];
+    }
+    __syncthreads();
+    const uint32_t n = s_pre[SCAN_WAVES_V2];
+    const uint64_t w0 = (uint64_t)blockIdx.x * SCAN_WAVES_V2;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      uint32_t v = 0;  // the largest v with s_pre[v] <= i: record i's wave
+#pragma unroll
+      for (uint32_t st = SCAN_WAVES_V2 / 2; st; st >>= 1) v += s_pre[v + st] <= i ? st : 0u;
+      const uint64_t r = i - s_pre[v];
+      if (!link_record(a, w0 + v, r, w0, w0 + SCAN_WAVES_V2))
+        a.defer[atomicAdd(&a.done[1], 1u)] = (uint32_t)((w0 + v) * a.wcap + r);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  uint32_t& s_last = lds.s_last;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1182,20 +1299,27 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // exclusive prefix of the wave counts: thread t owns waves [t*q, (t+1)*q).
-  // q <= 4 (up to 256 blocks): the thread's waves are loaded together into
+  // totals of the wave counts: thread t owns waves [t*q, (t+1)*q).  q <= 4
+  // (up to 256 blocks): the thread's waves are loaded together into
   // registers (one round trip instead of 2q dependent ones: the last block's
   // epilogue is on the critical path of every call)
   constexpr int QR = 4;
   uint64_t* s_wsum = (uint64_t*)lds.tab;  // the CRC tables are dead now
+  uint64_t* s_smax = s_wsum + SCAN_WAVES_V2;
   uint64_t* s_root = lds.s_root;
-  uint64_t* s_ovf = lds.s_ovf;
+  uint64_t* s_ovf = s_smax + SCAN_WAVES_V2;
   const uint32_t T = blockDim.x, t = threadIdx.x;
   const uint64_t q = (total_waves + T - 1) / T;
-  uint64_t sum = 0, rmax = 0, o = 0;
-  uint64_t vt[QR];
+  uint64_t sum = 0, rmax = 0, o = 0, smax = 0;
+  auto take = [&](uint64_t i, uint64_t v, uint64_t rt) {
+    const uint64_t cnt = v & ~(1ull << 63);
+    sum += cnt;
+    o |= v >> 63;
+    rmax = max(rmax, rt);
+    if (cnt) smax = max(smax, i * a.wcap + min(cnt, a.wcap));  // 1 + the wave's last slot
+  };
   if (q <= QR) {
-    uint64_t vr[QR];
+    uint64_t vt[QR], vr[QR];
 #pragma unroll
     for (int j = 0; j < QR; j++) {
       const uint64_t i = min(t * q + j, total_waves - 1);
@@ -1203,53 +1327,30 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       vr[j] = a.wave_root[i];
     }
 #pragma unroll
-    for (int j = 0; j < QR; j++) {
-      const bool in = (uint64_t)j < q && t * q + j < total_waves;
-      vt[j] = in ? vt[j] : 0ull;
-      sum += vt[j] & ~(1ull << 63);
-      o |= vt[j] >> 63;
-      rmax = max(rmax, in ? vr[j] : 0ull);
-    }
+    for (int j = 0; j < QR; j++)
+      if ((uint64_t)j < q && t * q + j < total_waves) take(t * q + j, vt[j], vr[j]);
   } else {
-    for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
-      const uint64_t v = a.wave_total[i];
-      sum += v & ~(1ull << 63);
-      o |= v >> 63;
-      rmax = max(rmax, a.wave_root[i]);
-    }
+    for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) take(i, a.wave_total[i], a.wave_root[i]);
   }
   rmax = wave_max_u64(rmax);
-  for (int d = 32; d > 0; d >>= 1) o |= __shfl_xor(o, d);
-  // inclusive scan of the T partials: inside each wave, then over the waves
-  uint64_t x = sum;
+  smax = wave_max_u64(smax);
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t y = __shfl_up(x, d);
-    if (lane >= d) x += y;
+  for (int d = 32; d > 0; d >>= 1) {
+    o |= __shfl_xor(o, d);
+    sum += __shfl_xor(sum, d);
   }
-  if (lane == 63) { s_wsum[wv] = x; s_root[wv] = rmax; s_ovf[wv] = o; }
+  if (lane == 0) { s_wsum[wv] = sum; s_root[wv] = rmax; s_ovf[wv] = o; s_smax[wv] = smax; }
   __syncthreads();
-  uint64_t wpre = 0;
-  for (int i = 0; i < wv; i++) wpre += s_wsum[i];
-  uint64_t run = wpre + x - sum;
-  if (q <= QR) {
-#pragma unroll
-    for (int j = 0; j < QR; j++) {
-      if ((uint64_t)j < q && t * q + j < total_waves) {
-        a.wave_base[t * q + j] = run;
-        run += vt[j] & ~(1ull << 63);
-      }
-    }
-  } else {
-    for (uint64_t i = t * q; i < min((t + 1) * q, total_waves); i++) {
-      a.wave_base[i] = run;
-      run += a.wave_total[i] & ~(1ull << 63);
-    }
-  }
   if (t == 0) {
-    uint64_t mr = 0, oo = 0, tot = 0;
-    for (int i = 0; i < SCAN_WAVES_V2; i++) { mr = max(mr, s_root[i]); oo |= s_ovf[i]; tot += s_wsum[i]; }
-    *a.k_total = tot;
+    uint64_t mr = 0, oo = 0, tot = 0, sm = 0;
+    for (int i = 0; i < SCAN_WAVES_V2; i++) {
+      mr = max(mr, s_root[i]);
+      oo |= s_ovf[i];
+      tot += s_wsum[i];
+      sm = max(sm, s_smax[i]);
+    }
+    a.k_total[0] = tot;
+    a.k_total[1] = sm;
     a.counters[0] = mr;
     a.counters[1] = top;  // the optimistic pass's start tail (find_top; 0: none)
     a.counters[2] = oo;
@@ -1257,6 +1358,16 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 #ifdef SRD_WAVE_STAMPS
     g_wave_stamp[8192 + 1023] = __builtin_amdgcn_s_memrealtime();
 #endif
+  }
+  if (link) {
+    // the deferred records: every wave is readable now
+    const uint32_t nd = a.done[1];
+    __syncthreads();
+    if (t == 0) a.done[1] = 0;
+    for (uint32_t i = t; i < nd; i += T) {
+      const uint64_t slot = a.defer[i], wd = slot / a.wcap;
+      link_record(a, wd, slot - wd * a.wcap, 0, total_waves);
+    }
   }
 }
 
