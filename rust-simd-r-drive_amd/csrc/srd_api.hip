@@ -1091,7 +1091,7 @@ static int alloc_fast(Ctx* c, uint64_t capK, uint32_t log2_nbk) {
   TRY(ensure(c, B_FLAG, capK));
   TRY(ensure(c, B_CHAIN_G, (capK + 1) * 8));
   TRY(ensure(c, B_PART, GLUE_BLOCKS * 4));
-  TRY(ensure(c, B_PARTEX, GLUE_BLOCKS * 4));
+  TRY(ensure(c, B_PARTEX, CHAIN_BLOCKS * CHAIN_WAVES * 4));
   TRY(ensure(c, B_PLAN, sizeof(Plan)));
   TRY(alloc_out(c, capK + 1));
   TRY(alloc_index(c, capK, log2_nbk));
@@ -1210,8 +1210,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       sa.childof = P<uint64_t>(c, B_CHILDOF);
       sa.flag = P<uint8_t>(c, B_FLAG);
       sa.part = P<uint32_t>(c, B_PART);
-      sa.part_ex = P<uint32_t>(c, B_PARTEX);
-      sa.chain_g = P<uint64_t>(c, B_CHAIN_G);
+      sa.wpart = P<uint32_t>(c, B_PARTEX);
       sa.counters = (const unsigned long long*)cnt;
       sa.plan = pl;
       sa.zero = index_zero_words(c, log2_nbk, &sa.n_zero);  // child2 zeroes the index's bucket fills

@@ -203,9 +203,8 @@ struct ShapeArgs {
   const uint32_t* has_child;  // retry rounds: the prune marks
   uint64_t* childof;
   uint8_t* flag;
-  uint32_t* part;
-  uint32_t* part_ex;
-  uint64_t* chain_g;
+  uint32_t* part;       // [CHAIN_BLOCKS] core records per chain block (check_kernel)
+  uint32_t* wpart;      // [CHAIN_BLOCKS * CHAIN_WAVES] core records per wave chunk (check_kernel)
   const unsigned long long* counters;
   Plan* plan;
   uint32_t coff;     // chain entries before the first candidate (1 whole file, 0 span mode)
@@ -337,19 +336,24 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
   const uint32_t n = block_waves(a, s_pre);
   uint32_t cnt = 0;
   bool fail = false;
-  // CR nodes per thread per pass, their loads issued level by level: the
+  // wave chunks: wave wi takes the block's records [c0, c1) (chain_finalize
+  // ranks them with the same chunks and the per-chunk counts, no barriers);
+  // CR records per lane per pass, their loads issued level by level: the
   // node's own words (parent, claim), then its parent's
+  const uint32_t wi = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t chunk = (n + CHAIN_WAVES - 1) / CHAIN_WAVES;
+  const uint32_t c0 = min(n, wi * chunk), c1 = min(n, c0 + chunk);
   constexpr int CR = 4;
-  for (uint32_t base = 0; base < n; base += CR * CHAIN_THREADS) {
+  for (uint32_t base = c0; base < c1; base += CR * 64) {
     uint64_t g[CR], cg[CR], cp[CR];
     int64_t par[CR], pp[CR];
     uint32_t hc[CR], hp[CR];
     bool in[CR];
 #pragma unroll
     for (int r = 0; r < CR; r++) {
-      const uint32_t i = base + (uint32_t)r * CHAIN_THREADS + threadIdx.x;
-      in[r] = i < n;
-      g[r] = slot_of(a, s_pre, in[r] ? i : 0u);
+      const uint32_t i = base + (uint32_t)r * 64 + lane;
+      in[r] = i < c1;
+      g[r] = slot_of(a, s_pre, in[r] ? i : c0);
       par[r] = a.d_par[g[r]];
       cg[r] = a.childof[g[r]];
       hc[r] = marks ? a.has_child[g[r]] : 0u;
@@ -381,6 +385,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
         fail = true;  // branch: another node holds the claim on the same parent
       }
     }
+  }
+  {
+    uint32_t wc = cnt;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) wc += __shfl_xor(wc, o);
+    if (lane == 0) a.wpart[blockIdx.x * CHAIN_WAVES + wi] = wc;
   }
   const uint32_t tot = block_sum_n<CHAIN_WAVES>(cnt, wsum);
   if (__syncthreads_or(fail) && threadIdx.x == 0) atomicOr(&a.plan->status, ST_SHAPE);
@@ -498,7 +508,11 @@ __device__ __forceinline__ uint32_t block_rank_rounds(const bool* f, uint32_t* w
 // work is a chain of four dependent loads (flag -> parent/slot -> records ->
 // parent record, tile values, table words); the R entries' loads of each level
 // are issued together
-constexpr int FIN_R = 2;  // 3 and 4 spill at 128 VGPRs
+#ifndef SRD_FIN_R
+#define SRD_FIN_R 2
+#endif
+constexpr int FIN_R = SRD_FIN_R;
+constexpr uint32_t WSLOW = 256;  // per-wave slow-entry queue (LDS) of chain_finalize_kernel
 
 // one chain entry's inputs (finalize_core's, loaded level by level)
 struct FinIn {
@@ -606,10 +620,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
                                                                       uint32_t log2_nbk) {
   __shared__ uint32_t wsum[CHAIN_WAVES * FIN_R];
   __shared__ uint32_t s_pre[BW_MAX + 1];
+  __shared__ uint32_t wslow[CHAIN_WAVES][WSLOW];
   __shared__ FinLds lt;
   uint32_t* const tab = lt.tab;
-  __shared__ uint32_t slowq[CHAIN_THREADS * FIN_R];
-  __shared__ uint32_t nslow;
   extern __shared__ uint32_t hist[];
   // the LDS tables' words first, into registers: their loads overlap the
   // plan's dependent ones below (one round trip instead of a load -> store
@@ -669,7 +682,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     lt.winit[ti] = r_winit;
     lt.zero_crc[ti] = r_zc;
   }
-  if (threadIdx.x == 0) nslow = 0;
   __syncthreads();
   // the root entry (whole file: chain entry 0, no candidate record); its
   // CRC's slow path, if any, runs after the candidates
@@ -679,22 +691,52 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     root_slow = finalize_core(f, 0, NO_REC, -1, root_t, &kh);
     atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
   }
-  uint64_t run = a.coff + before;  // this block's next chain position
+  uint64_t bend = a.coff + before;  // the end of this block's chain positions
   if (!troot) {
     const uint32_t n = block_waves(a, s_pre);
+    // wave chunks as in check_kernel: wave wi ranks its records from its
+    // chunk's offset (the per-chunk core counts) with ballots -- the waves
+    // never wait for each other inside the loop
+    const uint32_t wi = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    uint32_t woff, btot;
+    {
+      const uint32_t v = lane < CHAIN_WAVES ? a.wpart[blockIdx.x * CHAIN_WAVES + lane] : 0u;
+      uint32_t x = lane < wi ? v : 0u, y = v;
+#pragma unroll
+      for (int o = 32; o; o >>= 1) {
+        x += __shfl_xor(x, o);
+        y += __shfl_xor(y, o);
+      }
+      woff = x;
+      btot = y;
+    }
+    bend += btot;
+    uint64_t run = a.coff + before + woff;  // this wave's next chain position
+    const uint64_t run0 = run;
+    uint32_t nsq = 0;  // wave-uniform: entries in the wave's slow queue
+    auto flush_slow = [&]() {
+      if (!nsq) return;
+      unsigned long long sbase = 0;
+      if (lane == 0) sbase = atomicAdd(f.n_slow, (unsigned long long)nsq);
+      sbase = __shfl(sbase, 0);
+      for (uint32_t q = lane; q < nsq; q += 64) f.slow_list[sbase + q] = run0 + wslow[wi][q];
+    };
+    const uint32_t chunk = (n + CHAIN_WAVES - 1) / CHAIN_WAVES;
+    const uint32_t c0 = min(n, wi * chunk), c1 = min(n, c0 + chunk);
     const u32x4* t4 = (const u32x4*)f.tile;
-    for (uint32_t base = 0; base < n; base += CHAIN_THREADS * FIN_R) {
+    for (uint32_t base = c0; base < c1; base += 64 * FIN_R) {
       bool fl[FIN_R];
       uint64_t gi[FIN_R], kh[FIN_R];
       int64_t par[FIN_R];
       FinIn e[FIN_R];
       // level 1: core flag, parent and the record itself, all at the record's
-      // slot (idle lanes: the block's first record)
+      // slot (idle lanes: the chunk's first record)
 #pragma unroll
       for (int r = 0; r < FIN_R; r++) {
-        const uint32_t i = base + (uint32_t)r * CHAIN_THREADS + threadIdx.x;
-        gi[r] = slot_of(a, s_pre, i < n ? i : 0u);
-        fl[r] = i < n && a.flag[gi[r]];
+        const uint32_t i = base + (uint32_t)r * 64 + lane;
+        gi[r] = slot_of(a, s_pre, i < c1 ? i : c0);
+        fl[r] = i < c1 && a.flag[gi[r]];
         par[r] = a.d_par[gi[r]];
         e[r].mo = f.c_m[gi[r]];
         const u32x4 r0 = f.c_rec[2 * gi[r]], r1 = f.c_rec[2 * gi[r] + 1];
@@ -704,8 +746,13 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
         e[r].sxv = r1[1];
         e[r].fl = r1[3];
       }
-      uint32_t rank[FIN_R];
-      const uint32_t tot = block_rank_rounds<CHAIN_WAVES, FIN_R>(fl, wsum, rank);
+      uint32_t rank[FIN_R], tot = 0;
+#pragma unroll
+      for (int r = 0; r < FIN_R; r++) {
+        const uint64_t b = __ballot(fl[r]);
+        rank[r] = tot + (uint32_t)__popcll(b & lt_mask);
+        tot += (uint32_t)__popcll(b);
+      }
       // level 2: the parent's record, the tile values and table words.  k0
       // (the entry's start tile) is resident: start >= p >= the span's lower
       // tail in span mode.  A root-linked candidate (par == PAR_ROOT) has no
@@ -733,25 +780,27 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
         GST(f.o_crc_st[c], e[r].crc_st);
         atomicAdd(&hist[idx_bucket(kh[r], log2_nbk)], 1u);
       }
+      // entries whose CRC needs a wave go to the call's slow list (idx_dedup's
+      // blocks run them, one wave each), gathered in the wave's LDS queue:
+      // one list claim per wave and WSLOW entries
 #pragma unroll
       for (int r = 0; r < FIN_R; r++) {
-        if (!fl[r]) continue;
         const uint64_t c = run + rank[r];
-        if (finalize_in(f, c, e[r], lt)) slowq[atomicAdd(&nslow, 1u)] = (uint32_t)(c - run);
-      }
-      __syncthreads();
-      const uint32_t ns = nslow;
-      if (ns) {  // this pass's slow entries go to the call's list (idx_dedup's blocks run them, one wave each)
-        __shared__ unsigned long long sbase;
-        if (threadIdx.x == 0) sbase = atomicAdd(f.n_slow, (unsigned long long)ns);
-        __syncthreads();
-        for (uint32_t q = threadIdx.x; q < ns; q += CHAIN_THREADS) f.slow_list[sbase + q] = run + slowq[q];
-        __syncthreads();
-        if (threadIdx.x == 0) nslow = 0;
-        __syncthreads();
+        const bool slow = fl[r] && finalize_in(f, c, e[r], lt);
+        const uint64_t sb = __ballot(slow);
+        const uint32_t k = (uint32_t)__popcll(sb);
+        if (k) {
+          if (nsq + k > WSLOW) {
+            flush_slow();
+            nsq = 0;
+          }
+          if (slow) wslow[wi][nsq + __popcll(sb & lt_mask)] = (uint32_t)(c - run0);
+          nsq += k;
+        }
       }
       run += tot;
     }
+    flush_slow();
   }
   if (root_slow) f.slow_list[atomicAdd(f.n_slow, 1ull)] = 0;  // (block 0, thread 0 only)
   __syncthreads();
@@ -765,7 +814,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   }
   __syncthreads();
   const uint64_t n_chain = troot ? 1 : a.coff + total;
-  const uint64_t clo = min(n_chain, blockIdx.x ? a.coff + before : 0), chi = min(n_chain, run);
+  const uint64_t clo = min(n_chain, blockIdx.x ? a.coff + before : 0), chi = min(n_chain, bend);
   constexpr int SR = 4;  // keys loaded together per pass
   for (uint64_t base = clo; base < chi; base += SR * CHAIN_THREADS) {
     uint64_t k[SR];

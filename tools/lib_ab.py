@@ -1,9 +1,9 @@
-"""Two builds of the library A/B'd in ONE process on the same device-resident
+"""Two or more builds of the library A/B'd in ONE process on the same device-resident
 store (timing tool): NCTX contexts per build, the builds' calls interleaved
 round by round, so the per-context spread shows up as spread
 within each build instead of as a difference between them.  Every call's
 result is checked against the store's closed form.
-usage: python tools/lib_ab.py A.so B.so     env: NCTX (3), ROUNDS (10), REPS (10), CONFIG=c2|c3"""
+usage: python tools/lib_ab.py A.so B.so [C.so ...]     env: NCTX (3), ROUNDS (10), REPS (10), CONFIG=c2|c3"""
 import ctypes as C
 import json
 import os
@@ -25,8 +25,8 @@ def bind(path):
     return L
 
 
-libs = [bind(p) for p in sys.argv[1:3]]
-names = [os.path.basename(p) for p in sys.argv[1:3]]
+libs = [bind(p) for p in sys.argv[1:]]
+names = [os.path.basename(p) for p in sys.argv[1:]]
 nctx, rounds, reps = int(os.environ.get("NCTX", 3)), int(os.environ.get("ROUNDS", 10)), int(os.environ.get("REPS", 10))
 cfg = os.environ.get("CONFIG", "c2")
 if cfg == "c3":
@@ -66,7 +66,7 @@ out = {"config": cfg, "builds": names, "per_ctx": []}
 for i, (b, L, h) in enumerate(ctxs):
     out["per_ctx"].append({"build": names[b], "call_med": round(med(wall[i]), 4), "call_min": round(min(wall[i]), 4),
                            "scan_med": round(med(scan[i]), 4), "glue_med": round(med(wall[i]) - med(scan[i]), 4)})
-for b in range(2):
+for b in range(len(libs)):
     rows = [x for x in out["per_ctx"] if x["build"] == names[b]]
     out[names[b]] = {k: round(sum(x[k] for x in rows) / len(rows), 4) for k in ("call_med", "scan_med", "glue_med")}
 print(json.dumps(out, indent=1))
