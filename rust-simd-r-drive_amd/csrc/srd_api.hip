@@ -542,7 +542,7 @@ static void scan_weights(uint32_t (&wq)[16]) {
 }
 #ifdef SRD_DEBUG_API  // timing builds: A/B of scan variants inside one context (one workspace)
 extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
-  if (!c || v < 0 || v > 12) return SRD_ERR_ARG;
+  if (!c || v < 0 || v > 30) return SRD_ERR_ARG;
   c->scan_variant = (uint32_t)v;
   return 0;
 }
@@ -1043,7 +1043,7 @@ static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
 // zeroed here, idx_hist_kernel claims the ranges and idx_scatter_kernel fills them
 static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
                                  const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
-                                 Plan* pl, bool fused = false, const FinArgs* slow = nullptr) {
+                                 Plan* pl, bool fused = false, const FinArgs* slow = nullptr, bool zeroed = false) {
   TRY(next_lgen(c));
   IdxArgs ia = index_args(c, log2_nbk);
   ia.alias = fused ? 1u : 0u;
@@ -1061,7 +1061,8 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
   const uint32_t nbk = 1u << log2_nbk;
   if (!fused) {
     uint32_t nz = 0;
-    HIPCHK(hipMemsetAsync(index_zero_words(c, log2_nbk, &nz), 0, (size_t)nz * 4, c->stream));
+    uint32_t* zw = index_zero_words(c, log2_nbk, &nz);
+    if (!zeroed) HIPCHK(hipMemsetAsync(zw, 0, (size_t)nz * 4, c->stream));
     idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
     KCHK(c, "idx_hist_kernel");
     idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
@@ -1458,7 +1459,13 @@ extern "C" int srd_index_partition_device(srd_ctx* c, const uint64_t* d_keys, co
   return partition_impl(c, d_keys, d_vals, n, world, d_out_pairs, nullptr, counts);
 }
 
-__global__ void set_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
+__global__ void index_prep_kernel(Plan* pl, uint64_t n, uint32_t* zero, uint32_t nz) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nz) zero[i] = 0;
+  if (i < sizeof(Plan) / 4) ((uint32_t*)pl)[i] = 0;
+  __syncthreads();
+  if (i == 0) pl->n_chain = n;
+}
 
 // KeyIndexer::build over n (key_hash, meta_off or packed) device pairs given
 // as two arrays, in file order (latest position wins); output in chain order
@@ -1471,10 +1478,14 @@ static int index_build_sep(Ctx* c, const uint64_t* keys, const uint64_t* vals, u
   const uint32_t log2_nbk = index_log2_buckets(n);
   TRY(alloc_index(c, n, log2_nbk));
   Plan* pl = P<Plan>(c, B_MPLAN);
-  HIPCHK(hipMemsetAsync(pl, 0, sizeof(Plan), c->stream));
-  set_u64_kernel<<<1, 1, 0, c->stream>>>(&pl->n_chain, n);
-  KCHK(c, "set_u64_kernel");
-  TRY(launch_index_bucketed(c, keys, vals, &pl->n_chain, &pl->status, log2_nbk, okeys, opacked, pl));
+  // one launch zeroes the plan (n_chain = n) and the bucket fills (was a
+  // memset, a one-thread kernel and a second memset)
+  uint32_t nz = 0;
+  uint32_t* zw = index_zero_words(c, log2_nbk, &nz);
+  index_prep_kernel<<<(nz + 255) / 256, 256, 0, c->stream>>>(pl, n, zw, nz);
+  KCHK(c, "index_prep_kernel");
+  TRY(launch_index_bucketed(c, keys, vals, &pl->n_chain, &pl->status, log2_nbk, okeys, opacked, pl, false, nullptr,
+                            true));
   HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(spin_sync(c->stream));
   if (c->h_plan->idx_overflow) return index_global(c, n, n_index, keys, vals, okeys, opacked);
@@ -2269,18 +2280,48 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
       if (!r) r = ensure(c, B_GVAL, m1 * 8);
       if (!r) r = ensure(c, B_GOKEY, m1 * 8);
       if (!r) r = ensure(c, B_GOPACKED, m1 * 8);
-      uint64_t acc = 0;
-      for (uint32_t s = 0; s < nc && !r; s++) {
+      // every source's run: one gather launch reading the peers' HBM when
+      // every source GPU is peer-accessible, else one copy per run
+      GatherArgs ga{};
+      bool direct = true;
+      uint64_t acc = 0, nmax = 0;
+      for (uint32_t s = 0; s < nc; s++) {
         uint64_t off = 0;
         for (uint32_t q = 0; q < p; q++) off += sh[s].cnt[q];
-        const uint64_t n = sh[s].cnt[p];
         Ctx* cs = in.ctxs[s];
-        if (copy_to(c, P<uint64_t>(c, B_GKEY) + acc, cs, P<uint64_t>(cs, B_XKEY) + off, n * 8, in.peer_fail) != hipSuccess ||
-            copy_to(c, P<uint64_t>(c, B_GVAL) + acc, cs, P<uint64_t>(cs, B_XVAL) + off, n * 8, in.peer_fail) != hipSuccess) {
-          set_err("index exchange: peer copy failed");
-          r = SRD_ERR_HIP;
+        ga.src_k[s] = P<uint64_t>(cs, B_XKEY) + off;
+        ga.src_v[s] = P<uint64_t>(cs, B_XVAL) + off;
+        ga.dst_off[s] = acc;
+        acc += sh[s].cnt[p];
+        nmax = std::max<uint64_t>(nmax, sh[s].cnt[p]);
+        if (cs->device != c->device && !enable_peer(c->device, cs->device)) direct = false;
+      }
+      ga.dst_off[nc] = acc;
+      ga.dst_k = P<uint64_t>(c, B_GKEY);
+      ga.dst_v = P<uint64_t>(c, B_GVAL);
+      if (!r && direct && nmax) {
+        for (uint32_t s = 0; s < nc && !r; s++) {
+          Ctx* cs = in.ctxs[s];
+          if (cs != c && cs->ready_recorded && hipStreamWaitEvent(c->stream, cs->ev_ready, 0) != hipSuccess) {
+            set_err("index exchange: event wait failed");
+            r = SRD_ERR_HIP;
+          }
         }
-        acc += n;
+        if (!r) {
+          const dim3 grid((unsigned)std::min<uint64_t>((nmax + 255) / 256, 128), nc);
+          gather_runs_kernel<<<grid, 256, 0, c->stream>>>(ga);
+          if (hipGetLastError() != hipSuccess) { set_err("index exchange: gather launch failed"); r = SRD_ERR_HIP; }
+        }
+      } else if (!r) {
+        for (uint32_t s = 0; s < nc && !r; s++) {
+          const uint64_t n = sh[s].cnt[p];
+          Ctx* cs = in.ctxs[s];
+          if (copy_to(c, ga.dst_k + ga.dst_off[s], cs, ga.src_k[s], n * 8, in.peer_fail) != hipSuccess ||
+              copy_to(c, ga.dst_v + ga.dst_off[s], cs, ga.src_v[s], n * 8, in.peer_fail) != hipSuccess) {
+            set_err("index exchange: peer copy failed");
+            r = SRD_ERR_HIP;
+          }
+        }
       }
       if (!r) r = index_build_sep(c, P<uint64_t>(c, B_GKEY), P<uint64_t>(c, B_GVAL), NI, P<uint64_t>(c, B_GOKEY),
                                   P<uint64_t>(c, B_GOPACKED), &ni[p]);
@@ -2645,7 +2686,17 @@ static int launch_write(Ctx* c, hipStream_t s, const uint8_t* pay, const uint8_t
   if (!n) return 0;
   WriteArgs w{pay, keys, ent, n, out, base, kh, mo, null_only};
   const unsigned g = (unsigned)std::min<uint64_t>((n + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
-  write_kernel<<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
+#ifdef SRD_DEBUG_API
+  if (c->scan_variant == 21)
+    write_kernel<1><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
+  else if (c->scan_variant == 22)
+    write_kernel<2><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
+  else if (c->scan_variant == 25)
+    write_kernel<5><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
+
+  else
+#endif
+    write_kernel<<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
   HIPCHK(hipGetLastError());
   if (sync_debug()) {
     HIPCHK(hipStreamSynchronize(s));

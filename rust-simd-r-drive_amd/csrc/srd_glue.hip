@@ -1037,41 +1037,96 @@ __global__ __launch_bounds__(256) void part_count_kernel(PartArgs a) {
   __syncthreads();
   for (uint32_t o = threadIdx.x; o < a.world; o += blockDim.x) a.cnt[(uint64_t)o * GLUE_BLOCKS + blockIdx.x] = h[o];
 }
+// Stable scatter by owner: PR rounds of 256 pairs per pass, each wave ranks
+// its lanes per owner with one ballot per owner, and the block orders the
+// (round, wave) groups with one LDS exchange -- three barriers per 1024
+// pairs (it was two per owner per 256).
 __global__ __launch_bounds__(256) void part_scatter_kernel(PartArgs a) {
-  __shared__ uint32_t wsum[4];
+  constexpr int PR = 4;
+  __shared__ uint32_t wcnt[PR][4][PART_MAX_WORLD];
   __shared__ uint32_t run[PART_MAX_WORLD];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1;
   for (uint32_t o = threadIdx.x; o < a.world; o += blockDim.x) run[o] = a.off[(uint64_t)o * GLUE_BLOCKS + blockIdx.x];
   __syncthreads();
   uint64_t lo, hi;
   chunk_of(a.n, &lo, &hi);
-  for (uint64_t base = lo; base < hi; base += blockDim.x) {
-    const uint64_t i = base + threadIdx.x;
-    const bool in = i < hi;
-    const uint64_t k = in ? a.keys[i] : 0;
-    const uint32_t own = in ? owner_of(k, a.world) : ~0u;
-    for (uint32_t o = 0; o < a.world; o++) {
-      uint32_t tot;
-      const uint32_t r = block_rank256(own == o, wsum, &tot);
-      if (own == o) {
-        const uint64_t pos = (uint64_t)run[o] + r;
-        if (a.out_v) {
-          a.out[pos] = k;
-          a.out_v[pos] = a.vals[i];
-        } else {
-          a.out[2 * pos] = k;
-          a.out[2 * pos + 1] = a.vals[i];
-        }
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) run[o] += tot;
-      __syncthreads();
+  for (uint64_t base = lo; base < hi; base += PR * 256) {
+    uint64_t k[PR], v[PR];
+    uint32_t own[PR], rk[PR];
+#pragma unroll
+    for (int r = 0; r < PR; r++) {
+      const uint64_t i = base + (uint64_t)r * 256 + threadIdx.x;
+      const bool in = i < hi;
+      k[r] = in ? a.keys[i] : 0;
+      v[r] = in ? a.vals[i] : 0;
+      own[r] = in ? owner_of(k[r], a.world) : ~0u;
     }
+#pragma unroll
+    for (int r = 0; r < PR; r++) {
+      uint32_t wc = 0;
+      rk[r] = 0;
+      for (uint32_t o = 0; o < a.world; o++) {
+        const uint64_t b = __ballot(own[r] == o);
+        if (own[r] == o) rk[r] = (uint32_t)__popcll(b & lt);
+        if (lane == o) wc = (uint32_t)__popcll(b);
+      }
+      if (lane < a.world) wcnt[r][w][lane] = wc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PR; r++) {
+      if (own[r] == ~0u) continue;
+      const uint32_t o = own[r];
+      uint32_t before = run[o];
+      for (int rr = 0; rr < PR; rr++)
+        for (uint32_t ww = 0; ww < 4; ww++)
+          before += (rr < r || (rr == r && ww < w)) ? wcnt[rr][ww][o] : 0u;
+      const uint64_t pos = (uint64_t)before + rk[r];
+      if (a.out_v) {
+        a.out[pos] = k[r];
+        a.out_v[pos] = v[r];
+      } else {
+        a.out[2 * pos] = k[r];
+        a.out[2 * pos + 1] = v[r];
+      }
+    }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < a.world; o += blockDim.x) {
+      uint32_t t = 0;
+      for (int rr = 0; rr < PR; rr++)
+        for (uint32_t ww = 0; ww < 4; ww++) t += wcnt[rr][ww][o];
+      run[o] += t;
+    }
+    __syncthreads();
   }
 }
 __global__ void part_counts_kernel(PartArgs a) {
   const uint32_t o = threadIdx.x;
   if (o < a.world) a.counts[o] = a.off[(uint64_t)(o + 1) * GLUE_BLOCKS] - a.off[(uint64_t)o * GLUE_BLOCKS];
 }
+// An owner's runs pulled from every shard in ONE launch (blockIdx.y = the
+// source shard; its run read over xGMI straight from the source GPU's HBM,
+// peer access enabled) instead of two hipMemcpyPeerAsync per source: each
+// small copy cost a blit launch of ~5 us on the owner's stream
+struct GatherArgs {
+  const uint64_t* src_k[PART_MAX_WORLD];
+  const uint64_t* src_v[PART_MAX_WORLD];
+  uint64_t dst_off[PART_MAX_WORLD + 1];
+  uint64_t* dst_k;
+  uint64_t* dst_v;
+};
+__global__ __launch_bounds__(256) void gather_runs_kernel(GatherArgs a) {
+  const uint32_t s = blockIdx.y;
+  const uint64_t o = a.dst_off[s], n = a.dst_off[s + 1] - o;
+  const uint64_t* __restrict__ sk = a.src_k[s];
+  const uint64_t* __restrict__ sv = a.src_v[s];
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    a.dst_k[o + j] = sk[j];
+    a.dst_v[o + j] = sv[j];
+  }
+}
+
 // interleaved pairs -> key / value arrays (the bucketed build's input)
 __global__ void deinterleave_kernel(const uint64_t* pairs, uint64_t n, uint64_t* k, uint64_t* v) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {

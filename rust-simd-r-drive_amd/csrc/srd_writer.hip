@@ -71,6 +71,13 @@ __device__ u32x4 g_wdummy[4];
 // (half_suffix_xor): raw CRC of the block = (lo * x^16384) ^ hi.  The key
 // hashes (XXH3-64, compute_hash.rs:25-27) are computed 64 at a time, one
 // entry per lane, not by one lane per entry.
+// V: timing-only ablations of the SRD_DEBUG_API build (wrong outputs):
+// 1 = the copy alone (no CRC), 2 = the CRC alone (no payload stores),
+// 5 = the copy alone with coalesced lanes (16 B at 16 l + 1024 j).
+// Measured (tools/writer_ab.py, profiles/r04/writer_ab.txt): the copy alone
+// takes as long as the whole kernel -- the CRC is hidden; rejected: nontemporal
+// payload stores (2x slower), a 3-deep register ring (+0.6 %)
+template <int V = 0>
 __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs a) {
   __shared__ ScanLds lds;
   load_crc_lds(lds);
@@ -90,10 +97,11 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
     return !(e.flags & SRD_ENTRY_TOMB) && pay_al && (e.src & 15) == 0 && b * TILE + 64ull * lane + 64 <= e.len;
   };
   auto load_blk = [&](const srd_write_entry& e, uint64_t b, uint32_t (&o)[16]) {
-    const u32x4* q = vec_line(e, b) ? (const u32x4*)(a.pay + e.src + b * TILE + 64ull * lane) : g_wdummy;
+    const u32x4* q = vec_line(e, b) ? (const u32x4*)(a.pay + e.src + b * TILE + (V == 5 ? 16ull : 64ull) * lane)
+                                    : g_wdummy;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const u32x4 v = q[j];
+      const u32x4 v = q[V == 5 ? 64 * j : j];
       o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
     }
   };
@@ -120,17 +128,27 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
   // one unit of the sequence: block b of entry i (a tombstone is one unit
   // without a block); returns whether a next unit exists in the group (its
   // loads went to nx)
+  // the unit after (i0, b0) of entry e0
+  struct Unit {
+    uint64_t i, b;
+    srd_write_entry e;
+  };
+  auto advance = [&](uint64_t i0, uint64_t b0, const srd_write_entry& e0) -> Unit {
+    const uint64_t nb = (e0.flags & SRD_ENTRY_TOMB) ? 1 : (e0.len + TILE - 1) / TILE;
+    Unit u{i0, b0 + 1, e0};
+    if (u.b >= nb) {
+      u.i = i0 + W;
+      u.b = 0;
+      if (u.i < gend) u.e = ent_s(u.i);
+    }
+    return u;
+  };
   auto step = [&](uint32_t (&d)[16], uint32_t (&nx)[16]) -> bool {
     const bool tomb = e.flags & SRD_ENTRY_TOMB;
     const uint64_t nb = tomb ? 1 : (e.len + TILE - 1) / TILE;
-    uint64_t i2 = i, b2 = b + 1;
-    srd_write_entry e2 = e;
-    if (b2 >= nb) {
-      i2 = i + W;
-      b2 = 0;
-      if (i2 < gend) e2 = ent_s(i2);
-    }
-    const bool more = i2 < gend;
+    const Unit u2 = advance(i, b, e);
+    const uint64_t i2 = u2.i, b2 = u2.b;
+    const srd_write_entry e2 = u2.e;
     load_blk(e2, b2, nx);  // (past the group: a block of this entry again, or the dummy -- harmless)
     const int jl = (int)(((i - w) / W) % 64);  // the entry's lane in khl
     const uint64_t kh = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(khl >> 32), jl) << 32) |
@@ -164,12 +182,21 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
         // (extra memory ops on this path only: the ring's waits stay right)
         const uint32_t nl = o < e.len ? (uint32_t)min<uint64_t>(64, e.len - o) : 0u;
         const uint8_t* src = a.pay + e.src;
+        // (static register indices only: a dynamic d[q >> 2] put a ring
+        // array in scratch)
 #pragma unroll
-        for (int j = 0; j < 16; j++) d[j] = 0;
-        for (uint32_t q = 0; q < nl; q++) {
-          const uint8_t v = src[o + q];
-          dst[o + q] = v;
-          d[q >> 2] |= (uint32_t)v << (8 * (q & 3));
+        for (int j = 0; j < 16; j++) {
+          uint32_t wd = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t q = 4u * j + k;
+            if (q < nl) {
+              const uint8_t v = src[o + q];
+              dst[o + q] = v;
+              wd |= (uint32_t)v << (8 * k);
+            }
+          }
+          d[j] = wd;
         }
       }
       {
@@ -177,12 +204,14 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
 #pragma unroll
         for (int j = 0; j < 4; j++)
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]}, rb,
-                                                 vec ? 64u * lane + 16u * j : OOB_OFF, 0, 0);
+                                                 vec && V != 2 ? (V == 5 ? 16u * lane + 1024u * j : 64u * lane + 16u * j)
+                                                               : OOB_OFF,
+                                                 0, 0);
       }
 #pragma unroll
       for (int j = 0; j < 16; j++) any |= d[j];
       // raw CRC of this 4 KiB block (zero-padded past the payload)
-      const uint32_t hx = half_suffix_xor(lane_weight_or(crc_line4_wide(d, lds, R), nib_lane), lane);
+      const uint32_t hx = (V == 1 || V == 5) ? d[0] ^ d[15] : half_suffix_xor(lane_weight_or(crc_line4_wide(d, lds, R), nib_lane), lane);
       const uint32_t lo = __builtin_amdgcn_readlane(hx, 0), hi = __builtin_amdgcn_readlane(hx, 32);
       const uint32_t raw = mul16k_u(lo) ^ hi;
       acc = b ? mul_tile_u(acc) ^ raw : raw;
@@ -224,7 +253,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
     i = i2;
     b = b2;
     e = e2;
-    return more;
+    return i < gend;
   };
   uint32_t cur[16], nxt[16];
   // groups of 64 entries of the wave: their key hashes first (one per lane,

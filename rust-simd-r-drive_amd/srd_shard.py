@@ -1,4 +1,15 @@
-"""Multi-GPU open of one store sharded by entry range.
+"""Multi-GPU open of one store sharded by entry range --
+the torch.distributed variant, NOT the product path of bench.py.
+
+The product multi-GPU open is srd_validate_index_multi_device /
+srd_validate_index_multi (include/srd_amd.h): ONE process drives every GPU of
+the node (data_store.rs:84-117 is one call; north_star says "without RCCL"),
+with persistent per-context host threads and xGMI peer reads for the index
+exchange.  This module keeps the one-process-per-GPU formulation (gloo /
+RCCL collectives for the composition check and the index all_to_all) for
+callers that already run one rank per GPU; its protocol is tested on CPU with
+gloo (tests/test_shard_gloo.py) and its HIP backend on one GPU
+(tests/test_gpu_shard_dist.py).
 
 One process per GPU.  Rank r holds the file bytes of entries
 [first_r, first_r + n_r) in its HBM (plus < 16 KiB of the previous shard as a

@@ -262,3 +262,34 @@ def test_overflow_after_large_call_one_context():
         torch.cuda.empty_cache()
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_cross_block_parents_deferred_links(ctx, flags):
+    """The scan's link phase (link_record) links each block's records once its
+    tiles are done; a record whose previous record or parent span lies in
+    another block's waves is deferred to the last block.  Entries of 24 and
+    40 MiB between runs of small ones put hundreds of record-less waves
+    between a node and its parent (the previous wave empty, the parent span
+    blocks away), and a key overwritten across them; every output equals the
+    oracle's in both passes."""
+    rng = np.random.default_rng(0x5EED0009)
+    big = {300: 24 << 20, 700: 40 << 20, 701: 5 << 20}
+    entries = []
+    for i in range(1200):
+        ln = big.get(i, int(rng.integers(1, 3000)))
+        key = b"k-%d" % (i if i != 1100 else 7)  # entry 1100 overwrites key k-7
+        entries.append((xxhash.xxh3_64_intdigest(key), rng.integers(0, 256, ln, dtype=np.uint8).tobytes()))
+    buf = bytearray()
+    t = O.write_entries(buf, 0, entries)
+    store = np.frombuffer(bytes(buf[:t]), np.uint8)
+    r = S.validate_index(store, flags, ctx)
+    ch = O.chain_arrays(store, store.size)
+    assert (r.final_len, r.n_chain, r.n_crc_bad) == (store.size, len(ch), 0)
+    for k in ("meta_off", "key_hash", "prev_offset", "payload_start", "payload_len", "crc_stored", "crc_computed",
+              "crc_ok"):
+        assert np.array_equal(getattr(r, k).astype(np.uint64), ch[k].astype(np.uint64)), k
+    keys, packed = O.key_indexer_arrays(store, store.size)
+    assert len(keys) == 1199
+    o = np.argsort(r.index_key_hash, kind="stable")
+    assert np.array_equal(r.index_key_hash[o], keys) and np.array_equal(r.index_packed[o], packed)
