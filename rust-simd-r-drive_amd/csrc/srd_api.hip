@@ -280,9 +280,16 @@ int upload_tables() {
     for (int tb = 0; tb < 4; tb++)
       for (int b = 0; b < 256; b++) {
         t.m16k[tb][b] = mulp(x16k, (uint32_t)b << (8 * tb));
-        for (int q = 0; q < 3; q++)
+        for (int q = 0; q < 3; q++) {
           t.last[q][tb][b] = mulp(host_xpow8(g_host_tabs, 4 + 16 * (3 - q)), (uint32_t)b << (8 * tb));
+          t.last_c[q][tb][b] = mulp(host_xpow8(g_host_tabs, 4 + 1024 * (3 - q)), (uint32_t)b << (8 * tb));
+        }
+        t.m4096[tb][b] = mulp(host_xpow8(g_host_tabs, 512), (uint32_t)b << (8 * tb));
       }
+    for (int pos = 0; pos < 8; pos++)
+      for (int nb = 0; nb < 16; nb++)
+        for (int l = 0; l < 32; l++)
+          t.nib_c[((pos * 16 + nb) << 5) + l] = mulp(host_xpow8(g_host_tabs, 16 * (31 - l)), (uint32_t)nb << (4 * pos));
   }
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_tabs), &t, sizeof t));
   uploaded |= 1ull << dev;
@@ -2691,9 +2698,8 @@ static int launch_write(Ctx* c, hipStream_t s, const uint8_t* pay, const uint8_t
     write_kernel<1><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
   else if (c->scan_variant == 22)
     write_kernel<2><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
-  else if (c->scan_variant == 25)
-    write_kernel<5><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
-
+  else if (c->scan_variant == 29)
+    write_kernel<9><<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);
   else
 #endif
     write_kernel<<<g, SCAN_WAVES_V2 * 64, 0, s>>>(w);

@@ -67,6 +67,12 @@ struct DevTables {
   uint32_t xtile[65];              // X^e, X = x^32768 (one tile), e = 0..64
   uint32_t xt64[65];               // X^(64 q), q = 0..64 (with xtile: X^n for n < 4160 in one multiply)
   uint32_t mx64[4][256];           // v -> v * X^64 byte tables (the long-entry Horner step)
+  // the writer's coalesced lane layout (lane l holds the 16-byte pieces at
+  // 1024 j + 16 l of a 4 KiB block): the same slice-by-4 chains and lane-
+  // weight nibbles with the pieces' own distances
+  alignas(16) uint32_t last_c[3][4][256];  // v -> v * x^(32 + 8192 (3 - q))
+  alignas(16) uint32_t nib_c[8 * 16 * 32];  // c -> c * x^(128 (31 - l % 32))
+  uint32_t m4096[4][256];                   // v -> v * x^4096 (512 bytes: the half-lanes' distance)
 };
 __device__ DevTables g_tabs;
 #ifdef SRD_WAVE_STAMPS
@@ -470,14 +476,16 @@ __device__ __forceinline__ uint32_t half_suffix_xor(uint32_t v, int lane) {
 // global loads (one table word, 16 B of the nibble tables, 16 B of the last-
 // step tables) before any LDS store, then writes its word's 32 replicas with
 // 16-byte stores (a load -> store loop per word took ~10 us of the scan)
+// COAL: the writer's coalesced lane layout (DevTables::last_c / nib_c)
+template <bool COAL = false>
 __device__ __forceinline__ void load_crc_lds(ScanLds& lds) {
   static_assert(SCAN_WAVES_V2 * 64 == 1024 && sizeof(lds.nib) == 1024 * 16 && sizeof(lds.last) <= 1024 * 16,
                 "one 16-byte piece of nib / last per thread");
   const uint32_t u = threadIdx.x;  // tab word u: hi = u >> 9, b = (u >> 1) & 255, t = 2 hi + (u & 1)
   const uint32_t tv = g_tabs.tab[2 * (u >> 9) + (u & 1)][(u >> 1) & 255];
-  const u32x4 nv = ((const u32x4*)g_tabs.nib)[u];
+  const u32x4 nv = ((const u32x4*)(COAL ? g_tabs.nib_c : g_tabs.nib))[u];
   constexpr uint32_t NLAST = sizeof(lds.last) / 16;
-  const u32x4 lv = ((const u32x4*)&g_tabs.last[0][0][0])[u < NLAST ? u : 0];
+  const u32x4 lv = ((const u32x4*)(COAL ? &g_tabs.last_c[0][0][0] : &g_tabs.last[0][0][0]))[u < NLAST ? u : 0];
   u32x4* const tr = (u32x4*)(lds.tab + 32 * u);  // tab_lookup's layout: word (hi, b, t & 1, copy)
 #pragma unroll
   for (int j = 0; j < 8; j++) tr[j] = u32x4{tv, tv, tv, tv};

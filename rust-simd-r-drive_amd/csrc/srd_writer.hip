@@ -9,10 +9,12 @@
 //
 // One wave per entry (persistent grid of 16-wave blocks): the wave hashes the
 // key, zero-fills the prepad, streams the payload into its 64-byte-aligned
-// place in the output (4 KiB per step, one 64-byte line per lane) while
-// computing its CRC with the scan's LDS line-CRC machinery (crc_line1 +
-// lane weights + a wave XOR-reduce per 4 KiB), and writes the 20-byte
-// metadata (key_hash, prev_offset = the previous tail, crc) after it.
+// place in the output (4 KiB per step; lane l moves the 16-byte pieces at
+// 1024 j + 16 l, so every load and store instruction covers one contiguous
+// KiB) while computing its CRC with the scan's LDS slice-by-4 machinery
+// (four chains per lane, lane weights, a half-wave XOR per 4 KiB, with the
+// pieces' own distances in the tables), and writes the 20-byte metadata
+// (key_hash, prev_offset = the previous tail, crc) after it.
 // The layout (every entry's previous tail) comes from srd_batch_layout on the
 // host: prepad_len makes each start depend on all earlier lengths.
 
@@ -42,6 +44,12 @@ __device__ __forceinline__ uint32_t mul16k_u(uint32_t v) {
       (const __attribute__((address_space(4))) uint32_t*)&g_tabs.m16k[0][0];
   return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
 }
+// v * x^4096 (512 bytes) for a wave-uniform v by scalar loads
+__device__ __forceinline__ uint32_t mul4096_u(uint32_t v) {
+  const __attribute__((address_space(4))) uint32_t* m =
+      (const __attribute__((address_space(4))) uint32_t*)&g_tabs.m4096[0][0];
+  return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
+}
 // v * x^32768 (one 4 KiB block) = two x^16384 steps
 __device__ __forceinline__ uint32_t mul_tile_u(uint32_t v) { return mul16k_u(mul16k_u(v)); }
 // a table word at a wave-uniform index, by a scalar load
@@ -64,23 +72,34 @@ __device__ u32x4 g_wdummy[4];
 // One wave per entry, entries w, w + W, ... of the batch (W waves in the
 // grid).  The 4 KiB blocks of the wave's entries form one sequence; a 2-deep
 // register ring keeps the next block's loads in flight while the current
-// one is stored and checksummed.  Per block: each lane moves its 64-byte
-// line (4 x 16-byte loads and stores) and computes the line's raw CRC from
-// the same registers (crc_line4: four 16-byte slice-by-4 chains, LDS tables
-// as the scan's), weighted by lane (lane_weight_or) and XOR-reduced per half
-// (half_suffix_xor): raw CRC of the block = (lo * x^16384) ^ hi.  The key
-// hashes (XXH3-64, compute_hash.rs:25-27) are computed 64 at a time, one
+// one is stored and checksummed.  Per block: lane l moves its four 16-byte
+// pieces (1024 j + 16 l, j < 4) and computes their raw CRCs from the same
+// registers (crc_line4_wide: one slice-by-4 chain per piece, the last step of
+// pieces 0-2 shifted by their distance to piece 3 -- last_c), weighted by
+// lane (lane_weight_or with nib_c: x^(128 (31 - l % 32))) and XOR-reduced per
+// half-wave (half_suffix_xor): raw CRC of the block = (lo * x^4096) ^ hi.  The
+// key hashes (XXH3-64, compute_hash.rs:25-27) are computed 64 at a time, one
 // entry per lane, not by one lane per entry.
-// V: timing-only ablations of the SRD_DEBUG_API build (wrong outputs):
-// 1 = the copy alone (no CRC), 2 = the CRC alone (no payload stores),
-// 5 = the copy alone with coalesced lanes (16 B at 16 l + 1024 j).
-// Measured (tools/writer_ab.py, profiles/r04/writer_ab.txt): the copy alone
-// takes as long as the whole kernel -- the CRC is hidden; rejected: nontemporal
-// payload stores (2x slower), a 3-deep register ring (+0.6 %)
+// V: variants of the SRD_DEBUG_API build (tools/writer_ab.py): 1 = the copy
+// alone (no CRC, wrong outputs), 2 = the CRC alone (no payload stores, wrong
+// outputs), 9 = round 3's lane = 64-byte line layout.  Measured (one process,
+// two contexts, profiles/r04/writer_ab_*.txt): with lane = line the copy alone
+// took as long as the whole kernel (2.13 vs 2.14 ms) while the runtime's
+// device-to-device copy of the same bytes took 1.56-1.86 ms -- the strided
+// 16-byte stores (each instruction touching every line of the block) were the
+// bound; coalesced stores alone cut the copy to 1.89 ms.  The coalesced lanes
+// with the CRC: 2.02 -> 1.97 ms.  Rejected: nontemporal payload stores (2x
+// slower), a 3-deep register ring (+0.6 %, and +0.5 % with coalesced lanes).
 template <int V = 0>
 __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs a) {
+  // CO (the product layout): coalesced lanes -- lane l moves the 16-byte
+  // pieces at 1024 j + 16 l of each 4 KiB block (one contiguous KiB per load /
+  // store instruction) and checksums them with the same four slice-by-4
+  // chains, the chains' and lanes' distances in their own tables
+  // (DevTables::last_c, nib_c, m4096)
+  constexpr bool CO = V != 9;
   __shared__ ScanLds lds;
-  load_crc_lds(lds);
+  load_crc_lds<CO>(lds);
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t R[4];
@@ -96,12 +115,26 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
   auto vec_line = [&](const srd_write_entry& e, uint64_t b) -> bool {
     return !(e.flags & SRD_ENTRY_TOMB) && pay_al && (e.src & 15) == 0 && b * TILE + 64ull * lane + 64 <= e.len;
   };
+  // CO: piece j of the lane is a whole in-bounds 16-byte vector
+  auto vec_piece = [&](const srd_write_entry& e, uint64_t b, int j) -> bool {
+    return !(e.flags & SRD_ENTRY_TOMB) && pay_al && (e.src & 15) == 0 &&
+           b * TILE + 1024ull * j + 16ull * lane + 16 <= e.len;
+  };
   auto load_blk = [&](const srd_write_entry& e, uint64_t b, uint32_t (&o)[16]) {
-    const u32x4* q = vec_line(e, b) ? (const u32x4*)(a.pay + e.src + b * TILE + (V == 5 ? 16ull : 64ull) * lane)
-                                    : g_wdummy;
+    if constexpr (CO) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const u32x4* q =
+            vec_piece(e, b, j) ? (const u32x4*)(a.pay + e.src + b * TILE + 1024ull * j + 16ull * lane) : &g_wdummy[j];
+        const u32x4 v = *q;
+        o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
+      }
+      return;
+    }
+    const u32x4* q = vec_line(e, b) ? (const u32x4*)(a.pay + e.src + b * TILE + 64ull * lane) : g_wdummy;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const u32x4 v = q[V == 5 ? 64 * j : j];
+      const u32x4 v = q[j];
       o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
     }
   };
@@ -176,8 +209,35 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
         any = 0;
       }
       const uint64_t o = b * TILE + 64ull * lane;
-      const bool vec = vec_line(e, b);
-      if (!vec) {
+      const bool vec = CO ? true : vec_line(e, b);
+      bool vp[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) vp[j] = CO ? vec_piece(e, b, j) : vec;
+      if constexpr (CO) {
+        // a partial (or unaligned) piece: byte by byte, zero past the payload
+        const uint8_t* src = a.pay + e.src;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (!vp[j]) {
+            const uint64_t oj = b * TILE + 1024ull * j + 16ull * lane;
+            const uint32_t nl = oj < e.len ? (uint32_t)min<uint64_t>(16, e.len - oj) : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              uint32_t wd = 0;
+#pragma unroll
+              for (int kb = 0; kb < 4; kb++) {
+                const uint32_t q = 4u * k + kb;
+                if (q < nl) {
+                  const uint8_t v = src[oj + q];
+                  dst[oj + q] = v;
+                  wd |= (uint32_t)v << (8 * kb);
+                }
+              }
+              d[4 * j + k] = wd;
+            }
+          }
+        }
+      } else if (!vec) {
         // a partial (or unaligned) line: byte by byte, zero past the payload
         // (extra memory ops on this path only: the ring's waits stay right)
         const uint32_t nl = o < e.len ? (uint32_t)min<uint64_t>(64, e.len - o) : 0u;
@@ -204,16 +264,16 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
 #pragma unroll
         for (int j = 0; j < 4; j++)
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]}, rb,
-                                                 vec && V != 2 ? (V == 5 ? 16u * lane + 1024u * j : 64u * lane + 16u * j)
-                                                               : OOB_OFF,
+                                                 vp[j] && V != 2 ? (CO ? 16u * lane + 1024u * j : 64u * lane + 16u * j)
+                                                                 : OOB_OFF,
                                                  0, 0);
       }
 #pragma unroll
       for (int j = 0; j < 16; j++) any |= d[j];
       // raw CRC of this 4 KiB block (zero-padded past the payload)
-      const uint32_t hx = (V == 1 || V == 5) ? d[0] ^ d[15] : half_suffix_xor(lane_weight_or(crc_line4_wide(d, lds, R), nib_lane), lane);
+      const uint32_t hx = V == 1 ? d[0] ^ d[15] : half_suffix_xor(lane_weight_or(crc_line4_wide(d, lds, R), nib_lane), lane);
       const uint32_t lo = __builtin_amdgcn_readlane(hx, 0), hi = __builtin_amdgcn_readlane(hx, 32);
-      const uint32_t raw = mul16k_u(lo) ^ hi;
+      const uint32_t raw = (CO ? mul4096_u(lo) : mul16k_u(lo)) ^ hi;
       acc = b ? mul_tile_u(acc) ^ raw : raw;
       if (b + 1 == nb) {
         if (a.null_only && !__ballot(any != 0) && lane == 0) atomicOr(a.null_only, 1u);

@@ -2,10 +2,11 @@
 SRD_DEBUG_API build, `make -C rust-simd-r-drive_amd variant V=dbg
 DEFS=-DSRD_DEBUG_API`): the C5 batch (1M x 4 KiB entries, keys
 bench-key-{i}) with payloads, keys and entries resident in HBM, as bench.py's
-device_resident leg.  Variant 0 is the product kernel, checked against the C2 store; 21 (copy
-alone) and 22 (CRC alone) are timing-only ablations.  Also times the runtime's
+device_resident leg.  Variants 0 (the product kernel, coalesced lanes) and 29 (round 3's lane =
+line layout) are checked against the C2 store; 21 (copy alone) and 22 (CRC
+alone) are timing-only ablations.  Also times the runtime's
 device-to-device copy of the same bytes.
-usage: python tools/writer_ab.py [variants, default 0,21,22]   env: NCTX (2), ROUNDS (6), REPS (5)"""
+usage: python tools/writer_ab.py [variants, default 0,21,22,29]   env: NCTX (2), ROUNDS (6), REPS (5)"""
 import ctypes as C
 import json
 import os
@@ -21,7 +22,7 @@ import srd_amd as S  # noqa: E402
 
 L = S.lib()
 L.srd_debug_set_scan_variant.argtypes = [C.c_void_p, C.c_int]
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,21,22").split(",")]
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,21,22,29").split(",")]
 nctx, rounds, reps = int(os.environ.get("NCTX", 2)), int(os.environ.get("ROUNDS", 6)), int(os.environ.get("REPS", 5))
 n, PL = 1 << 20, 4096
 size = S.synth_store_len(n, PL)
@@ -69,7 +70,7 @@ for rnd in range(rounds):
                 run(c, reps)
                 e1.record()
             torch.cuda.synchronize()
-            if v == 0:
+            if v in (0, 29):
                 assert torch.equal(out[:size], store[:size]), "variant 0 output differs from the C2 store"
             if rnd:
                 res[(i, v)].append(e0.elapsed_time(e1) / reps)
