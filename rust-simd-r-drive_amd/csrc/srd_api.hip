@@ -206,7 +206,7 @@ enum BufId {
   B_O_PIECES, B_O_SUF, B_O_SXM, B_O_TAIL, B_SLOW,
   B_HKEYS, B_HVALS, B_LATEST, B_IPOS, B_IKEY, B_IPACKED,
   B_CUB_TMP,
-  B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HIST, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
+  B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
   B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
@@ -1001,14 +1001,12 @@ static int set_single_root(Ctx* c, uint64_t t) {
 
 // KeyIndexer::build (key_indexer.rs:98-124) as a bucketed build over the
 // pairs (kh[i], mo[i]), i < *n_dev, in file order (latest = last position);
-// *status != 0 disables it.  Scratch (alloc_index): B_HIST = the claimed
-// bucket bases [IDX_HBLOCKS][nbk], B_HOFF = the bucket fills [nbk] (zero
+// *status != 0 disables it.  Scratch (alloc_index): B_HOFF = the bucket fills [nbk] (zero
 // before the claims) followed by the chunk counts [GLUE_BLOCKS], B_SKEY = nbk
 // buckets of IDX_TCAP records, B_LATEST8.  pl->n_index / pl->idx_overflow are
 // written.
 static int alloc_index(Ctx* c, uint64_t n_cap, uint32_t log2_nbk) {
   const uint64_t nbk = (uint64_t)1 << log2_nbk;
-  TRY(ensure(c, B_HIST, nbk * IDX_HBLOCKS * 4));
   TRY(ensure(c, B_HOFF, (nbk + GLUE_BLOCKS) * 4));
   TRY(ensure(c, B_SKEY, nbk * IDX_TCAP * 16));
   TRY(ensure_z(c, B_LATEST8, n_cap + 1));  // zero on (re)allocation: no entry carries a live generation
@@ -1037,7 +1035,6 @@ static uint32_t index_log2_buckets(uint64_t n_est) {
 static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
   IdxArgs ia{};
   ia.log2_nbk = log2_nbk;
-  ia.bbase = P<uint32_t>(c, B_HIST);
   ia.bfill = P<uint32_t>(c, B_HOFF);
   ia.ccount = ia.bfill + ((size_t)1 << log2_nbk);
   ia.srec = P<u64x2>(c, B_SKEY);
@@ -1047,7 +1044,7 @@ static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
 }
 // fused: chain_finalize_kernel already claimed the bucket ranges and wrote
 // the records (child2_kernel zeroed the fills); otherwise the fills are
-// zeroed here, idx_hist_kernel claims the ranges and idx_scatter_kernel fills them
+// zeroed here, and idx_hist_scatter_kernel claims the ranges and fills them
 static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
                                  const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
                                  Plan* pl, bool fused = false, const FinArgs* slow = nullptr, bool zeroed = false) {
@@ -1070,10 +1067,8 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
     uint32_t nz = 0;
     uint32_t* zw = index_zero_words(c, log2_nbk, &nz);
     if (!zeroed) HIPCHK(hipMemsetAsync(zw, 0, (size_t)nz * 4, c->stream));
-    idx_hist_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
-    KCHK(c, "idx_hist_kernel");
-    idx_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
-    KCHK(c, "idx_scatter_kernel");
+    idx_hist_scatter_kernel<<<IDX_HBLOCKS, 256, nbk * 4, c->stream>>>(ia);
+    KCHK(c, "idx_hist_scatter_kernel");
   }
   FinArgs fs{};  // n_slow == nullptr: no slow list
   if (slow) fs = *slow;

@@ -417,11 +417,9 @@ struct IdxArgs {
   const uint32_t* status;
   uint32_t log2_nbk;
   // Buckets of fixed capacity IDX_TCAP: bucket k owns srec[k*IDX_TCAP, ...).
-  // Each histogram block claims a range per bucket with one atomicAdd on
-  // bfill[k] (no histogram scan); bbase[b*nbk + k] = block b's first slot.
-  // bfill (nbk) is zero before the claims.
+  // Each block claims a range per bucket with one atomicAdd on bfill[k] (no
+  // histogram scan).  bfill (nbk) is zero before the claims.
   uint32_t* bfill;
-  uint32_t* bbase;       // [IDX_HBLOCKS * nbk]
   u64x2* srec;           // (key, chain index) per entry, in its bucket's range
   uint8_t* latest;       // [n] == lgen: NOT the latest entry of its key (idx_dedup writes only those)
   uint8_t lgen;          // this build's generation (1..255; the host clears the array on wrap)
@@ -440,13 +438,6 @@ struct IdxArgs {
 
 __device__ __forceinline__ uint64_t idx_n(const IdxArgs& a) { return *a.status ? 0 : *a.n_dev; }
 
-// block b's per-bucket counts (LDS) -> claimed ranges of the buckets
-__device__ __forceinline__ void idx_claim(const IdxArgs& a, const uint32_t* hist, uint32_t nbk, uint32_t b) {
-  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) {
-    const uint32_t n = hist[k];
-    a.bbase[(uint64_t)b * nbk + k] = n ? atomicAdd(&a.bfill[k], n) : 0u;
-  }
-}
 // ---------------------------------------------------------------------------
 // The plan (every block decides it from the same inputs; block 0 publishes
 // it) fused with the whole per-entry stage: chain rank of every core node
@@ -837,7 +828,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
 // --------------------------------------------------------------------------
 // KeyIndexer::build, bucketed
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void idx_hist_kernel(IdxArgs a) {
+// KeyIndexer::build's bucketing in one launch: each block histograms its chunk in LDS, claims its
+// ranges of the buckets (one atomicAdd per bucket) and scatters the chunk --
+// no per-(block, bucket) base table in HBM and the keys read once more from
+// L2 instead of from a second launch (dedup takes the latest position, so the
+// order inside a bucket does not matter)
+__global__ __launch_bounds__(256) void idx_hist_scatter_kernel(IdxArgs a) {
   extern __shared__ uint32_t lds_u32[];
   const uint32_t nbk = 1u << a.log2_nbk;
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = 0;
@@ -847,16 +843,11 @@ __global__ __launch_bounds__(256) void idx_hist_kernel(IdxArgs a) {
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x)
     atomicAdd(&lds_u32[xxh3_64_u64(a.kh[c]) >> (64 - a.log2_nbk)], 1u);
   __syncthreads();
-  idx_claim(a, lds_u32, nbk, blockIdx.x);
-}
-
-__global__ __launch_bounds__(256) void idx_scatter_kernel(IdxArgs a) {
-  extern __shared__ uint32_t lds_u32[];
-  const uint32_t nbk = 1u << a.log2_nbk;
-  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) lds_u32[k] = a.bbase[(uint64_t)blockIdx.x * nbk + k];
+  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) {
+    const uint32_t n = lds_u32[k];
+    lds_u32[k] = n ? atomicAdd(&a.bfill[k], n) : 0u;
+  }
   __syncthreads();
-  uint64_t lo, hi;
-  chunk_of(idx_n(a), &lo, &hi);
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) {
     const uint64_t k = a.kh[c];
     const uint32_t bk = (uint32_t)(xxh3_64_u64(k) >> (64 - a.log2_nbk));
