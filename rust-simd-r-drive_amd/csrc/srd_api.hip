@@ -374,6 +374,11 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 11>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 12) {
     hipExtLaunchKernelGGL(scan_kernel<FULL, false, 12>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 13) {
+    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 13>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 14) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 14>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 14>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 10) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 10>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 10>, grid, block, 0, s, e0, e1, 0, a);

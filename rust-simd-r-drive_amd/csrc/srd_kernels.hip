@@ -630,6 +630,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // timing-only ablations (results not checked): 11 = coalesced tile loads
   // (lane l, load j reads 16 B at 1024 j + 16 l), 12 = 11 memory-only
   constexpr bool COAL = V == 11 || V == 12;
+  // 13 = timing-only: none of process()'s six per-tile stores (tile values,
+  // records, span counts) -- what their VMEM issue slots cost
+  constexpr bool NOSTORE = V == 13;
+  // 14 = the per-tile store points of round 3 (a store point after every
+  // tile instead of after every ring round)
+  constexpr bool TILE_SP = V == 14 || RING2;
   uint32_t memonly_acc = 0;
   __shared__ ScanLds lds;
   // lanes of the record queue rq: with F1 its lane 63 is scratch
@@ -686,7 +692,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   bool ovf = false;     // wave-uniform: a span had more candidates than slots
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
-  uint32_t tacc = 0, scnt = 0, sfirst = 0;
+  uint32_t tacc = 0;
+  // the span that ended since the last store point (uniform; at most one:
+  // a store point closes every ring round of 3 tiles, a span has 4)
+  bool se_pend = false;
+  uint64_t se_span = 0;
+  uint32_t se_cnt = 0, se_first = 0;
   uint32_t rq[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) rq[i] = 0;
@@ -920,13 +931,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       tacc = writelane_u32(v0, 4 * t, tacc);
       tacc = writelane_u32(v1, 4 * t + 1, tacc);
       tacc = writelane_u32(v2, 4 * t + 2, tacc);
-      const bool flush = t == 15 || k + 1 == k1;  // uniform
-      const uint64_t g = k & ~15ull;
-      const uint32_t lo = (uint32_t)(max(g, k0) - g) * 4;
-      // branch-free (a uniform branch here split the tile's basic block)
-      const uint32_t lo2 = flush ? lo : 0u, n2 = flush ? 4u * t + 4u - lo : 0u;
-      const uint32_t off = (uint32_t)lane - lo2 < n2 ? 4u * lane : OOB_OFF;
-      __builtin_amdgcn_raw_buffer_store_b32(tacc, out_rsrc(a.tile + 4 * g, 256), off, 0, 0);
     }
 
     if constexpr (F1 && F1_AFTER && !FULL) {
@@ -1151,14 +1155,40 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       for (int j = 0; j < 4; j++) win[j] = d[12 + j];
       win[22] = hx;
     }
-    // span end: the span's buffered records (slot = lane) and its count
-    // (lane span%64 of scnt, one store per 64 spans) -- unconditional stores
-    const bool span_end = (k + 1) % SPAN_TILES == 0 || k + 1 == k1;  // uniform
+    // span end: its record count and first record (stored at the next store point)
+    if ((k + 1) % SPAN_TILES == 0 || k + 1 == k1) {  // uniform
+      se_pend = true;
+      se_span = span;
+      se_cnt = count;
+      se_first = (uint32_t)wtotal;
+      wtotal += count;
+      count = 0;
+    }
+  };
+
+  // A store point after the tiles [kf, kf + nt): their per-tile values
+  // (lanes 4 (k % 16) + j of tacc), the buffered records once >= FLUSH_AT are
+  // pending (and at the wave's end), the ended span's count / first record.
+  // Six UNCONDITIONAL buffer stores whose unused lanes carry an out-of-range
+  // offset (dropped by the hardware): a store under a branch makes the count
+  // of memory ops between a prefetch load and its wait path-dependent, and
+  // the compiler then waits for the store's completion too (~10 % of the
+  // kernel).  Their issue slots are not free either (all six per tile cost
+  // 7-8 %, profiles/r04/variant_ab_no_stores.txt), so the ring loop runs one
+  // store point per round of 3 tiles, not one per tile.
+  auto store_point = [&](uint64_t kf, uint32_t nt) {
+    if constexpr (MEMONLY || NOSTORE) return;
+    const bool last = kf + nt == k1;  // uniform
+    {
+      const uint32_t dd = (((uint32_t)lane >> 2) - (uint32_t)(kf & 15)) & 15u;
+      const uint32_t off = dd < nt ? 16u * dd + 4u * ((uint32_t)lane & 3u) : OOB_OFF;
+      __builtin_amdgcn_raw_buffer_store_b32(tacc, out_rsrc(a.tile + 4 * kf, 16u * nt), off, 0, 0);
+    }
     {
       // (optimistic pass only; the full pass stores its records directly)
       constexpr uint64_t FLUSH_AT = 40;
       const uint64_t pend = wtotal + count - flushed;  // records pending (lanes [0, min(pend, 64)))
-      const bool fl = span_end && (pend >= FLUSH_AT || k + 1 == k1);  // uniform
+      const bool fl = pend >= FLUSH_AT || last;  // uniform
       const bool wr = fl && ((rvalid >> lane) & 1);
       const uint64_t rb = w * a.wcap + flushed;  // lane 0's record
       const uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
@@ -1168,23 +1198,17 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
                                              wr ? 32u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
                                              wr ? 32u * lane + 16u : OOB_OFF, 0, 0);
-      const uint32_t sp = (uint32_t)(span & 63);
-      scnt = (span_end && (uint32_t)lane == sp) ? count : scnt;
-      sfirst = (span_end && (uint32_t)lane == sp) ? (uint32_t)wtotal : sfirst;
-      const bool sfl = span_end && (sp == 63 || k + 1 == k1);
-      const uint64_t sg = span & ~63ull;
-      const uint32_t slo = (uint32_t)(max(sg, k0 / SPAN_TILES) - sg);
-      const uint32_t soff = (sfl && (uint32_t)lane >= slo && (uint32_t)lane <= sp) ? 4u * lane : OOB_OFF;
-      __builtin_amdgcn_raw_buffer_store_b32(scnt, out_rsrc(a.span_count + sg, 256), soff, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(sfirst, out_rsrc(a.span_first + sg, 256), soff, 0, 0);
-      if (span_end) {
-        wtotal += count;
-        count = 0;
-        if (fl) {
-          flushed = wtotal;
-          rvalid = 0;
-        }
+      if (fl) {
+        flushed = wtotal + count;
+        rvalid = 0;
       }
+    }
+    {
+      const uint64_t sg = se_span & ~63ull;
+      const uint32_t soff = se_pend && (uint32_t)lane == (uint32_t)(se_span & 63) ? 4u * lane : OOB_OFF;
+      __builtin_amdgcn_raw_buffer_store_b32(se_cnt, out_rsrc(a.span_count + sg, 256), soff, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(se_first, out_rsrc(a.span_first + sg, 256), soff, 0, 0);
+      se_pend = false;
     }
   };
 
@@ -1207,7 +1231,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // Dummy stores (out-of-range offsets: dropped by the hardware; distinct,
   // or the compiler merges them as dead stores) give the entry the same queue.
   auto pad_stores = [&](uint32_t g) {
-    constexpr uint32_t NST = 6u;  // process()'s unconditional stores
+    constexpr uint32_t NST = (NOSTORE || MEMONLY) ? 0u : 6u;  // a store point's unconditional stores
 #pragma unroll
     for (uint32_t i = 0; i < NST; i++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, out_rsrc(a.tile, 256), OOB_OFF - 64u * (NST * g + i), 0, 0);
@@ -1218,8 +1242,11 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // ring tiles run in the unpipelined loop below with the file's tail tiles.
   constexpr uint32_t RD = RING2 ? 2 : 3;  // ring depth
   const uint32_t nfull = nk / RD;
+  // (the entry's queue = the loop latch's: with a store point per tile the
+  // stores of one tile follow every load; with one per round, only tile
+  // B's loads have a store point behind them before the loop comes round)
   load_tile(k0, A);
-  pad_stores(0);
+  if constexpr (TILE_SP) pad_stores(0);
   if constexpr (!RING2) {
     load_tile(k0 + 1, Bv);
     pad_stores(1);
@@ -1233,19 +1260,25 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       __builtin_amdgcn_s_setprio(3);
       load_tile(k0 + min(j + 1, nk), Bv);
       process(k0 + j, A, body);
+      store_point(k0 + j, 1);
       __builtin_amdgcn_s_setprio(3);
       load_tile(k0 + min(j + 2, nk), A);
       process(k0 + j + 1, Bv, body);
+      store_point(k0 + j + 1, 1);
     } else {
       __builtin_amdgcn_s_setprio(3);
       load_tile(k0 + min(j + 2, nk), Cv);
       process(k0 + j, A, body);
+      if constexpr (TILE_SP) store_point(k0 + j, 1);
       __builtin_amdgcn_s_setprio(3);
       load_tile(k0 + min(j + 3, nk), A);
       process(k0 + j + 1, Bv, body);
+      if constexpr (TILE_SP) store_point(k0 + j + 1, 1);
       __builtin_amdgcn_s_setprio(3);
       load_tile(k0 + min(j + 4, nk), Bv);
       process(k0 + j + 2, Cv, body);
+      if constexpr (TILE_SP) store_point(k0 + j + 2, 1);
+      else store_point(k0 + j, 3);
     }
   }
   const uint64_t kr = k0 + (uint64_t)RD * nfull;
@@ -1254,6 +1287,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   for (uint64_t k = kr; k < k1; k++) {
     load_tile(k, A);
     process(k, A, std::true_type{});
+    store_point(k, 1);
   }
 
   if constexpr (MEMONLY) {
