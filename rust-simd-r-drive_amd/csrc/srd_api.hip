@@ -212,7 +212,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
-  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN, B_DEFER,
+  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN,
   B_COUNT_
 };
 
@@ -1092,7 +1092,6 @@ static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo,
 // pass (the check could not prove the chain from file_len).
 static int alloc_fast(Ctx* c, uint64_t capK, uint32_t log2_nbk) {
   TRY(ensure(c, B_DPAR, capK * 4));
-  TRY(ensure(c, B_DEFER, capK * 4));
   TRY(ensure_z(c, B_HASCHILD, capK * 4));
   TRY(ensure_z(c, B_HASCHILD2, capK * 4));
   TRY(ensure_z(c, B_CHILDOF, capK * 8));
@@ -1179,7 +1178,6 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.childof = P<unsigned long long>(c, B_CHILDOF);
     a.gen = c->gen;
     a.span_lo = lo;
-    a.defer = P<uint32_t>(c, B_DEFER);
     a.zero2 = index_zero_words(c, log2_nbk, &a.n_zero2);
     TRY(scan_wave_args(c, &a));
     hipEvent_t e0, e1;
@@ -1194,6 +1192,9 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       return 0;
     }
 #endif
+    // every record's node test, parent and claim (slot space), one block per scan wave
+    link2_kernel<<<(unsigned)total_waves, 256, 0, c->stream>>>(a);
+    KCHK(c, "link2_kernel");
     // ---- shape check, chain, finalize, index; retried on device with more
     //      prune rounds when false candidates chained onto each other ----
     Plan hp{};

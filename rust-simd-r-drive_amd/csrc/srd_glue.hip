@@ -6,16 +6,15 @@
 // waits once, on the outcome idx_emit publishes to pinned host memory:
 //
 //   scan            (srd_kernels.hip) strong candidates only, each wave's
-//                   records dense in its region (ScanPart); then every block
-//                   links its own records (link_record: node test of
-//                   single-candidate records, parent lookup -- the previous
-//                   record, else a binary search in the parent's span -- and
-//                   the claim on the parent, the earliest claimer winning,
-//                   claim_word) while slower blocks still scan; the last
-//                   block links the records that needed another block's
-//                   waves.  Slot space throughout: record r of wave w is
-//                   slot w*wcap + r.  Block 0 zeroes the plan and the index
-//                   bucket fills
+//                   records dense in its region (ScanPart); block 0 zeroes
+//                   the plan and the index bucket fills
+//   link2           (srd_kernels.hip) one block per scan wave: every
+//                   record's node test, parent (the previous record, else a
+//                   binary search in the parent's span, skipped when the
+//                   would-be parent's prev field rules a record out) and the
+//                   claim on it, the earliest claimer winning (claim_word).
+//                   Slot space throughout: record r of wave w is slot
+//                   w*wcap + r
 //   check           shape test from the claims alone: the core nodes (claimed
 //                   by someone, or the start node at file_len - 20) must form
 //                   ONE chain from the start down to a root -- each core node's

@@ -162,16 +162,13 @@ struct ScanArgs {
   // (the full pass keeps span*cap + slot)
   uint32_t* span_first;
   uint64_t wcap;
-  // optimistic pass (d_par != nullptr): every block links its own waves'
-  // records once its tiles are done (link_record, in slot space: record r of
-  // wave w is slot w*wcap + r), hidden under the other blocks' scan; a record
-  // that needs a wave of another block goes to defer[] (count: done[1]) and
-  // the last block links it.  k_total[1] = 1 + the slot of the last record (0: none)
+  // the link step (link2_kernel, over the same arguments) works in slot
+  // space: record r of wave w is slot w*wcap + r.  k_total[1] = 1 + the slot
+  // of the last record (0: none)
   int32_t* d_par;                  // [slots] the parent's slot, PAR_ROOT or PAR_MISS
   unsigned long long* childof;     // [slots] claims on parents (claim_word)
   uint32_t gen;                    // this call's claim generation
   uint64_t span_lo;                // span mode: the shard's lower tail (0 = whole file)
-  uint32_t* defer;                 // [slots]
   uint32_t* zero2;                 // zeroed by block 0 as well: the index's bucket fills
   uint32_t n_zero2;
   // host-side only: the scan variant to launch (0 = the build's default;
@@ -551,10 +548,8 @@ __device__ __forceinline__ uint64_t find_top(const uint8_t* file, uint64_t flen,
 // the scan): the deferred node test of a single-candidate record
 // (data_store.rs:404-470), its parent -- the previous record in file order
 // when that record's metadata sits at p - 20, else a binary search in the
-// parent's span -- and the claim on it (the earliest claimer wins).  Waves
-// [wlo, whi) are readable; false = the record needs another wave (nothing
-// was written: the caller defers it).
-__device__ bool link_record(const ScanArgs& a, uint64_t w, uint64_t r, uint64_t wlo, uint64_t whi) {
+// parent's span -- and the claim on it (the earliest claimer wins).
+__device__ void link_record(const ScanArgs& a, uint64_t w, uint64_t r) {
   const uint64_t gi = w * a.wcap + r;
   uint64_t gprev = 0;
   bool hp = true;
@@ -563,7 +558,6 @@ __device__ bool link_record(const ScanArgs& a, uint64_t w, uint64_t r, uint64_t 
   } else if (w == 0) {
     hp = false;  // the first resident record: nothing before it is resident
   } else {
-    if (w - 1 < wlo) return false;
     const uint64_t wt = a.wave_total[w - 1] & ~(1ull << 63);
     hp = wt > 0 && wt <= a.wcap;  // an overflowed wave fails the pass anyway (ST_OVERFLOW)
     gprev = (w - 1) * a.wcap + (hp ? wt - 1 : 0);
@@ -583,9 +577,19 @@ __device__ bool link_record(const ScanArgs& a, uint64_t w, uint64_t r, uint64_t 
   const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // span s holds m in [16 KiB s - 14, +16 KiB)
   // in a store without garbage the parent is the previous record: one load
   int64_t par = hp && mprev == mp ? (int64_t)gprev : PAR_MISS;
-  if (node && par == PAR_MISS && sp2 >= a.part.s_lo && sp2 < a.n_spans) {
+  // Otherwise a record at mp needs mp's prev field pp = u64 at p - 12 with
+  // 20 <= pp < mp (every record is a strong node, data_store.rs:404-470).
+  // One 8-byte file read settles most misses here: a false candidate's p is
+  // whatever its checksum bytes held (C3: ~940 K of them per call, p
+  // anywhere in the first 4 GiB), whose "parent" bytes are payload: no
+  // binary search in a random span for it.  pp == 0 is the root rule below.
+  // (Resident bytes only: in span mode p - 20 may lie below the span.)
+  uint64_t pp = 1;
+  const bool res = mp >= a.k_lo * (uint64_t)TILE;
+  if (node && par == PAR_MISS && res) pp = ld_u64_unaligned(a.file, p - 12);
+  const bool maybe_rec = !res || (pp >= 20 && pp < mp);
+  if (node && par == PAR_MISS && maybe_rec && sp2 >= a.part.s_lo && sp2 < a.n_spans) {
     const uint64_t w2 = part_span_wave(a.part, sp2 - a.part.s_lo);
-    if (w2 < wlo || w2 >= whi) return false;
     const uint32_t f2 = a.span_first[sp2];
     const uint32_t n2 = (uint32_t)min<uint64_t>(a.span_count[sp2], a.wcap - min<uint64_t>(f2, a.wcap));
     uint32_t lo = 0, hi = n2;
@@ -601,14 +605,26 @@ __device__ bool link_record(const ScanArgs& a, uint64_t w, uint64_t r, uint64_t 
   } else if (par == PAR_MISS) {
     if (a.span_lo) {
       if (p == a.span_lo) par = PAR_ROOT;  // the shard's first entry (its parent is the previous shard's last)
-    } else if (p >= 21 && ld_u64_unaligned(a.file, p - 12) == 0) {
+    } else if (p >= 21 && pp == 0) {
       par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
     }
   }
   if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
   a.d_par[gi] = (int32_t)par;
   if (par >= 0) atomicMax(&a.childof[par], claim_word(a.gen, gi));
-  return true;
+}
+
+// The link step (optimistic pass), one block per scan wave right after the
+// scan: every record of the wave's region through link_record.  (Round 4
+// tried it inside the scan's epilogue -- each block linking its own records
+// once its tiles were done, the last block the records that needed another
+// block's: the early blocks' work hid, but the last block's ~4 K (C2) to
+// ~40 K (C3) records in one block sat on the scan's critical path, and the
+// scan ran 6 % (C2) to 11 % (C3) longer for a 22 us kernel saved.)
+__global__ __launch_bounds__(256) void link2_kernel(ScanArgs a) {
+  const uint64_t w = blockIdx.x;
+  const uint64_t nrec = min(a.wave_total[w] & ~(1ull << 63), a.wcap);  // records past wcap: ST_OVERFLOW
+  for (uint64_t r = threadIdx.x; r < nrec; r += blockDim.x) link_record(a, w, r);
 }
 
 template <bool FULL, bool WIDE, int V = 0>
@@ -692,12 +708,16 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   bool ovf = false;     // wave-uniform: a span had more candidates than slots
   // store batching (registers, flushed with few wide stores): per-tile values
   // of 16 tiles, span counts of 64 spans, and up to 64 records of the span
-  uint32_t tacc = 0;
-  // the span that ended since the last store point (uniform; at most one:
-  // a store point closes every ring round of 3 tiles, a span has 4)
-  bool se_pend = false;
-  uint64_t se_span = 0;
-  uint32_t se_cnt = 0, se_first = 0;
+  // per-tile values, lanes 4 (k % 16) + j of the 16-tile group's register
+  // (two: a group can complete in the middle of a ring round, whose later
+  // tiles already fill the next group), and span counts / first records in
+  // lane span % 64 of scnt / sfirst; stored by the next store point once a
+  // group completes (16 tiles, 64 spans) or the wave ends -- few, whole-line
+  // stores (one real store per tile and per span was 15 % of the scan)
+  uint32_t tacc0 = 0, tacc1 = 0, scnt = 0, sfirst = 0;
+  bool tg_pend = false, sg_pend = false;  // uniform: a group to store
+  uint64_t tg_base = 0, sg_base = 0;
+  uint32_t tg_par = 0, tg_lo = 0, tg_hi = 0, sg_lo = 0, sg_hi = 0;
   uint32_t rq[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) rq[i] = 0;
@@ -928,9 +948,22 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const int t = (int)(k & 15);
       const uint32_t v0 = __builtin_amdgcn_readlane(hx, 0), v1 = __builtin_amdgcn_readlane(hx, 1),
                      v2 = __builtin_amdgcn_readlane(hx, 32);
-      tacc = writelane_u32(v0, 4 * t, tacc);
-      tacc = writelane_u32(v1, 4 * t + 1, tacc);
-      tacc = writelane_u32(v2, 4 * t + 2, tacc);
+      // (branch-free: a uniform branch here split the tile's basic block)
+      const bool odd = (k >> 4) & 1;
+      uint32_t tv = odd ? tacc1 : tacc0;
+      tv = writelane_u32(v0, 4 * t, tv);
+      tv = writelane_u32(v1, 4 * t + 1, tv);
+      tv = writelane_u32(v2, 4 * t + 2, tv);
+      tacc0 = odd ? tacc0 : tv;
+      tacc1 = odd ? tv : tacc1;
+      if (t == 15 || k + 1 == k1) {  // uniform: the group is complete
+        const uint64_t g = k & ~15ull;
+        tg_pend = true;
+        tg_base = g;
+        tg_par = odd ? 1u : 0u;
+        tg_lo = (uint32_t)(max(g, k0) - g) * 4;
+        tg_hi = 4u * t + 4u;
+      }
     }
 
     if constexpr (F1 && F1_AFTER && !FULL) {
@@ -939,7 +972,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     }
     if constexpr (F1 && !FULL) {
       // the first flagged line's record (at most one candidate: the node test
-      // is link_record's, F_NT) into the register queue; lane 63 of rq is scratch
+      // is link_record', F_NT) into the register queue; lane 63 of rq is scratch
       // (a tile without a record writes there), so the queue holds 63
       const bool single = f1_pm != 0;  // uniform
       const int bl = single ? __builtin_ctzll(f1_pm) : 0;
@@ -1155,34 +1188,41 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       for (int j = 0; j < 4; j++) win[j] = d[12 + j];
       win[22] = hx;
     }
-    // span end: its record count and first record (stored at the next store point)
+    // span end: its record count and first record into lane span % 64
     if ((k + 1) % SPAN_TILES == 0 || k + 1 == k1) {  // uniform
-      se_pend = true;
-      se_span = span;
-      se_cnt = count;
-      se_first = (uint32_t)wtotal;
+      const uint32_t sp = (uint32_t)(span & 63);
+      scnt = (uint32_t)lane == sp ? count : scnt;
+      sfirst = (uint32_t)lane == sp ? (uint32_t)wtotal : sfirst;
+      if (sp == 63 || k + 1 == k1) {  // the 64-span group is complete
+        const uint64_t sg = span & ~63ull;
+        sg_pend = true;
+        sg_base = sg;
+        sg_lo = (uint32_t)(max(sg, k0 / SPAN_TILES) - sg);
+        sg_hi = sp;
+      }
       wtotal += count;
       count = 0;
     }
   };
 
-  // A store point after the tiles [kf, kf + nt): their per-tile values
-  // (lanes 4 (k % 16) + j of tacc), the buffered records once >= FLUSH_AT are
-  // pending (and at the wave's end), the ended span's count / first record.
-  // Six UNCONDITIONAL buffer stores whose unused lanes carry an out-of-range
-  // offset (dropped by the hardware): a store under a branch makes the count
-  // of memory ops between a prefetch load and its wait path-dependent, and
-  // the compiler then waits for the store's completion too (~10 % of the
-  // kernel).  Their issue slots are not free either (all six per tile cost
-  // 7-8 %, profiles/r04/variant_ab_no_stores.txt), so the ring loop runs one
-  // store point per round of 3 tiles, not one per tile.
+  // A store point after the tiles [kf, kf + nt): a completed 16-tile group
+  // of per-tile values, the buffered records once >= FLUSH_AT are pending
+  // (and at the wave's end), a completed 64-span group of span counts / first
+  // records.  Six UNCONDITIONAL buffer stores whose unused lanes carry an
+  // out-of-range offset (dropped by the hardware): a store under a branch
+  // makes the count of memory ops between a prefetch load and its wait
+  // path-dependent, and the compiler then waits for the store's completion
+  // too (~10 % of the kernel).  Their issue slots are not free either (all
+  // six per tile cost 7-8 %, profiles/r04/variant_ab_no_stores.txt), so the
+  // ring loop runs one store point per round of 3 tiles, not one per tile (a
+  // round completes at most one group of either kind).
   auto store_point = [&](uint64_t kf, uint32_t nt) {
     if constexpr (MEMONLY || NOSTORE) return;
     const bool last = kf + nt == k1;  // uniform
     {
-      const uint32_t dd = (((uint32_t)lane >> 2) - (uint32_t)(kf & 15)) & 15u;
-      const uint32_t off = dd < nt ? 16u * dd + 4u * ((uint32_t)lane & 3u) : OOB_OFF;
-      __builtin_amdgcn_raw_buffer_store_b32(tacc, out_rsrc(a.tile + 4 * kf, 16u * nt), off, 0, 0);
+      const uint32_t off = tg_pend && (uint32_t)lane - tg_lo < tg_hi - tg_lo ? 4u * lane : OOB_OFF;
+      __builtin_amdgcn_raw_buffer_store_b32(tg_par ? tacc1 : tacc0, out_rsrc(a.tile + 4 * tg_base, 256), off, 0, 0);
+      tg_pend = false;
     }
     {
       // (optimistic pass only; the full pass stores its records directly)
@@ -1204,11 +1244,10 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       }
     }
     {
-      const uint64_t sg = se_span & ~63ull;
-      const uint32_t soff = se_pend && (uint32_t)lane == (uint32_t)(se_span & 63) ? 4u * lane : OOB_OFF;
-      __builtin_amdgcn_raw_buffer_store_b32(se_cnt, out_rsrc(a.span_count + sg, 256), soff, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(se_first, out_rsrc(a.span_first + sg, 256), soff, 0, 0);
-      se_pend = false;
+      const uint32_t soff = sg_pend && (uint32_t)lane >= sg_lo && (uint32_t)lane <= sg_hi ? 4u * lane : OOB_OFF;
+      __builtin_amdgcn_raw_buffer_store_b32(scnt, out_rsrc(a.span_count + sg_base, 256), soff, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(sfirst, out_rsrc(a.span_first + sg_base, 256), soff, 0, 0);
+      sg_pend = false;
     }
   };
 
@@ -1293,43 +1332,18 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   if constexpr (MEMONLY) {
     if (memonly_acc == 0x12345678u) a.counters[3] = memonly_acc;  // (keeps the loads)
   }
-  // ---- epilogue: per-wave results; the optimistic pass links the block's
-  // records; the last block to finish reduces the per-wave results and links
-  // the deferred records (cdna guide: plain stores, vmcnt(0), barrier, lane-0
-  // agent release, add; the last block acquires before reading) ----
-  const bool link = a.d_par != nullptr;  // uniform
-  uint32_t* s_pre = (uint32_t*)lds.s_ovf;  // [17] prefix of the block's wave record counts
+  // ---- epilogue: per-wave results; the last block to finish reduces them
+  // (cdna guide: plain stores, vmcnt(0), barrier, lane-0 agent release, add;
+  // the last block acquires before reading) ----
   if (lane == 0) {
     a.wave_total[w] = wtotal | (ovf ? (1ull << 63) : 0ull);
     a.wave_root[w] = rootmax;  // wave-uniform already
-    if (link) s_pre[wv + 1] = (uint32_t)min<uint64_t>(wtotal, a.wcap);  // records past wcap were not stored
 #ifdef SRD_WAVE_STAMPS  // timing-only build (tools/wave_stamps.py): each wave's end, 100 MHz clock
     if (w < 8192) g_wave_stamp[w] = __builtin_amdgcn_s_memrealtime();
 #endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (link) {
-    // the block's records in file order (its 16 waves' regions, flattened);
-    // their records and counts are visible to the whole block now
-    if (threadIdx.x == 0) {
-      s_pre[0] = 0;
-      for (int v = 0; v < SCAN_WAVES_V2; v++) s_pre[v + 1] += s_pre[v];
-    }
-    __syncthreads();
-    const uint32_t n = s_pre[SCAN_WAVES_V2];
-    const uint64_t w0 = (uint64_t)blockIdx.x * SCAN_WAVES_V2;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      uint32_t v = 0;  // the largest v with s_pre[v] <= i: record i's wave
-#pragma unroll
-      for (uint32_t st = SCAN_WAVES_V2 / 2; st; st >>= 1) v += s_pre[v + st] <= i ? st : 0u;
-      const uint64_t r = i - s_pre[v];
-      if (!link_record(a, w0 + v, r, w0, w0 + SCAN_WAVES_V2))
-        a.defer[atomicAdd(&a.done[1], 1u)] = (uint32_t)((w0 + v) * a.wcap + r);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
   uint32_t& s_last = lds.s_last;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1400,16 +1414,6 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 #ifdef SRD_WAVE_STAMPS
     g_wave_stamp[8192 + 1023] = __builtin_amdgcn_s_memrealtime();
 #endif
-  }
-  if (link) {
-    // the deferred records: every wave is readable now
-    const uint32_t nd = a.done[1];
-    __syncthreads();
-    if (t == 0) a.done[1] = 0;
-    for (uint32_t i = t; i < nd; i += T) {
-      const uint64_t slot = a.defer[i], wd = slot / a.wcap;
-      link_record(a, wd, slot - wd * a.wcap, 0, total_waves);
-    }
   }
 }
 

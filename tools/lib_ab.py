@@ -39,8 +39,10 @@ t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
 S.synth_store_device(t.data_ptr(), n, 4096, lens, seed=seed)
 torch.cuda.synchronize()
 ctxs = []
-for b, L in enumerate(libs):
-    for _ in range(nctx):
+# contexts created round-robin over the builds (contexts created first have
+# run slower in some processes: no build gets all the early ones)
+for _ in range(nctx):
+    for b, L in enumerate(libs):
         h = C.c_void_p()
         assert L.srd_ctx_create(0, C.byref(h)) == 0
         assert L.srd_ctx_set_timing(h, S.TIMING_SCAN) == 0
