@@ -592,9 +592,19 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
       if (k0 == k1) {
         y = acc ^ sxm;
       } else {
-        // one tile step: v * x^32768 = (v * x^16384) * x^16384, two table multiplies
-        for (uint64_t k = k0 + 1; k < k1; k++)
-          acc = mul16k_lds(m16k, mul16k_lds(m16k, acc)) ^ tile_T(a.tile, k);
+        // one tile step: v * x^32768 = (v * x^16384) * x^16384, two table
+        // multiplies; the whole tiles' values loaded 4 at a time (their loads
+        // do not wait for the chain)
+        const u32x4* t4 = (const u32x4*)a.tile;
+        for (uint64_t kb = k0 + 1; kb < k1; kb += 4) {
+          u32x4 tv[4];
+#pragma unroll
+          for (int q = 0; q < 4; q++) tv[q] = t4[kb + q < k1 ? kb + q : k1];
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (kb + q < k1)  // tile_T(k) = mul16k(T_lo) ^ SX_32
+              acc = mul16k_lds(m16k, mul16k_lds(m16k, acc)) ^ mul16k_lds(m16k, tv[q][0]) ^ tv[q][2];
+        }
         y = mul16k_lds(m16k, mul16k_lds(m16k, acc)) ^ (mul16k_lds(m16k, e.t1[0]) ^ e.t1[2]) ^ sxm;
       }
       crc = ~(mulp(t.invpow[(k1 + 1) * TILE - mo], y) ^ tail);

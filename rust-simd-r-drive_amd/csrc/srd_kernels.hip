@@ -1751,7 +1751,14 @@ __device__ __forceinline__ uint32_t crc_from_pieces(uint64_t s, uint64_t m, uint
   return ~(mulp(g_tabs.invpow[dd], y) ^ tail);
 }
 
-constexpr uint64_t LONG_TILES = 4;  // whole tiles a finalize thread combines serially
+// whole tiles a finalize thread combines serially (longer entries go to the
+// slow list, a wave each).  C3 glue (tools/lib_ab.py, contexts interleaved):
+// 4 -> 1.66 ms, 8 -> 1.61, 16 -> 1.57, 32 -> 1.57; C2 (entries of 2 tiles)
+// unchanged
+#ifndef SRD_LONG_TILES
+#define SRD_LONG_TILES 16
+#endif
+constexpr uint64_t LONG_TILES = SRD_LONG_TILES;
 constexpr uint64_t NO_REC = ~0ull;
 __device__ void finalize_one(const FinArgs& a, uint64_t c, uint64_t root_t);
 __device__ bool finalize_core(const FinArgs& a, uint64_t c, uint64_t gi, int64_t pgi, uint64_t root_t, uint64_t* kh_out);
