@@ -146,6 +146,21 @@ def test_root_entry_metadata_lines(ctx, flags):
         check_against_oracle(O.synth_store(len(lens), lens=lens), ctx, flags, f"root{first}")
 
 
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_whole_tile_counts_around_the_inline_limit(ctx, flags):
+    # a finalize lane combines up to LONG_TILES (16) whole tiles itself, a
+    # longer entry takes the slow list (a wave each): entries of 1..22 whole
+    # tiles between their start and metadata tiles, at shifting alignments
+    # (the small entries between them move every start within its tile)
+    rnd = random.Random(17)
+    lens = []
+    for w in range(1, 23):
+        for d in (-70, -1, 0, 1, 63, 2100):
+            lens += [w * 4096 + d, rnd.choice([20, 77, 1000, 4095, 2048 + 7])]
+    lens = np.array(lens, np.uint64)
+    check_against_oracle(O.synth_store(len(lens), lens=lens), ctx, flags, "tiles")
+
+
 def test_tombstones_and_overwrites_random(ctx):
     rnd = random.Random(11)
     buf = bytearray()
