@@ -285,6 +285,7 @@ int upload_tables() {
           t.last_c[q][tb][b] = mulp(host_xpow8(g_host_tabs, 4 + 1024 * (3 - q)), (uint32_t)b << (8 * tb));
         }
         t.m4096[tb][b] = mulp(host_xpow8(g_host_tabs, 512), (uint32_t)b << (8 * tb));
+        t.m32k[tb][b] = mulp(g_host_tabs.x32768, (uint32_t)b << (8 * tb));
       }
     for (int pos = 0; pos < 8; pos++)
       for (int nb = 0; nb < 16; nb++)

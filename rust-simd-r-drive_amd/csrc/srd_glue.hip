@@ -515,6 +515,7 @@ struct FinIn {
 struct FinLds {
   uint32_t tab[1024];         // CRC slice-by-4
   uint32_t m16k[1024];        // v -> v * x^16384
+  uint32_t m32k[1024];        // v -> v * x^32768 (a tile step)
   uint32_t winit[64], zero_crc[64];
   uint32_t invpow[4097];
 };
@@ -592,9 +593,9 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
       if (k0 == k1) {
         y = acc ^ sxm;
       } else {
-        // one tile step: v * x^32768 = (v * x^16384) * x^16384, two table
-        // multiplies; the whole tiles' values loaded 4 at a time (their loads
-        // do not wait for the chain)
+        // one tile step: v * x^32768, one table multiply (m32k); the whole
+        // tiles' values loaded 4 at a time (their loads do not wait for the
+        // chain)
         const u32x4* t4 = (const u32x4*)a.tile;
         for (uint64_t kb = k0 + 1; kb < k1; kb += 4) {
           u32x4 tv[4];
@@ -603,9 +604,9 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
 #pragma unroll
           for (int q = 0; q < 4; q++)
             if (kb + q < k1)  // tile_T(k) = mul16k(T_lo) ^ SX_32
-              acc = mul16k_lds(m16k, mul16k_lds(m16k, acc)) ^ mul16k_lds(m16k, tv[q][0]) ^ tv[q][2];
+              acc = mul16k_lds(t.m32k, acc) ^ mul16k_lds(m16k, tv[q][0]) ^ tv[q][2];
         }
-        y = mul16k_lds(m16k, mul16k_lds(m16k, acc)) ^ (mul16k_lds(m16k, e.t1[0]) ^ e.t1[2]) ^ sxm;
+        y = mul16k_lds(t.m32k, acc) ^ (mul16k_lds(m16k, e.t1[0]) ^ e.t1[2]) ^ sxm;
       }
       crc = ~(mulp(t.invpow[(k1 + 1) * TILE - mo], y) ^ tail);
     }
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   static_assert(CHAIN_THREADS == 1024, "one word of each 1024-word table per thread");
   const uint32_t ti = threadIdx.x;
   const uint32_t r_tab = g_tabs.tab[ti >> 8][ti & 255],
-                 r_m16k = (&g_tabs.m16k[0][0])[ti];
+                 r_m16k = (&g_tabs.m16k[0][0])[ti], r_m32k = (&g_tabs.m32k[0][0])[ti];
   uint32_t r_inv[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) r_inv[j] = g_tabs.invpow[ti + 1024 * j];
@@ -675,6 +676,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
   tab[ti] = r_tab;
   lt.m16k[ti] = r_m16k;
+  lt.m32k[ti] = r_m32k;
 #pragma unroll
   for (int j = 0; j < 4; j++) lt.invpow[ti + 1024 * j] = r_inv[j];
   if (ti == 0) lt.invpow[4096] = r_inv_last;
