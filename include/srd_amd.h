@@ -60,6 +60,19 @@ extern "C" {
 #define SRD_MODE_FULL 1            /* full pass (torn tail / corrupt store / unusual structure) */
 #define SRD_MODE_SPAN_UNPROVEN 3   /* span mode: the shard's chain was not proven; use the whole-file path */
 
+/* srd_device_result.full_reason: why the optimistic pass left the call to
+ * the full pass (mode SRD_MODE_FULL) or left a span unproven
+ * (SRD_MODE_SPAN_UNPROVEN); SRD_FULL_NONE when it decided.  The full pass
+ * costs ~1.8x the optimistic one, so a store that always lands here (e.g. one
+ * above ~1 TiB: SRD_FULL_SLOT_SPACE) is visible instead of silently slower. */
+#define SRD_FULL_NONE 0
+#define SRD_FULL_FORCED 1     /* SRD_FLAG_FORCE_FULL */
+#define SRD_FULL_SLOT_SPACE 2 /* scan waves x candidate slots per wave >= the glue's 31-bit slot space */
+#define SRD_FULL_WAVES 3      /* more scan waves per chain block than the shape check's bound */
+#define SRD_FULL_NO_START 4   /* no strong node or root at the start tail (find_top): torn / corrupt end */
+#define SRD_FULL_UNPROVEN 5   /* the recorded nodes do not prove one chain (shape / root count) */
+#define SRD_FULL_CAP 6        /* the candidate slots per span could not grow further */
+
 /* option flags */
 #define SRD_FLAG_FORCE_FULL 1u   /* skip the optimistic (strong-candidate) pass */
 #define SRD_FLAG_NO_CRC 2u       /* structural recovery + index only */
@@ -114,7 +127,7 @@ typedef struct {
   uint64_t n_index;        /* KeyIndexer entries */
   uint64_t n_crc_bad;      /* chain entries whose CRC does not match */
   uint64_t n_candidates;   /* chain-node candidates recorded by the scan */
-  uint64_t n_weak;         /* reserved (0) */
+  uint64_t full_reason;    /* SRD_FULL_*: why the optimistic pass did not decide (0 when it did) */
   uint32_t mode;           /* 0 = optimistic pass sufficed, 1 = full pass */
   uint32_t reserved;       /* host results: 1 = arrays owned by the context */
   /* chain, file order; device pointers */

@@ -65,6 +65,8 @@ def lib():
         L.orc_xxh3_64.argtypes = [C.c_void_p, C.c_size_t]
         L.orc_crc32.restype = C.c_uint32
         L.orc_crc32.argtypes = [C.c_void_p, C.c_size_t]
+        L.orc_crc32_ranges.restype = None
+        L.orc_crc32_ranges.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int]
         L.orc_crc32_table.restype = C.c_uint32
         L.orc_crc32_table.argtypes = [C.c_void_p, C.c_size_t]
         L.orc_recover_valid_chain.restype = C.c_uint64
@@ -96,6 +98,20 @@ def xxh3_64(data: bytes) -> int:
 def crc32(data) -> int:
     buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     return lib().orc_crc32(buf.ctypes.data_as(C.c_void_p), buf.size)
+
+
+def crc32_ranges(buf: np.ndarray, starts, lens, threads: int = 16) -> np.ndarray:
+    """compute_checksum of buf[starts[i] : starts[i] + lens[i]] for every i
+    (PCLMUL crc32, threaded): uint32 array."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    starts = np.ascontiguousarray(starts, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint64)
+    assert starts.size == lens.size and (starts.size == 0 or int((starts + lens).max()) <= buf.size)
+    out = np.zeros(starts.size, np.uint32)
+    if starts.size:
+        lib().orc_crc32_ranges(buf.ctypes.data_as(C.c_void_p), starts.ctypes.data_as(C.c_void_p),
+                               lens.ctypes.data_as(C.c_void_p), starts.size, out.ctypes.data_as(C.c_void_p), threads)
+    return out
 
 
 def as_u8(file) -> np.ndarray:

@@ -298,6 +298,34 @@ uint32_t orc_crc32_update(uint32_t crc, const void *data, size_t len) {
   return ~crc_slice8(s, (const uint8_t *)data, len);
 }
 uint32_t orc_crc32(const void *data, size_t len) { return orc_crc32_update(0, data, len); }
+
+/* compute_checksum (compute_checksum.rs:15-20) of n byte ranges of buf,
+ * buf[starts[i], starts[i] + lens[i]), on `threads` threads (contiguous
+ * blocks of ranges): the independent checker of the GPU's crc_computed at
+ * full C3 size (tests/test_gpu_scale.py) */
+typedef struct {
+  const uint8_t *buf;
+  const uint64_t *starts, *lens;
+  uint32_t *out;
+  uint64_t lo, hi;
+} crc_range_job;
+static void *crc_range_worker(void *p) {
+  crc_range_job *j = (crc_range_job *)p;
+  for (uint64_t i = j->lo; i < j->hi; i++) j->out[i] = orc_crc32(j->buf + j->starts[i], (size_t)j->lens[i]);
+  return NULL;
+}
+void orc_crc32_ranges(const uint8_t *buf, const uint64_t *starts, const uint64_t *lens, uint64_t n,
+                      uint32_t *out, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64];
+  crc_range_job jobs[64];
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (crc_range_job){buf, starts, lens, out, n * (uint64_t)t / threads, n * (uint64_t)(t + 1) / threads};
+    pthread_create(&th[t], NULL, crc_range_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
 uint32_t orc_crc32_table(const void *data, size_t len) {
   pthread_once(&crc_once, crc_init);
   return ~crc_slice8(~0u, (const uint8_t *)data, len);

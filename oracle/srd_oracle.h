@@ -35,6 +35,10 @@ void orc_xxh3_64_batch(const uint8_t *buf, const uint64_t *offs,
 uint32_t orc_crc32(const void *data, size_t len);       /* crc32fast-equivalent */
 uint32_t orc_crc32_update(uint32_t crc, const void *data, size_t len);
 uint32_t orc_crc32_table(const void *data, size_t len); /* portable slice-by-8 */
+/* orc_crc32 of buf[starts[i], starts[i] + lens[i]) for i < n, threaded */
+void orc_crc32_ranges(const uint8_t *buf, const uint64_t *starts,
+                      const uint64_t *lens, uint64_t n, uint32_t *out,
+                      int threads);
 int orc_has_pclmul(void);
 
 /* ---- format (simd-r-drive-entry-handle/src/) ---- */

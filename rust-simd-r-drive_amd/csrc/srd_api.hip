@@ -143,6 +143,10 @@ struct Ctx {
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
   uint32_t scan_wq[16] = {};  // ScanPart::wq (scan_weights())
   uint32_t scan_variant = 0;  // ScanArgs::variant (srd_debug_set_scan_variant)
+  // the optimistic pass's slot-space bound (the glue's parent words are 31-bit):
+  // 2^31; SRD_SLOT_LIMIT_LOG2 (10..31, read at srd_ctx_create) lowers it so the
+  // SRD_FULL_SLOT_SPACE fallback can be tested on a small store
+  uint64_t slot_limit = 1ull << 31;
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -211,7 +215,7 @@ enum BufId {
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
-  B_WTOT, B_WROOT, B_WBASE, B_KTOT, B_DONE, B_SPAN_FIRST,
+  B_WTOT, B_WROOT, B_KTOT, B_DONE, B_SPAN_FIRST,
   B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN,
   B_COUNT_
 };
@@ -334,7 +338,7 @@ constexpr uint32_t kDbgScanOnly = 1u << 30;  // SRD_DEBUG_API timing builds: the
 template <bool FULL>
 static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr) {
-  const dim3 grid(g), block(SCAN_WAVES_V2 * 64);
+  const dim3 grid(g), block(scan_nw((int)a.variant) * 64);
 #ifdef SRD_SCAN_MARKER_EVENTS  // timing A/B builds: marker events around a plain launch
   constexpr bool marker = true;
 #else
@@ -383,6 +387,21 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
   } else if (a.variant == 10) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 10>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 10>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 20) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 20>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 20>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 21) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 21>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 21>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 23) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 23>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 23>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 24) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 24>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 24>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 22) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 22>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 22>, grid, block, 0, s, e0, e1, 0, a);
 #endif
   } else if (e0) {
     if (a.flen > kWide)
@@ -603,6 +622,10 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->scan_blocks = (unsigned)ncu;
   scan_weights(c->scan_wq);
+  if (const char* e = getenv("SRD_SLOT_LIMIT_LOG2")) {
+    const long v = strtol(e, nullptr, 10);
+    if (v >= 10 && v <= 31) c->slot_limit = 1ull << v;
+  }
   *out = c;
   return 0;
 }
@@ -654,34 +677,44 @@ static void grow_cap(CandCap& k, uint64_t bytes) {
   k.grown_bytes = bytes;
 }
 
-static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g) {
+// the scan grid of `variant` over ns resident spans: blocks (<= blocks per
+// CU x CUs) and waves per block (scan_nw / scan_bpc)
+static unsigned scan_grid(const Ctx* c, uint32_t variant, uint64_t ns, uint32_t* nw) {
+  *nw = (uint32_t)scan_nw((int)variant);
+  return (unsigned)std::min<uint64_t>((ns + *nw - 1) / *nw, (uint64_t)c->scan_blocks * scan_bpc((int)variant));
+}
+static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g, uint32_t nw) {
   ScanPart p{};
   p.s_lo = s_lo;
   p.ns = ns;
   p.g = g;
-  for (int q = 0; q < 16; q++) p.wq[q] = c->scan_wq[q];
+  p.nw = nw;
+  if (nw == 16) {
+    for (int q = 0; q < 16; q++) p.wq[q] = c->scan_wq[q];
+  } else {  // (the fitted shares are the 16-wave block's) an even split
+    for (uint32_t q = 0; q < nw; q++) p.wq[q] = 65536u / nw;
+    p.wq[nw - 1] += 65536u - nw * (65536u / nw);
+  }
   part_fill_cw(p);
   return p;
 }
 // an upper bound on the spans of one wave
 static uint64_t part_max_wave_spans(const ScanPart& p) {
   if (!p.g) return 1;
-  const uint32_t wmax = *std::max_element(p.wq, p.wq + 16);
+  const uint32_t wmax = *std::max_element(p.wq, p.wq + p.nw);
   const uint64_t nb = (p.ns + p.g - 1) / p.g;
   return (nb * wmax + 65535) / 65536 + 1;
 }
 
 // the scan kernel's per-wave results and last-block reduction (ScanArgs)
 static int scan_wave_args(Ctx* c, ScanArgs* a) {
-  const uint64_t W = (uint64_t)c->scan_blocks * SCAN_WAVES_V2;
+  const uint64_t W = (uint64_t)c->scan_blocks * 32;  // up to 32 waves per CU (scan_grid)
   TRY(ensure(c, B_WTOT, W * 8));
   TRY(ensure(c, B_WROOT, W * 8));
-  TRY(ensure(c, B_WBASE, W * 8));
   TRY(ensure(c, B_KTOT, 64));
   TRY(ensure_z(c, B_DONE, 64));  // zero once; the scan's last block resets it
   a->wave_total = P<uint64_t>(c, B_WTOT);
   a->wave_root = P<uint64_t>(c, B_WROOT);
-  a->wave_base = P<uint64_t>(c, B_WBASE);
   a->k_total = P<uint64_t>(c, B_KTOT);
   a->done = P<uint32_t>(c, B_DONE);
   return 0;
@@ -929,8 +962,9 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.wcap = 0;  // the full pass stores records at span * cap + slot
     TRY(scan_wave_args(c, &a));
     if (n_spans) {
-      unsigned g = (unsigned)std::min<uint64_t>((n_spans + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
-      a.part = scan_part(c, 0, n_spans, g);
+      uint32_t nw;
+      const unsigned g = scan_grid(c, a.variant, n_spans, &nw);
+      a.part = scan_part(c, 0, n_spans, g, nw);
       hipEvent_t e0, e1;
       TRY(next_scan_events(c, &e0, &e1));
       if (full)
@@ -1097,7 +1131,6 @@ static int alloc_fast(Ctx* c, uint64_t capK, uint32_t log2_nbk) {
   TRY(ensure_z(c, B_HASCHILD2, capK * 4));
   TRY(ensure_z(c, B_CHILDOF, capK * 8));
   TRY(ensure(c, B_FLAG, capK));
-  TRY(ensure(c, B_CHAIN_G, (capK + 1) * 8));
   TRY(ensure(c, B_PART, GLUE_BLOCKS * 4));
   TRY(ensure(c, B_PARTEX, CHAIN_BLOCKS * CHAIN_WAVES * 4));
   TRY(ensure(c, B_PLAN, sizeof(Plan)));
@@ -1125,17 +1158,18 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const uint32_t log2_nbk = index_log2_buckets(n_est);
     // the scan's partition (ScanPart): total_waves waves of at most spw
     // spans; each wave's records are dense in its region of wcap = spw * cap slots
-    const unsigned g = (unsigned)std::min<uint64_t>((ns_rel + SCAN_WAVES_V2 - 1) / SCAN_WAVES_V2, c->scan_blocks);
-    const ScanPart part = scan_part(c, s_lo, ns_rel, g);
-    const uint64_t total_waves = (uint64_t)g * SCAN_WAVES_V2;
+    uint32_t nw;
+    const unsigned g = scan_grid(c, c->scan_variant, ns_rel, &nw);
+    const ScanPart part = scan_part(c, s_lo, ns_rel, g, nw);
+    const uint64_t total_waves = (uint64_t)g * nw;
     const uint64_t spw = part_max_wave_spans(part);
     const uint64_t wcap = spw * c->copt.cap;
     // the glue works in slot space (slot = wave * wcap + record): its parent
     // words are 31-bit; stores above ~1 TiB (or a denser cap) take the full pass
     const uint64_t capK = total_waves * wcap;
-    if (capK >= (1ull << 31)) return 0;
+    if (capK >= c->slot_limit) { out->full_reason = SRD_FULL_SLOT_SPACE; return 0; }
     const uint32_t wpb = (uint32_t)((total_waves + CHAIN_BLOCKS - 1) / CHAIN_BLOCKS);  // scan waves per chain block
-    if (wpb > BW_MAX) return 0;
+    if (wpb > BW_MAX) { out->full_reason = SRD_FULL_WAVES; return 0; }
     TRY(alloc_scan(c, nt_rel, std::max<uint64_t>(ns_rel, total_waves * spw), c->copt.cap));
     TRY(ensure(c, B_SPAN_FIRST, (ns_rel + 1) * 4));
     TRY(alloc_fast(c, capK, log2_nbk));
@@ -1330,13 +1364,18 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       if (!(hp.status & retry_bits) || (hp.status & ~retry_bits) || rounds >= 6) break;
     }
     out->n_candidates = hp.K;
-    out->n_weak = 0;
     if (hp.status & ST_OVERFLOW) {
-      if (c->copt.cap >= SPAN_BYTES) return 0;  // cannot happen (<= one candidate per byte); not provable here
+      // (cannot happen: <= one candidate per byte) not provable here
+      if (c->copt.cap >= SPAN_BYTES) { out->full_reason = SRD_FULL_CAP; return 0; }
       grow_cap(c->copt, flen - span_off);
+      out->full_reason = SRD_FULL_CAP;  // (if the attempts run out)
       continue;
     }
-    if (hp.status) return 0;  // not provable here -> full pass (whole file) / unproven (span)
+    if (hp.status) {  // not provable here -> full pass (whole file) / unproven (span)
+      out->full_reason = (hp.status & ST_NOSTART) ? SRD_FULL_NO_START : SRD_FULL_UNPROVEN;
+      return 0;
+    }
+    out->full_reason = SRD_FULL_NONE;
     out->final_len = flen - hp.top_gap;  // find_top's start tail (a torn tail within TOP_WINDOW bytes: below flen)
     out->n_chain = hp.n_chain;
     out->n_crc_bad = hp.n_bad;
@@ -1569,6 +1608,7 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
     return finish(c, d_file, flen, 0, flags, out);
   }
   bool full = flags & SRD_FLAG_FORCE_FULL;
+  if (full) out->full_reason = SRD_FULL_FORCED;
   uint64_t K = 0, h[8];
   // ---- optimistic pass: strong candidates only; valid iff the chain from
   //      file_len is proven through recorded nodes ----
@@ -1581,8 +1621,8 @@ static int validate_device_impl(srd_ctx* c, const uint8_t* d_file, uint64_t flen
   out->mode = 1;
   TRY(run_scan(c, d_file, flen, true, &K, h));
   out->n_candidates = K;
-  if (debug_env()) fprintf(stderr, "full pass: K=%lu candidates\n", (unsigned long)K);
-  out->n_weak = 0;
+  if (debug_env()) fprintf(stderr, "full pass: K=%lu candidates (reason %lu)\n", (unsigned long)K,
+                           (unsigned long)out->full_reason);
   const uint64_t max_root = h[0];
   uint64_t best_g1 = 0, tlin = 0;
   if (K) {

@@ -717,12 +717,22 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     uint64_t run = a.coff + before + woff;  // this wave's next chain position
     const uint64_t run0 = run;
     uint32_t nsq = 0;  // wave-uniform: entries in the wave's slow queue
+    // (the queue passes values between lanes through LDS: wavefront fences
+    // and a wave barrier order the writers' stores before the reads here and
+    // the reads before the slots' reuse, as scan_kernel's window does)
+    auto wave_sync = [&]() {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     auto flush_slow = [&]() {
       if (!nsq) return;
+      wave_sync();
       unsigned long long sbase = 0;
       if (lane == 0) sbase = atomicAdd(f.n_slow, (unsigned long long)nsq);
       sbase = __shfl(sbase, 0);
       for (uint32_t q = lane; q < nsq; q += 64) f.slow_list[sbase + q] = run0 + wslow[wi][q];
+      wave_sync();
     };
     const uint32_t chunk = (n + CHAIN_WAVES - 1) / CHAIN_WAVES;
     const uint32_t c0 = min(n, wi * chunk), c1 = min(n, c0 + chunk);

@@ -93,12 +93,13 @@ struct ScanPart {
   uint64_t s_lo;   // first resident span
   uint64_t ns;     // resident spans
   uint32_t g;      // scan blocks
-  uint32_t wq[16];  // share of wave slot v of each block; wq[0] + .. + wq[15] == 65536
+  uint32_t nw;     // waves per scan block (<= 16; the launch's variant sets it, scan_geom)
+  uint32_t wq[16];  // share of wave slot v of each block; wq[0] + .. + wq[nw-1] == 65536
   uint32_t cw[17];  // cumulative: cw[v] = wq[0] + .. + wq[v-1] (part_fill_cw)
 };
 __host__ __device__ __forceinline__ void part_fill_cw(ScanPart& p) {
   p.cw[0] = 0;
-  for (int v = 0; v < 16; v++) p.cw[v + 1] = p.cw[v] + p.wq[v];
+  for (uint32_t v = 0; v < 16; v++) p.cw[v + 1] = p.cw[v] + (v < p.nw ? p.wq[v] : 0u);
 }
 // cumulative share of the waves below v (v <= 16)
 __host__ __device__ __forceinline__ uint64_t part_cw(const ScanPart& p, uint32_t v) { return p.cw[v]; }
@@ -112,15 +113,15 @@ __host__ __device__ __forceinline__ void part_wave_range(const ScanPart& p, uint
   *r0 = bs + ((nb * part_cw(p, v)) >> 16);
   *r1 = bs + ((nb * part_cw(p, v + 1)) >> 16);
 }
-// the scan wave (b * 16 + v) holding resident-relative span rel < ns
+// the scan wave (b * nw + v) holding resident-relative span rel < ns
 __device__ __forceinline__ uint64_t part_span_wave(const ScanPart& p, uint64_t rel) {
   uint64_t b = rel * p.g / p.ns;
   while (b + 1 < p.g && part_block_start(p, b + 1) <= rel) b++;
   const uint64_t bs = part_block_start(p, b), nb = part_block_start(p, b + 1) - bs, o = rel - bs;
   uint32_t v = 0;
 #pragma unroll
-  for (uint32_t j = 1; j < 16; j++) v += o >= ((nb * part_cw(p, j)) >> 16) ? 1u : 0u;
-  return b * 16 + v;
+  for (uint32_t j = 1; j < 16; j++) v += j < p.nw && o >= ((nb * part_cw(p, j)) >> 16) ? 1u : 0u;
+  return b * p.nw + v;
 }
 
 struct ScanArgs {
@@ -148,12 +149,12 @@ struct ScanArgs {
   // per-wave results, reduced by the last block to finish (no atomics on the
   // counters, no memset, no span-base scan launch): wave w's record count
   // (bit 63: a span overflowed its slots), its largest root tail; the last
-  // block writes wave_base[w] = exclusive prefix of the counts, *k_total,
-  // counters[0] (max root tail), [1] = 0, [2] (overflow); `done` counts the
-  // finished blocks (the last block resets it to 0)
+  // block writes k_total[0] = the record total, k_total[1] = 1 + the last
+  // record's slot, counters[0] (max root tail), [1] (find_top's tail), [2]
+  // (overflow); `done` counts the finished blocks (the last block resets it
+  // to 0).  The glue works in slot space (w * wcap + r): no wave bases.
   uint64_t* wave_total;
   uint64_t* wave_root;
-  uint64_t* wave_base;
   uint64_t* k_total;
   uint32_t* done;
   // optimistic pass: the records of scan wave w are DENSE in file order at
@@ -497,6 +498,110 @@ __device__ __forceinline__ void crc_lane_bases(uint32_t (&R)[4], int lane) {
   for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
 }
 
+// ---- the rotated layout (the occupancy variants of scan_kernel) ----
+// ScanLds replicates each slice-by-4 table 32 times (lane l reads copy l % 32:
+// conflict-free, 128 KiB), so one 16-wave block fills the CU's LDS.  The four
+// lookups of one slice-by-4 step only have to go to 32 distinct banks per
+// 32-lane group, not to the same table: in lookup slot j lane l takes byte
+// k = (j + l) & 3 of the state and table T_(3-k), so the 32 lanes of a group
+// read 4 different tables, 8 lanes each, and 8 replicas per table suffice.
+// Row b (256 B) of `tn`: words 0-31 = T_t[b] replica r at word 8 t + r (bank
+// 8 t + r; r = (l >> 2) & 7); words 32-63 of rows 0-127 = the lane-weight
+// nibble table (row pos * 16 + nb, word 32 + l % 32: bank l % 32).  64 KiB
+// for both (ScanLds: 144 KiB), so two blocks fit a CU.
+template <int NW>
+struct alignas(4096) ScanLdsR {
+  uint32_t last[3 * 4 * 256];  // 12 KiB, unreplicated (as ScanLds::last), at offset 0
+  uint32_t tn[256 * 64];       // 64 KiB, 4 KiB-aligned (lane_weight_rot ORs nibble bits 8-11 into the base)
+  uint32_t win[NW][24];
+  uint64_t s_root[NW], s_ovf[NW];
+  uint32_t s_last;
+};
+// lane constants of the rotated lookups: Rr byte k = the row offset of
+// table T_(3-k), replica (l >> 2) & 7; SL[j] = v_perm selector of slot j
+// (address byte 0 = Rr byte k, byte 1 = state byte k, bytes 2-3 zero)
+__device__ __forceinline__ void rot_lane_consts(uint32_t& Rr, uint32_t (&SL)[4], int lane) {
+  const uint32_t r4 = 4u * (((uint32_t)lane >> 2) & 7u);
+  Rr = (96u + r4) | ((64u + r4) << 8) | ((32u + r4) << 16) | (r4 << 24);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t k = ((uint32_t)j + (uint32_t)lane) & 3u;
+    SL[j] = 0x0c0c0000u | ((4u + k) << 8) | k;
+  }
+}
+__device__ __forceinline__ uint32_t rot_lookup(const uint32_t* tn, uint32_t s, uint32_t Rr, uint32_t sel) {
+  return *(const uint32_t*)((const char*)tn + __builtin_amdgcn_perm(s, Rr, sel));
+}
+// crc_line4 over the rotated tables: the same four 16-byte chains, the same
+// shifted last steps (chains 0-2 through `last`), the same raw line CRC
+template <class L>
+__device__ __forceinline__ uint32_t crc_line4_rot(const uint32_t (&d)[16], const L& lds, uint32_t Rr,
+                                                  const uint32_t (&SL)[4]) {
+  uint32_t s[4] = {d[0], d[4], d[8], d[12]};
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t t0 = rot_lookup(lds.tn, s[q], Rr, SL[0]), t1 = rot_lookup(lds.tn, s[q], Rr, SL[1]);
+      const uint32_t t2 = rot_lookup(lds.tn, s[q], Rr, SL[2]), t3 = rot_lookup(lds.tn, s[q], Rr, SL[3]);
+      s[q] = xor3(xor3(t0, t1, d[4 * q + j + 1]), t2, t3);
+    }
+  }
+  uint32_t v[4];
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    const uint32_t* m = lds.last + 1024 * q;
+    v[q] = xor3(m[s[q] & 0xff], m[256 + ((s[q] >> 8) & 0xff)], m[512 + ((s[q] >> 16) & 0xff)]) ^ m[768 + (s[q] >> 24)];
+  }
+  v[3] = xor3(rot_lookup(lds.tn, s[3], Rr, SL[0]), rot_lookup(lds.tn, s[3], Rr, SL[1]),
+              rot_lookup(lds.tn, s[3], Rr, SL[2])) ^
+         rot_lookup(lds.tn, s[3], Rr, SL[3]);
+  return xor3(v[0], v[1], v[2]) ^ v[3];
+}
+// lane_weight_or over the rotated layout's nibble rows: nibble pos of c at
+// address bits 8-11, pos in the ds_read offset (lbase = tn + 128 + 4 (l % 32))
+__device__ __forceinline__ uint32_t lane_weight_rot(uint32_t c, uint32_t lbase) {
+  uint32_t v[8];
+#pragma unroll
+  for (int pos = 0; pos < 8; pos++) {
+    const int sh = 4 * pos - 8;
+    const uint32_t x = sh < 0 ? c << (-sh) : c >> sh;
+    v[pos] = lds_ld(((x & 0xF00u) | lbase) + pos * 4096);
+  }
+  return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6] ^ v[7]);
+}
+// the rotated layout's tables into LDS (all NW * 64 threads; ends with a
+// block barrier): every thread's global loads first, then its LDS stores
+template <int NW>
+__device__ __forceinline__ void load_rot_lds(ScanLdsR<NW>& lds) {
+  constexpr uint32_t T = NW * 64, NT = (1024 + T - 1) / T, NL = (768 + T - 1) / T;
+  const uint32_t u = threadIdx.x;
+  uint32_t tv[NT];
+  u32x4 nv[NT], lv[NL];
+#pragma unroll
+  for (uint32_t i = 0; i < NT; i++) {
+    const uint32_t x = min(u + i * T, 1023u);
+    tv[i] = g_tabs.tab[x >> 8][x & 255];
+    nv[i] = ((const u32x4*)g_tabs.nib)[x];  // 16 B of row x >> 3 (32 words per row)
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < NL; i++) lv[i] = ((const u32x4*)&g_tabs.last[0][0][0])[min(u + i * T, 767u)];
+#pragma unroll
+  for (uint32_t i = 0; i < NT; i++) {
+    const uint32_t x = u + i * T;
+    if (x < 1024) {
+      u32x4* tr = (u32x4*)(lds.tn + (x & 255) * 64 + 8 * (x >> 8));  // T_t[b], replicas 0-7
+      tr[0] = u32x4{tv[i], tv[i], tv[i], tv[i]};
+      tr[1] = u32x4{tv[i], tv[i], tv[i], tv[i]};
+      *(u32x4*)(lds.tn + (x >> 3) * 64 + 32 + 4 * (x & 7)) = nv[i];
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < NL; i++)
+    if (u + i * T < 768) ((u32x4*)lds.last)[u + i * T] = lv[i];
+  __syncthreads();
+}
+
 // recover_valid_chain's outer loop (data_store.rs:388-479) walks the cursor t
 // down from file_len and skips every t whose metadata fails its first test,
 // entry_start < metadata_offset (:390-420; entry_start = prev + prepad(prev),
@@ -628,12 +733,28 @@ __global__ __launch_bounds__(256) void link2_kernel(ScanArgs a) {
   for (uint64_t r = threadIdx.x; r < nrec; r += blockDim.x) link_record(a, w, r);
 }
 
+// The scan's geometry per variant (host and device): waves per block and
+// blocks per CU.  20 / 21: the rotated tables (ScanLdsR, 78 KiB) and a
+// 2-deep register ring, two blocks of 10 / 12 waves per CU = 5 / 6 waves per
+// SIMD (VGPR budget 96 / 80, amdgpu_waves_per_eu); 22: the rotated tables at
+// today's geometry (one 16-wave block per CU, 3-deep ring).
+// 23: the rotated tables, 2-deep ring, two 8-wave blocks per CU (4 waves
+// per SIMD, as 0: the geometry at equal occupancy); 24: the rotated tables
+// and the 2-deep ring in today's geometry.
+constexpr int scan_nw(int V) { return V == 20 ? 10 : V == 21 ? 12 : V == 23 ? 8 : 16; }
+constexpr int scan_bpc(int V) { return V == 20 || V == 21 || V == 23 ? 2 : 1; }
+constexpr int scan_wpe(int V) { return (scan_nw(V) * scan_bpc(V)) / 4; }
+constexpr bool scan_rot(int V) { return V >= 20 && V <= 24; }
+
 template <bool FULL, bool WIDE, int V = 0>
-__global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a) {
+__global__ __launch_bounds__(scan_nw(V) * 64) __attribute__((amdgpu_waves_per_eu(scan_wpe(V), scan_wpe(V))))
+void scan_kernel(ScanArgs a) {
+  constexpr int NW = scan_nw(V);
+  constexpr bool ROT = scan_rot(V);
   constexpr bool F1 = (V == 1 || V == 2) ? !kFlag1 : kFlag1;
   constexpr bool F1_AFTER = V == 2;  // F1's staging + test after the CRC, at priority 2
   constexpr bool CRC2 = V == 3;
-  constexpr bool RING2 = V == 4 || V == 5;  // a 2-deep register ring (one tile in flight), 16 VGPRs fewer
+  constexpr bool RING2 = V == 4 || V == 5 || V == 20 || V == 21 || V == 23 || V == 24;  // a 2-deep register ring (one tile in flight), 16 VGPRs fewer
   constexpr bool WIDE16 = V == 5 || V == 6;  // crc_line4_wide: each level's 16 lookups issued together
   // timing-only ablations (wrong results; SRD_DEBUG_API's scan-only calls):
   // 7 = the ring's loads alone (each tile XOR-folded), 8 = the whole tile
@@ -654,7 +775,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // tile instead of after every ring round)
   constexpr bool TILE_SP = V == 14 || RING2;
   uint32_t memonly_acc = 0;
-  __shared__ ScanLds lds;
+  using Lds = std::conditional_t<ROT, ScanLdsR<NW>, ScanLds>;
+  static_assert(ROT || NW == SCAN_WAVES_V2, "ScanLds holds 16 windows");
+  __shared__ Lds lds;
   // lanes of the record queue rq: with F1 its lane 63 is scratch
   constexpr uint64_t RQ_LANES = F1 ? 63 : 64;
   if (blockIdx.x == 0) {
@@ -665,7 +788,8 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
 #ifdef SRD_WAVE_STAMPS
   if (threadIdx.x == 0) g_wave_stamp[8192 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
-  load_crc_lds(lds);
+  if constexpr (ROT) load_rot_lds(lds);
+  else load_crc_lds(lds);
 #ifdef SRD_WAVE_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < 256) g_wave_stamp[8192 + 256 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -675,16 +799,34 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // below (k, B, span, bounds) stays in SGPRs / scalar branches
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t R[4];
+  uint32_t Rr = 0, SL[4] = {0, 0, 0, 0};
+  if constexpr (ROT) {
+    rot_lane_consts(Rr, SL, lane);
+  } else {
 #pragma unroll
-  for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
+    for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
+  }
   const uint8_t* __restrict__ file = a.file;
   const uint64_t flen = a.flen;
   uint32_t* win = lds.win[wv];
-  const uint32_t nib_lane = lds_off(lds.nib) + 4u * (lane & 31);  // 2 KiB-aligned table base + the lane's bank
+  uint32_t nib_lane;
+  if constexpr (ROT) nib_lane = lds_off(lds.tn) + 128u + 4u * (lane & 31);  // 4 KiB-aligned rows, words 32-63
+  else nib_lane = lds_off(lds.nib) + 4u * (lane & 31);  // 2 KiB-aligned table base + the lane's bank
+  // the line CRC and its lane weight (the variant's table layout)
+  auto line_crc = [&](const uint32_t (&x)[16]) -> uint32_t {
+    if constexpr (ROT) return crc_line4_rot(x, lds, Rr, SL);
+    else if constexpr (V == 3) return crc_line2(x, lds, R);
+    else if constexpr (V == 5 || V == 6 || V == 10) return crc_line4_wide(x, lds, R);
+    else return crc_line4(x, lds, R);
+  };
+  auto lane_wt = [&](uint32_t c) -> uint32_t {
+    if constexpr (ROT) return lane_weight_rot(c, nib_lane);
+    else return lane_weight_or(c, nib_lane);
+  };
 
   // contiguous tile range per wave (whole spans, ScanPart)
-  const uint64_t total_waves = (uint64_t)gridDim.x * SCAN_WAVES_V2;
-  const uint64_t w = (uint64_t)blockIdx.x * SCAN_WAVES_V2 + wv;
+  const uint64_t total_waves = (uint64_t)gridDim.x * NW;
+  const uint64_t w = (uint64_t)blockIdx.x * NW + wv;
   uint64_t r0, r1;
   part_wave_range(a.part, blockIdx.x, (uint32_t)wv, &r0, &r1);
   uint64_t k0 = (a.part.s_lo + r0) * SPAN_TILES;
@@ -736,6 +878,19 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // lane weights, suffix XOR, filter) is one basic block.
   const uint64_t nohbm_k = (a.part.s_lo + part_block_start(a.part, blockIdx.x)) * SPAN_TILES;
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
+    if constexpr (ROT) {
+      // buffer loads over the tile (base in SGPRs, one 32-bit lane offset):
+      // no 64-bit lane address pair held across the loop (the occupancy
+      // variants' VGPR budget)
+      const __amdgpu_buffer_rsrc_t t = out_rsrc(file + k * (uint64_t)TILE, TILE);
+      const uint32_t vo = 64u * (uint32_t)lane;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(t, vo, 16 * j, 0));
+        o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
+      }
+      return;
+    }
     const u32x4* q = (const u32x4*)(file + (NOHBM ? nohbm_k + (k & 1) : k) * (uint64_t)TILE + (COAL ? 16ull : 64ull) * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -776,7 +931,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const u32x4 v = q[j];
       pl[4 * j] = v[0]; pl[4 * j + 1] = v[1]; pl[4 * j + 2] = v[2]; pl[4 * j + 3] = v[3];
     }
-    const uint32_t cp = crc_line4(pl, lds, R);
+    const uint32_t cp = line_crc(pl);
     if (lane == 0) {
 #pragma unroll
       for (int j = 0; j < 4; j++) win[j] = has_prev ? pl[12 + j] : 0u;
@@ -935,9 +1090,9 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
     // a setprio here would split the scheduling region between the window
     // test above and the CRC's lookups)
     if (!F1 || F1_AFTER || tail_tile) __builtin_amdgcn_s_setprio(3);
-    const uint32_t c = CRC2 ? crc_line2(d, lds, R) : (WIDE16 || WIDE16B) ? crc_line4_wide(d, lds, R) : crc_line4(d, lds, R);
+    const uint32_t c = line_crc(d);
     __builtin_amdgcn_s_setprio(0);
-    const uint32_t hx = half_suffix_xor(lane_weight_or(c, nib_lane), lane);
+    const uint32_t hx = half_suffix_xor(lane_wt(c), lane);
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
     // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
     // tiles.  Every store of this loop is an UNCONDITIONAL buffer store whose
@@ -1231,14 +1386,33 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
       const uint64_t pend = wtotal + count - flushed;  // records pending (lanes [0, min(pend, 64)))
       const bool fl = pend >= FLUSH_AT || last;  // uniform
       const bool wr = fl && ((rvalid >> lane) & 1);
-      const uint64_t rb = w * a.wcap + flushed;  // lane 0's record
-      const uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
+      uint64_t rb = w * a.wcap + flushed;  // lane 0's record
+      uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
+      if constexpr (ROT) {
+        // uniform by construction, but the compiler's divergence analysis
+        // loses it: as VGPRs the three descriptors cost a waterfall loop
+        // around each store (and registers the occupancy variants lack)
+        rb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rb);
+        // (min<uint64_t> compiles to f64 VALU math here: a select instead)
+        const uint64_t left = a.wcap > flushed ? a.wcap - flushed : 0;
+        rn = __builtin_amdgcn_readfirstlane(left >= 64 ? 64u : (uint32_t)left);
+        const uint32_t o32 = wr ? 32u * lane : OOB_OFF;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + rb, rn * 8),
+                                              wr ? 8u * lane : OOB_OFF, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
+                                               o32, 0, 0);
+        // (the second half through a descriptor 16 B further: one lane offset for both)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]},
+                                               out_rsrc((const char*)(a.c_rec + 2 * rb) + 16, rn * 32), o32, 0, 0);
+      } else {
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + rb, rn * 8),
                                             wr ? 8u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
                                              wr ? 32u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
                                              wr ? 32u * lane + 16u : OOB_OFF, 0, 0);
+      }
       if (fl) {
         flushed = wtotal + count;
         rvalid = 0;
@@ -1361,10 +1535,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   // registers (one round trip instead of 2q dependent ones: the last block's
   // epilogue is on the critical path of every call)
   constexpr int QR = 4;
-  uint64_t* s_wsum = (uint64_t*)lds.tab;  // the CRC tables are dead now
-  uint64_t* s_smax = s_wsum + SCAN_WAVES_V2;
+  uint64_t* s_wsum;  // the CRC tables are dead now
+  if constexpr (ROT) s_wsum = (uint64_t*)lds.tn;
+  else s_wsum = (uint64_t*)lds.tab;
+  uint64_t* s_smax = s_wsum + NW;
   uint64_t* s_root = lds.s_root;
-  uint64_t* s_ovf = s_smax + SCAN_WAVES_V2;
+  uint64_t* s_ovf = s_smax + NW;
   const uint32_t T = blockDim.x, t = threadIdx.x;
   const uint64_t q = (total_waves + T - 1) / T;
   uint64_t sum = 0, rmax = 0, o = 0, smax = 0;
@@ -1400,7 +1576,7 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void scan_kernel(ScanArgs a)
   __syncthreads();
   if (t == 0) {
     uint64_t mr = 0, oo = 0, tot = 0, sm = 0;
-    for (int i = 0; i < SCAN_WAVES_V2; i++) {
+    for (int i = 0; i < NW; i++) {
       mr = max(mr, s_root[i]);
       oo |= s_ovf[i];
       tot += s_wsum[i];

@@ -157,6 +157,12 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
     x.flags = (uint32_t)(kf >> 32);
     return x;
   };
+  // entry p's metadata ends at t (p's layout: data_store.rs:863-931), so the
+  // wave of p writes the prepad that follows it (the metadata store below)
+  auto meets = [&](const srd_write_entry& p, uint64_t t) -> bool {
+    const uint64_t pmo = (p.flags & SRD_ENTRY_TOMB) ? p.tail + 1 : p.tail + prepad64(p.tail) + p.len;
+    return pmo + 20 == t;
+  };
   uint32_t acc = 0, any = 0;
   // one unit of the sequence: block b of entry i (a tombstone is one unit
   // without a block); returns whether a next unit exists in the group (its
@@ -196,8 +202,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
     // block, the single NULL byte of a tombstone (data_store.rs:864-897)
     // (an entry's prepad is written by the wave of the batch's previous entry,
     // with that entry's metadata -- one whole line instead of two partial
-    // ones from two waves; only the batch's first entry writes its own)
-    const uint32_t nz = tomb ? 1u : (b == 0 && i == 0 ? (uint32_t)pad : 0u);
+    // ones from two waves -- when that entry's metadata ends at this entry's
+    // tail; the batch's first entry, and one whose table predecessor ends
+    // elsewhere (a caller-built, gapped or reordered srd_batch_write_device
+    // table), writes its own)
+    bool own_pad = i == 0;
+    if (!tomb && b == 0 && i > 0) own_pad = !meets(ent_s(i - 1), e.tail);  // uniform
+    const uint32_t nz = tomb ? 1u : (b == 0 && own_pad ? (uint32_t)pad : 0u);
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, out_rsrc(a.out + (e.tail - a.base), nz), (uint32_t)lane, 0, 0);
     bool done = tomb;
     uint32_t crc = 0xD202EF8Du;  // CRC32(b"\0")
@@ -295,10 +306,13 @@ __global__ __launch_bounds__(SCAN_WAVES_V2 * 64, 1) void write_kernel(WriteArgs 
     // none), so the line holding both is written whole by this wave; the
     // (key_hash, metadata offset) pair
     {
+      // the next entry's prepad only when it follows this entry (meets(); a
+      // table out of order or with gaps: 20 bytes, the next entry's wave writes
+      // its own prepad)
       uint64_t next_start = mo + 20;
       if (i + 1 < a.n) {
-        const srd_write_entry en = ent_s(i + 1);  // en.tail == mo + 20
-        next_start = (en.flags & SRD_ENTRY_TOMB) ? en.tail : en.tail + prepad64(en.tail);
+        const srd_write_entry en = ent_s(i + 1);
+        if (en.tail == mo + 20) next_start = (en.flags & SRD_ENTRY_TOMB) ? en.tail : en.tail + prepad64(en.tail);
       }
       const uint32_t nb_meta = done ? (uint32_t)(next_start - mo) : 0u;  // 20 .. 83
       const uint64_t v = lane < 8 ? kh : lane < 16 ? e.tail : (uint64_t)crc;

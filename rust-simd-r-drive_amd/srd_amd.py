@@ -37,6 +37,9 @@ TIMING_NONE, TIMING_SCAN, TIMING_CALL = 0, 1, 2  # srd_ctx_set_timing levels
 SRD_MODE_OPTIMISTIC = 0
 SRD_MODE_FULL = 1
 SRD_MODE_SPAN_UNPROVEN = 3
+# srd_device_result.full_reason (include/srd_amd.h)
+SRD_FULL_NONE, SRD_FULL_FORCED, SRD_FULL_SLOT_SPACE, SRD_FULL_WAVES = 0, 1, 2, 3
+SRD_FULL_NO_START, SRD_FULL_UNPROVEN, SRD_FULL_CAP = 4, 5, 6
 SRD_FLAG_MERGE_INDEX = 16  # multi-GPU open: the whole index on ctxs[0] (default: by owner)
 SRD_MULTI_COMPOSED, SRD_MULTI_NEIGHBOUR, SRD_MULTI_WHOLE_FILE = 0, 1, 2  # srd_multi_summary.path
 SPAN_ALIGN = 16384  # span_off granularity of srd_validate_span_device
@@ -67,7 +70,7 @@ class DeviceResult(C.Structure):
     _fields_ = [
         ("file_len", C.c_uint64), ("final_len", C.c_uint64), ("n_chain", C.c_uint64),
         ("n_index", C.c_uint64), ("n_crc_bad", C.c_uint64), ("n_candidates", C.c_uint64),
-        ("n_weak", C.c_uint64), ("mode", C.c_uint32), ("reserved", C.c_uint32),
+        ("full_reason", C.c_uint64), ("mode", C.c_uint32), ("reserved", C.c_uint32),
         ("meta_off", C.c_void_p), ("key_hash", C.c_void_p), ("prev_offset", C.c_void_p),
         ("payload_start", C.c_void_p), ("payload_len", C.c_void_p),
         ("crc_stored", C.c_void_p), ("crc_computed", C.c_void_p), ("crc_ok", C.c_void_p),
@@ -274,7 +277,7 @@ class Result:
         self.n_index = r.n_index
         self.n_crc_bad = r.n_crc_bad
         self.n_candidates = r.n_candidates
-        self.n_weak = r.n_weak
+        self.full_reason = r.full_reason
         self.mode = r.mode
 
         def arr(p, n, dt):

@@ -35,7 +35,7 @@ int main(int argc, char **argv) {
   if (argc == 2 && !strcmp(argv[1], "--layout")) {
     printf("{");
     F(srd_result, file_len); F(srd_result, final_len); F(srd_result, n_chain); F(srd_result, n_index);
-    F(srd_result, n_crc_bad); F(srd_result, n_candidates); F(srd_result, n_weak); F(srd_result, mode);
+    F(srd_result, n_crc_bad); F(srd_result, n_candidates); F(srd_result, full_reason); F(srd_result, mode);
     F(srd_result, reserved); F(srd_result, meta_off); F(srd_result, key_hash); F(srd_result, prev_offset);
     F(srd_result, payload_start); F(srd_result, payload_len); F(srd_result, crc_stored);
     F(srd_result, crc_computed); F(srd_result, crc_ok); F(srd_result, index_key_hash);

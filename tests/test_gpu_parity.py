@@ -130,6 +130,33 @@ def _zipf_lens(n, seed=0x5EED0003, s=2.0):
     return L.astype(np.uint64)
 
 
+def test_full_reason_codes(ctx):
+    """srd_device_result.full_reason: why the optimistic pass did not decide
+    (the full-pass fallback, ~1.8x a call, is visible).  An intact
+    store decides (NONE); SRD_FLAG_FORCE_FULL; a cut deep inside an entry (no
+    strong node at the start tail, data_store.rs:388-420); and the slot-space
+    bound (capK >= 2^31 for a store above ~1 TiB) forced on a C1 store by a
+    context created under SRD_SLOT_LIMIT_LOG2=10 -- the outputs stay the
+    oracle's in every case."""
+    st = O.synth_store(1000)
+    r = check_against_oracle(st, ctx, 0, "intact")
+    assert (r.mode, r.full_reason) == (S.SRD_MODE_OPTIMISTIC, S.SRD_FULL_NONE)
+    r = check_against_oracle(st, ctx, S.SRD_FLAG_FORCE_FULL, "forced")
+    assert (r.mode, r.full_reason) == (S.SRD_MODE_FULL, S.SRD_FULL_FORCED)
+    r = check_against_oracle(st[: st.size - 1500], ctx, 0, "cut")
+    assert r.mode == S.SRD_MODE_FULL and r.full_reason in (S.SRD_FULL_NO_START, S.SRD_FULL_UNPROVEN)
+    os.environ["SRD_SLOT_LIMIT_LOG2"] = "10"
+    try:
+        c2 = S.Context(0)
+    finally:
+        del os.environ["SRD_SLOT_LIMIT_LOG2"]
+    try:
+        r = check_against_oracle(st, c2, 0, "slot limit")
+        assert (r.mode, r.full_reason) == (S.SRD_MODE_FULL, S.SRD_FULL_SLOT_SPACE)
+    finally:
+        c2.close()
+
+
 @pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
 def test_mixed_sizes(ctx, flags):
     lens = _zipf_lens(3000)

@@ -172,6 +172,28 @@ def test_full_c3_properties(ctx):
     for i in np.random.default_rng(5).integers(0, n, 300):
         s0 = int(mo[i] - ln[i])
         assert int(crc[i]) == zlib.crc32(t[s0:int(mo[i])].cpu().numpy().tobytes()), i
+    # every entry's crc_computed against an independent CRC (entry_handle.rs:
+    # 260-275 / compute_checksum.rs:15-20): the oracle's PCLMUL CRC on the host
+    # over the store streamed D2H in ~2 GiB groups of whole entries (crc_stored
+    # was written by the device's synth_kernel, which shares the scan's CRC
+    # machinery, so crc == st alone could hide a bug common to both)
+    ps = (mo - ln).astype(np.uint64)
+    host = torch.empty(2 << 30 | 1 << 21, dtype=torch.uint8, pin_memory=True)
+    hn = host.numpy()
+    i0 = checked = 0
+    while i0 < n:
+        g0 = int(ps[i0])
+        i1 = int(np.searchsorted(mo, np.uint64(g0 + (2 << 30)), side="right"))
+        i1 = max(i1, i0 + 1)
+        g1 = int(mo[i1 - 1])
+        host[: g1 - g0].copy_(t[g0:g1])
+        got = O.crc32_ranges(hn[: g1 - g0], ps[i0:i1] - np.uint64(g0), ln[i0:i1], threads=16)
+        bad = np.nonzero(got != crc[i0:i1])[0]
+        assert bad.size == 0, ("crc_computed differs from the host CRC", int(i0 + bad[0]), bad.size)
+        checked += i1 - i0
+        i0 = i1
+    assert checked == n
+    del host, hn
     # one flipped byte in a 1 MiB entry -> exactly that entry's CRC is bad
     big = int(np.nonzero(ln > (1 << 19))[0][len(np.nonzero(ln > (1 << 19))[0]) // 2])
     pos = int(mo[big]) - 12345
@@ -265,14 +287,13 @@ def test_overflow_after_large_call_one_context():
 
 
 @pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
-def test_cross_block_parents_deferred_links(ctx, flags):
-    """The scan's link phase (link_record) links each block's records once its
-    tiles are done; a record whose previous record or parent span lies in
-    another block's waves is deferred to the last block.  Entries of 24 and
-    40 MiB between runs of small ones put hundreds of record-less waves
-    between a node and its parent (the previous wave empty, the parent span
-    blocks away), and a key overwritten across them; every output equals the
-    oracle's in both passes."""
+def test_link_record_parents_across_empty_waves(ctx, flags):
+    """link_record's parent lookup (link2_kernel, after the scan) across empty
+    waves and distant spans: entries of 24 and 40 MiB between runs of small
+    ones put hundreds of record-less scan waves between a node and its parent
+    (the previous wave's region empty, the parent's span in a wave blocks
+    away: the span_first / part_span_wave lookup), and a key is overwritten
+    across them; every output equals the oracle's in both passes."""
     rng = np.random.default_rng(0x5EED0009)
     big = {300: 24 << 20, 700: 40 << 20, 701: 5 << 20}
     entries = []

@@ -169,3 +169,56 @@ def test_batch_write_c5_shape_equals_c2_store(ctx):
     assert nt == size
     assert torch.equal(out[:size], store[:size])
     assert int(mo[-1]) == size - 20 and int(kh[0]) == O.xxh3_64(b"bench-key-0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["gap", "reversed"])
+def test_batch_write_device_gapped_and_reordered_tables(ctx, order):
+    """srd_batch_write_device on a caller-built entry table whose entries do
+    not follow one another: two batches laid out by
+    srd_batch_layout at tails 0 and ntA + 1013, the table [A, B] (a gap
+    between A's last metadata and B's first tail) or [B, A] (tails out of
+    order).  Each entry writes exactly its own bytes -- the prepad of an entry
+    whose table predecessor does not end at its tail is written by its own
+    wave -- so the bytes between the batches keep the buffer's fill and the
+    bytes of each batch equal the oracle writer's (data_store.rs:847-939)."""
+    import ctypes as C
+    import torch
+    rng = random.Random(11 if order == "gap" else 12)
+    keys_a, pays_a = rand_batch(rng, 40)
+    keys_b, pays_b = rand_batch(rng, 40)
+    ents_a, nt_a = S.batch_layout(0, keys_a, pays_a)
+    t_b = nt_a + 1013
+    ents_b, nt_b = S.batch_layout(t_b, keys_b, pays_b)
+    pay_a, key_a = b"".join(pays_a), b"".join(keys_a)
+    for e in ents_b:  # B's sources follow A's in the shared blobs
+        e.src += len(pay_a)
+        e.key_src += len(key_a)
+    table = list(ents_a) + list(ents_b) if order == "gap" else list(ents_b) + list(ents_a)
+    n = len(table)
+    arr = (S.WriteEntry * n)(*table)
+    d_ent = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).cuda()
+    d_pay = torch.frombuffer(bytearray(pay_a + b"".join(pays_b)), dtype=torch.uint8).cuda()
+    d_key = torch.frombuffer(bytearray(key_a + b"".join(keys_b)), dtype=torch.uint8).cuda()
+    fill = 0xAB
+    d_out = torch.full((nt_b + 128,), fill, dtype=torch.uint8, device="cuda")
+    d_kh = torch.zeros(n, dtype=torch.int64, device="cuda")
+    d_mo = torch.zeros(n, dtype=torch.int64, device="cuda")
+    S._check(S.lib().srd_batch_write_device(ctx.h, C.c_void_p(d_key.data_ptr()), C.c_void_p(d_pay.data_ptr()),
+                                            C.c_void_p(d_ent.data_ptr()), n, C.c_void_p(d_out.data_ptr()), 0,
+                                            C.c_void_p(d_kh.data_ptr()), C.c_void_p(d_mo.data_ptr()), None))
+    torch.cuda.synchronize()
+    want_a_nt, want_a, kh_a = oracle_write(0, keys_a, pays_a, False)
+    want_b_nt, want_b, kh_b = oracle_write(t_b, keys_b, pays_b, False, bytes(t_b))
+    assert (want_a_nt, want_b_nt) == (nt_a, nt_b)
+    want = want_a + bytes([fill]) * (t_b - nt_a) + want_b + bytes([fill]) * 128
+    got = d_out.cpu().numpy().tobytes()
+    assert got == want
+    mos_a = ref_layout(0, pays_a, False)[1]
+    mos_b = ref_layout(t_b, pays_b, False)[1]
+    kh = [int(x) & (2**64 - 1) for x in d_kh.cpu().tolist()]
+    mo = [int(x) for x in d_mo.cpu().tolist()]
+    if order == "gap":
+        assert kh == kh_a + kh_b and mo == mos_a + mos_b
+    else:
+        assert kh == kh_b + kh_a and mo == mos_b + mos_a
