@@ -147,6 +147,10 @@ struct Ctx {
   // 2^31; SRD_SLOT_LIMIT_LOG2 (10..31, read at srd_ctx_create) lowers it so the
   // SRD_FULL_SLOT_SPACE fallback can be tested on a small store
   uint64_t slot_limit = 1ull << 31;
+  // round 0 of the optimistic pass runs the shape check inside
+  // chain_finalize_kernel<true> (look-back ranks) instead of check_kernel +
+  // chain_finalize_kernel<false>; srd_debug_set_glue_fused A/Bs the two
+  bool glue_fused = true;
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -216,7 +220,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_KTOT, B_DONE, B_SPAN_FIRST,
-  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN,
+  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN, B_LOOKB,
   B_COUNT_
 };
 
@@ -576,6 +580,11 @@ static void scan_weights(uint32_t (&wq)[16]) {
 extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
   if (!c || v < 0 || v > 30) return SRD_ERR_ARG;
   c->scan_variant = (uint32_t)v;
+  return 0;
+}
+extern "C" int srd_debug_set_glue_fused(srd_ctx* c, int fused) {
+  if (!c) return SRD_ERR_ARG;
+  c->glue_fused = fused != 0;
   return 0;
 }
 extern "C" int srd_debug_set_scan_weights(srd_ctx* c, const double* w, int n) {
@@ -1133,6 +1142,7 @@ static int alloc_fast(Ctx* c, uint64_t capK, uint32_t log2_nbk) {
   TRY(ensure(c, B_FLAG, capK));
   TRY(ensure(c, B_PART, GLUE_BLOCKS * 4));
   TRY(ensure(c, B_PARTEX, CHAIN_BLOCKS * CHAIN_WAVES * 4));
+  TRY(ensure_z(c, B_LOOKB, CHAIN_BLOCKS * 8));  // look-back granules: zero = no call's tag
   TRY(ensure(c, B_PLAN, sizeof(Plan)));
   TRY(alloc_out(c, capK + 1));
   TRY(alloc_index(c, capK, log2_nbk));
@@ -1283,9 +1293,12 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
         child2_kernel<<<GLUE_BLOCKS, GLUE_THREADS, 0, c->stream>>>(sa);  // core-only claims
         KCHK(c, "child2_kernel");
       }
-      check_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, 0, c->stream>>>(sa);
-      KCHK(c, "check_kernel");
-      HIPCHK(hipGetLastError());
+      const bool fused = rounds == 0 && c->glue_fused;
+      if (!fused) {
+        check_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, 0, c->stream>>>(sa);
+        KCHK(c, "check_kernel");
+        HIPCHK(hipGetLastError());
+      }
       // ---- plan + chain ranks + per-entry outputs / CRC + index histogram ----
       FinArgs f{};
       f.file = d_file;
@@ -1311,8 +1324,13 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.slow_list = P<uint64_t>(c, B_SLOW);       // entries that need a wave (idx_dedup runs them)
       f.n_slow = (unsigned long long*)&pl->n_slow;  // zeroed with the plan
       f.o_packed = P<uint64_t>(c, B_O_PACKED);
-      chain_finalize_kernel<<<CHAIN_BLOCKS, CHAIN_THREADS, (1u << log2_nbk) * 4, c->stream>>>(
-          sa, f, index_args(c, log2_nbk), log2_nbk);
+      unsigned long long* lb = P<unsigned long long>(c, B_LOOKB);
+      if (fused)
+        chain_finalize_kernel<true><<<CHAIN_BLOCKS, CHAIN_THREADS, (1u << log2_nbk) * 4, c->stream>>>(
+            sa, f, index_args(c, log2_nbk), log2_nbk, lb);
+      else
+        chain_finalize_kernel<false><<<CHAIN_BLOCKS, CHAIN_THREADS, (1u << log2_nbk) * 4, c->stream>>>(
+            sa, f, index_args(c, log2_nbk), log2_nbk, lb);
       KCHK(c, "chain_finalize_kernel");
       HIPCHK(hipGetLastError());
       // ---- KeyIndexer::build (bucketed; the global table in SRD_INDEX_GLOBAL timing builds) ----

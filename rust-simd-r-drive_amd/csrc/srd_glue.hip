@@ -617,8 +617,77 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
   return false;
 }
 
+// ---- the fused shape check (FUSED chain_finalize_kernel, round 0) ----
+// Each chain block checks its own records (check_kernel's test), then learns
+// the core records of the blocks before it by a decoupled look-back over one
+// 8-byte granule per block: {tag = 24 bits of the call generation (never 0),
+// state (1 = the block's own aggregate, 2 = its inclusive prefix), the shape
+// failure bit, the root-linked core nodes (saturating at 3), the core count}.
+// The data is the flag (the cdna guide's Guideline 16, form R2): relaxed
+// agent-scope atomic stores and loads, no fence, no per-call memset (a stale
+// granule carries another call's tag).  A block only waits for LOWER blocks,
+// dispatched before it, so the grid cannot deadlock; a bounded spin that runs
+// out sets ST_LOOKBACK and the host takes the full pass.
+constexpr uint32_t ST_LOOKBACK = 32;
+constexpr uint64_t LB_CNT = (1ull << 35) - 1;
+__device__ __forceinline__ uint64_t lb_pack(uint32_t tag, uint32_t st, bool fail, uint32_t nr, uint64_t cnt) {
+  return ((uint64_t)tag << 40) | ((uint64_t)st << 38) | ((uint64_t)fail << 37) | ((uint64_t)min(nr, 3u) << 35) |
+         (cnt & LB_CNT);
+}
+__device__ __forceinline__ uint32_t lb_tag(uint32_t gen) { return gen % 0xFFFFFFu + 1u; }
+// wave 0 of block b: the exclusive prefix of blocks [0, b) -- core count,
+// failure, root-linked nodes; false when the spin bound ran out
+__device__ bool lb_lookback(unsigned long long* desc, uint32_t b, uint32_t tag, uint64_t* cnt, bool* fail,
+                            uint32_t* nr) {
+  typedef __attribute__((address_space(1))) unsigned long long gu64;
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t sum = 0;
+  bool f = false;
+  uint32_t n = 0;
+  uint32_t spins = 0;
+  for (int64_t j = (int64_t)b - 1; j >= 0; j -= 64) {
+    const int64_t idx = j - (int64_t)lane;
+    uint64_t v;
+    for (;;) {  // until every lane's granule carries this call's tag (lanes past block 0: a zero prefix)
+      v = idx >= 0 ? __hip_atomic_load((gu64*)(desc + idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : lb_pack(tag, 2, false, 0, 0);
+      const bool ok = (v >> 40) == tag && ((v >> 38) & 3) != 0;
+      if (__all(ok)) break;
+      if (++spins > (1u << 22)) return false;  // uniform
+      __builtin_amdgcn_s_sleep(2);
+    }
+    const uint64_t inc = __ballot(((v >> 38) & 3) == 2);
+    const uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+    const bool take = lane <= first;
+    uint64_t c = take ? (v & LB_CNT) : 0;
+    uint32_t r = take ? (uint32_t)((v >> 35) & 3) : 0u;
+    uint32_t fl = take ? (uint32_t)((v >> 37) & 1) : 0u;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+      c += __shfl_xor(c, o);
+      r += __shfl_xor(r, o);
+      fl |= __shfl_xor(fl, o);
+    }
+    sum += c;
+    n += r;
+    f = f || fl;
+    if (inc) break;
+  }
+  *cnt = sum;
+  *fail = f;
+  *nr = n;
+  return true;
+}
+
+// FUSED (round 0 of the optimistic pass): check_kernel's shape test of the
+// block's own records first, the chain ranks from the look-back instead of
+// check_kernel's per-block totals, the plan written by the LAST block once
+// its prefix holds every block -- one launch and one pass over the slot
+// words fewer.  The retry rounds (prune marks) keep check_kernel + !FUSED.
+template <bool FUSED>
 __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs a, FinArgs f, IdxArgs ia,
-                                                                      uint32_t log2_nbk) {
+                                                                      uint32_t log2_nbk,
+                                                                      unsigned long long* lb_desc) {
   __shared__ uint32_t wsum[CHAIN_WAVES * FIN_R];
   __shared__ uint32_t s_pre[BW_MAX + 1];
   __shared__ uint32_t wslow[CHAIN_WAVES][WSLOW];
@@ -640,21 +709,24 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   const uint64_t K = a.Kp[0];
   const bool incomplete = dense_incomplete(a);
   uint64_t before = 0, total = 0;
-  block_prefix_n<CHAIN_WAVES>(a.part, incomplete ? 0u : (uint32_t)CHAIN_BLOCKS, wsum, &before, &total);
+  if constexpr (!FUSED)
+    block_prefix_n<CHAIN_WAVES>(a.part, incomplete ? 0u : (uint32_t)CHAIN_BLOCKS, wsum, &before, &total);
   Plan* pl = a.plan;
-  uint32_t st = pl->status;  // check_kernel's shape bits
+  uint32_t st = FUSED ? 0u : pl->status;  // check_kernel's shape bits (FUSED: this kernel's own, below)
   // whole file only: the start tail is itself a root tail (prev 0): one
   // entry spans [0, t) (recover_valid_chain's walk ends at once)
   const uint64_t top = a.counters[1];
   const bool troot = a.coff && top >= 21 && ld_u64_unaligned(a.file, top - 12) == 0;
-  const uint64_t root_t = troot ? top : pl->root_t;
+  uint64_t root_t = troot ? top : FUSED ? 0 : pl->root_t;
   if (a.counters[2]) st |= ST_OVERFLOW;
   const uint64_t start = incomplete ? NO_NODE : start_node(a);
   if (start == NO_NODE) st |= ST_NOSTART;
-  if (pl->nroot != 1) st |= ST_ROOTS;
+  if (!FUSED && pl->nroot != 1) st |= ST_ROOTS;
   __syncthreads();  // this block has read pl->status / nroot / root_t before block 0 rewrites them
   const uint32_t nbk = 1u << log2_nbk;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  // the plan: !FUSED block 0 now; FUSED the last block, once the look-back
+  // has every block's count (or now, when the counters alone decide)
+  auto write_plan = [&](uint32_t s2, uint64_t tot) {
     pl->K = K;
     pl->max_root = a.counters[0];
     pl->top_gap = top ? a.flen - top : 0;
@@ -667,12 +739,113 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       pl->chain_core = 0;
     } else {
       pl->start = start;
-      pl->status = st;
-      pl->chain_core = total;
-      pl->n_chain = st ? 0 : a.coff + total;
+      pl->status = s2;
+      pl->chain_core = tot;
+      pl->n_chain = s2 ? 0 : a.coff + tot;
+    }
+  };
+  const bool plan_block = FUSED ? blockIdx.x + 1 == gridDim.x : blockIdx.x == 0;
+  if ((!FUSED || st || troot) && plan_block && threadIdx.x == 0) write_plan(st, total);
+  if (st && !troot) return;
+  // FUSED: the shape check of this block's records (check_kernel, round 0),
+  // then the look-back; per-wave core counts in LDS
+  __shared__ uint32_t s_wcnt[CHAIN_WAVES];
+  __shared__ uint64_t s_lb[2];
+  __shared__ uint32_t s_fail, s_nroot, s_lbok;
+  __shared__ unsigned long long s_root_t;
+  if constexpr (FUSED) {
+    if (!troot) {
+      if (threadIdx.x == 0) { s_fail = 0; s_nroot = 0; s_root_t = 0; }
+      const uint32_t n = block_waves(a, s_pre);  // (barrier inside)
+      const uint64_t tag = (uint64_t)a.gen << 32;
+      const uint32_t wi = threadIdx.x >> 6, lane = threadIdx.x & 63;
+      const uint32_t chunk = (n + CHAIN_WAVES - 1) / CHAIN_WAVES;
+      const uint32_t c0 = min(n, wi * chunk), c1 = min(n, c0 + chunk);
+      uint32_t cnt = 0, nr = 0;
+      bool fail = false;
+      constexpr int CR = 4;
+      for (uint32_t base = c0; base < c1; base += CR * 64) {
+        uint64_t g[CR], cg[CR], cp[CR];
+        int64_t par[CR], pp[CR];
+        bool in[CR];
+#pragma unroll
+        for (int r = 0; r < CR; r++) {
+          const uint32_t i = base + (uint32_t)r * 64 + lane;
+          in[r] = i < c1;
+          g[r] = slot_of(a, s_pre, in[r] ? i : c0);
+          par[r] = a.d_par[g[r]];
+          cg[r] = a.childof[g[r]];
+        }
+#pragma unroll
+        for (int r = 0; r < CR; r++) {
+          const uint64_t q = par[r] >= 0 ? (uint64_t)par[r] : g[r];
+          pp[r] = a.d_par[q];
+          cp[r] = a.childof[q];
+        }
+#pragma unroll
+        for (int r = 0; r < CR; r++) {
+          if (!in[r]) break;
+          const int64_t p = par[r];
+          const bool linked = (cg[r] & ~0xffffffffull) == tag;
+          const bool core = g[r] == start || (linked && (p >= 0 || p == PAR_ROOT));  // is_core(g)
+          GST(a.flag[g[r]], (uint8_t)core);
+          if (!core) continue;
+          cnt++;
+          const bool plinked = (cp[r] & ~0xffffffffull) == tag;
+          if (p == PAR_ROOT) {
+            nr++;
+            const u32x4 r0 = a.c_rec[2 * g[r]];
+            s_root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);  // (any one: nroot != 1 fails the call)
+          } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
+            fail = true;  // dangling
+          } else if (cp[r] != claim_word(a.gen, g[r])) {
+            fail = true;  // branch
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 32; o; o >>= 1) {
+        cnt += __shfl_xor(cnt, o);
+        nr += __shfl_xor(nr, o);
+      }
+      if (lane == 0) {
+        s_wcnt[wi] = cnt;
+        if (nr) atomicAdd(&s_nroot, nr);
+      }
+      if (__ballot(fail) && lane == 0) s_fail = 1;
+      __syncthreads();
+      uint32_t btot = 0;
+#pragma unroll
+      for (int i = 0; i < CHAIN_WAVES; i++) btot += s_wcnt[i];
+      const uint32_t ltag = lb_tag(a.gen);
+      typedef __attribute__((address_space(1))) unsigned long long gu64;
+      if (threadIdx.x == 0 && blockIdx.x > 0)
+        __hip_atomic_store((gu64*)(lb_desc + blockIdx.x), lb_pack(ltag, 1, s_fail, s_nroot, btot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      if (wi == 0) {
+        uint64_t pc = 0;
+        bool pf = false;
+        uint32_t pn = 0;
+        const bool ok = lb_lookback(lb_desc, blockIdx.x, ltag, &pc, &pf, &pn);
+        if (lane == 0) {
+          const bool f2 = pf || s_fail;
+          const uint32_t n2 = pn + s_nroot;
+          __hip_atomic_store((gu64*)(lb_desc + blockIdx.x), lb_pack(ltag, 2, f2, n2, pc + btot), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          s_lb[0] = pc;
+          s_lb[1] = pc + btot;
+          s_lbok = ok;
+          if (plan_block)  // every block's count, failure and root links are in the prefix
+            write_plan((ok ? 0u : ST_LOOKBACK) | (f2 ? ST_SHAPE : 0u) | (n2 != 1 ? ST_ROOTS : 0u), pc + btot);
+        }
+      }
+      __syncthreads();
+      before = s_lb[0];
+      total = s_lb[1];  // (this block's inclusive prefix; the last block's is the total)
+      if (!s_lbok) return;
+      root_t = s_root_t;
     }
   }
-  if (st && !troot) return;
   for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
   tab[ti] = r_tab;
   lt.m16k[ti] = r_m16k;
@@ -688,7 +861,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   // the root entry (whole file: chain entry 0, no candidate record); its
   // CRC's slow path, if any, runs after the candidates
   bool root_slow = false;
-  if (blockIdx.x == 0 && a.coff && threadIdx.x == 0) {
+  // (FUSED: the block holding the root-linked core node -- it alone knows
+  // root_t -- or block 0 for a start tail that is itself a root)
+  const bool root_block = FUSED && !troot ? root_t != 0 : blockIdx.x == 0;
+  if (root_block && a.coff && threadIdx.x == 0) {
     uint64_t kh;
     root_slow = finalize_core(f, 0, NO_REC, -1, root_t, &kh);
     atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
@@ -703,7 +879,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     const uint64_t lt_mask = (1ull << lane) - 1;
     uint32_t woff, btot;
     {
-      const uint32_t v = lane < CHAIN_WAVES ? a.wpart[blockIdx.x * CHAIN_WAVES + lane] : 0u;
+      const uint32_t v = lane < CHAIN_WAVES ? (FUSED ? s_wcnt[lane] : a.wpart[blockIdx.x * CHAIN_WAVES + lane]) : 0u;
       uint32_t x = lane < wi ? v : 0u, y = v;
 #pragma unroll
       for (int o = 32; o; o >>= 1) {
@@ -825,8 +1001,23 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     hist[k] = n ? atomicAdd(&ia.bfill[k], n) : 0u;
   }
   __syncthreads();
-  const uint64_t n_chain = troot ? 1 : a.coff + total;
-  const uint64_t clo = min(n_chain, blockIdx.x ? a.coff + before : 0), chi = min(n_chain, bend);
+  // this block's chain positions [clo, chi) (block 0 from 0: the root entry;
+  // FUSED: the root block scatters position 0 on its own below)
+  uint64_t clo, chi;
+  if constexpr (FUSED) {
+    clo = troot ? 0 : a.coff + before;
+    chi = troot ? (blockIdx.x == 0 ? 1 : 0) : bend;
+    if (!troot && root_block && a.coff && threadIdx.x == 0) {
+      const uint64_t k0 = f.o_kh[0];
+      const uint32_t bk = idx_bucket(k0, log2_nbk);
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      if (pos < IDX_TCAP) ia.srec[(uint64_t)bk * IDX_TCAP + pos] = u64x2{k0, 0};
+    }
+  } else {
+    const uint64_t n_chain = troot ? 1 : a.coff + total;
+    clo = min(n_chain, blockIdx.x ? a.coff + before : 0);
+    chi = min(n_chain, bend);
+  }
   constexpr int SR = 4;  // keys loaded together per pass
   for (uint64_t base = clo; base < chi; base += SR * CHAIN_THREADS) {
     uint64_t k[SR];
