@@ -41,7 +41,8 @@ import torch  # noqa: E402
 import srd_amd as S  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-SCAN_SAMPLE = 4  # event-stamp every 4th scan launch (roofline.kernel_ms)
+SCAN_SAMPLE = 2  # event-stamp every 2nd scan launch (roofline.kernel_ms: >= 10 launches at 20 steps)
+PROBE_REPS = 8  # runs of the in-run streaming ceiling (srd_stream_probe_device; roofline.peak_measured)
 
 
 def kernel_sources_hash() -> str:
@@ -533,6 +534,15 @@ def main():
         torch.cuda.synchronize(d)
     dt = time.perf_counter() - t0
     scan_ms_sum, scan_n, _ = ctx.timings()
+    shard_ms = None
+    if multi is not None:
+        buf = (C.c_double * world)()
+        k = S.lib().srd_ctx_multi_shard_ms(ctx.h, buf, world)
+        shard_ms = [round(buf[i], 4) for i in range(min(k, world))]
+    # the streaming-read ceiling of the scan's geometry on these very bytes,
+    # after the timed region (the measured stream-read peak)
+    probe_bytes = (flen if multi is None else cuts[1] - soffs[0]) // 4096 * 4096
+    probe_best, probe_med = S.stream_probe_device(store.data_ptr(), probe_bytes, PROBE_REPS, ctx)
     scan_each = sorted(ctx.scan_list())  # the sampled timed steps' scan durations (ms), one per launch
     if multi is not None:
         multi["scan_ms"] = [(scan_ms_sum, scan_n)] + [c.timings()[:2] for c in ctxs[1:]]
@@ -608,6 +618,16 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
+            # the measured ceiling: srd_stream_probe_device streams the same
+            # store with the scan's geometry (one 16-wave block per CU, 64 B
+            # per lane, 3-deep ring) and does nothing with the bytes, best of
+            # PROBE_REPS runs in this process.  peak_measured = file bytes /
+            # probe ms; frac_measured = probe ms / scan ms (the scan against
+            # streaming alone, in algorithmic bytes: both read the same file)
+            "peak_measured": round(probe_bytes / (probe_best * 1e-3) / 1e9, 1),
+            "probe_ms_best": round(probe_best, 4),
+            "probe_ms_median": round(probe_med, 4),
+            "frac_measured": round(probe_best / scan_ms, 4),
             "traffic": traffic,
             "traffic_note": traffic_note,
             # the whole step (scan + glue + one host sync) against the same peak
@@ -617,13 +637,20 @@ def main():
     }
     if multi is not None:
         k = max(multi["n"], 1)
+        path_name = {S.SRD_MULTI_COMPOSED: "composed", S.SRD_MULTI_NEIGHBOUR: "neighbour",
+                     S.SRD_MULTI_WHOLE_FILE: "whole_file"}.get(summ.path, str(summ.path))
         out["multi"] = {"devices": devs, "shard_scan_ms": [round(x, 4) for x in shard_scan],
                         "validate_ms": round(multi["validate_ms"] / k, 4),
+                        "shard_validate_ms_last_call": shard_ms,
                         "exchange_ms": round(multi["exchange_ms"] / k, 4),
                         "call_ms": round(multi["total_ms"] / k, 4),
+                        "path": path_name, "mode": int(summ.mode),
+                        "peer_errors": int(summ.peer_errors), "shard_errors": int(summ.shard_errors),
                         "note": "validate_ms = the slowest shard's validate (host wall, its own thread); "
-                                "exchange_ms = index by owner over xGMI peer copies + owner builds; "
-                                "step = max over shards by construction (one call, all shards joined)"}
+                                "exchange_ms = index by owner over xGMI peer reads + owner builds; path = how "
+                                "the store composed (composed: every shard proven alone); peer_errors = cross-GPU "
+                                "copies staged by the runtime because peer access was refused (0: every exchange "
+                                "read the peers' HBM directly); step = max over shards by construction"}
     if world == 1 and not args.no_cpu and args.config == "c2":
         out["cpu_baseline"] = cpu_baseline(store, size, bytes_alg, args.cpu_budget)
     if args.e2e and world == 1:

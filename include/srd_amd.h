@@ -286,6 +286,10 @@ int srd_validate_index_multi_device(srd_ctx *const *ctxs, uint32_t n_ctx,
 /* The summary of the last multi-GPU open (host or device input) that had ctx
  * as ctxs[0]: which path decided it, totals, timings. */
 int srd_ctx_multi_summary(srd_ctx *ctx, srd_multi_summary *out);
+/* Its per-shard validate times (host wall ms of each shard's own thread,
+ * re-validations included): copies up to cap of them to out and returns the
+ * shard count (< 0: error). */
+int srd_ctx_multi_shard_ms(srd_ctx *ctx, double *out, int cap);
 /* Staging of the last host-input call on ctx: *mode = 0 pinned input, 1
  * registered mapping, 2 bounce buffers, 3 pageable copy (-1 none yet);
  * *stage_ms = host wall time from the call's start until the store was in
@@ -297,6 +301,16 @@ int srd_ctx_stage_info(srd_ctx *ctx, int *mode, double *stage_ms);
  * KeyIndexer HashMap applies to every key_hash.  Asynchronous on `stream`. */
 int srd_index_hash_device(srd_ctx *ctx, const uint64_t *d_keys, uint64_t n,
                           uint64_t *d_out, void *stream);
+
+/* Measurement utility (bench.py's roofline.peak_measured; not part of the
+ * reference interface): the streaming-read ceiling of the scan's geometry
+ * -- one 16-wave block per CU, a contiguous tile range per wave, 64 B per
+ * lane, a 3-deep register ring, no work on the bytes -- over the first
+ * floor(bytes / 4096) tiles of d_buf, timed `reps` times (after one warm-up
+ * run) with HIP events on the context stream.  *best_ms / *median_ms
+ * (nullable) over the reps.  Synchronises. */
+int srd_stream_probe_device(srd_ctx *ctx, const uint8_t *d_buf, uint64_t bytes,
+                            int reps, double *best_ms, double *median_ms);
 
 /* recover_valid_chain: final_len only (host input). */
 int srd_recover_valid_chain(srd_ctx *ctx, const uint8_t *file,

@@ -28,6 +28,7 @@
 #include "srd_glue.hip"
 #include "srd_writer.hip"
 #include "srd_index.hip"
+#include "srd_probe.hip"
 
 using namespace srd;
 
@@ -192,6 +193,7 @@ struct Ctx {
   std::vector<hipStream_t> stage_streams;
   std::vector<hipEvent_t> stage_ev;
   srd_multi_summary last_multi{};  // the last multi-GPU open with this context as ctxs[0]
+  std::vector<double> last_shard_ms;  // its per-shard validate times (srd_ctx_multi_shard_ms)
   void* h_out = nullptr;  // pinned host result arrays (srd_validate_index / _multi)
   uint64_t h_out_n = 0;
   uint8_t lgen = 0;  // generation of the index build's non-latest marks (B_LATEST8)
@@ -220,7 +222,7 @@ enum BufId {
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
   B_GKEY, B_GVAL, B_GOKEY, B_GOPACKED,
   B_WTOT, B_WROOT, B_KTOT, B_DONE, B_SPAN_FIRST,
-  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN, B_LOOKB,
+  B_XKEY, B_XVAL, B_GATHER, B_RFLAG, B_O_PACKED, B_VSCAN, B_LOOKB, B_PROBE, B_XTOT,
   B_COUNT_
 };
 
@@ -403,6 +405,12 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
   } else if (a.variant == 24) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 24>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 24>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 25) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 25>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 25>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 26) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 26>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 26>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 22) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 22>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 22>, grid, block, 0, s, e0, e1, 0, a);
@@ -1484,8 +1492,11 @@ extern "C" int srd_validate_span_device(srd_ctx* c, const uint8_t* d_span, uint6
 // stable partition of n (key, value) device pairs by owner rank; interleaved
 // output at out (out_v == nullptr) or keys at out / values at out_v.  counts
 // (host, [world]) receives the group sizes.  Synchronises.
+// counts (host, nullable): the per-owner pair counts, read back with one
+// host round trip; d_counts (nullable): their device address instead, no
+// sync (the multi-GPU exchange's owners read them over xGMI)
 static int partition_impl(Ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, uint32_t world,
-                          uint64_t* out, uint64_t* out_v, uint64_t* counts) {
+                          uint64_t* out, uint64_t* out_v, uint64_t* counts, const uint64_t** d_counts = nullptr) {
   const uint64_t nc = (uint64_t)world * GLUE_BLOCKS + 1;
   TRY(ensure(c, B_PCNT, nc * 4));
   TRY(ensure(c, B_POFF, nc * 4 + 8 * PART_MAX_WORLD));
@@ -1510,8 +1521,11 @@ static int partition_impl(Ctx* c, const uint64_t* keys, const uint64_t* vals, ui
   part_counts_kernel<<<1, 64, 0, c->stream>>>(a);
   KCHK(c, "part_counts_kernel");
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(counts, a.counts, world * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(spin_sync(c->stream));
+  if (d_counts) *d_counts = a.counts;
+  if (counts) {
+    HIPCHK(hipMemcpyAsync(counts, a.counts, world * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(spin_sync(c->stream));
+  }
   return 0;
 }
 
@@ -1555,6 +1569,37 @@ static int index_build_sep(Ctx* c, const uint64_t* keys, const uint64_t* vals, u
   HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(spin_sync(c->stream));
   if (c->h_plan->idx_overflow) return index_global(c, n, n_index, keys, vals, okeys, opacked);
+  *n_index = c->h_plan->n_index;
+  return 0;
+}
+
+__global__ void index_prep_dev_kernel(Plan* pl, const uint64_t* d_n, uint32_t* zero, uint32_t nz) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nz) zero[i] = 0;
+  if (i < sizeof(Plan) / 4) ((uint32_t*)pl)[i] = 0;
+  __syncthreads();
+  if (i == 0) pl->n_chain = *d_n;
+}
+// index_build_sep with the pair count on the device (*d_n <= n_max): the
+// multi-GPU owners' build right behind their gather, no host round trip for
+// the count; buckets sized for n_est expected pairs.  Synchronises once.
+static int index_build_dev(Ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n_max, const uint64_t* d_n,
+                           uint64_t n_est, uint64_t* okeys, uint64_t* opacked, uint64_t* n_index) {
+  *n_index = 0;
+  if (!n_max) return 0;
+  TRY(ensure(c, B_MPLAN, sizeof(Plan)));
+  const uint32_t log2_nbk = index_log2_buckets(std::max<uint64_t>(n_est, 1));
+  TRY(alloc_index(c, n_max, log2_nbk));
+  Plan* pl = P<Plan>(c, B_MPLAN);
+  uint32_t nz = 0;
+  uint32_t* zw = index_zero_words(c, log2_nbk, &nz);
+  index_prep_dev_kernel<<<(std::max<uint32_t>(nz, 64) + 255) / 256, 256, 0, c->stream>>>(pl, d_n, zw, nz);
+  KCHK(c, "index_prep_dev_kernel");
+  TRY(launch_index_bucketed(c, keys, vals, &pl->n_chain, &pl->status, log2_nbk, okeys, opacked, pl, false, nullptr,
+                            true));
+  HIPCHK(hipMemcpyAsync(c->h_plan, pl, sizeof(Plan), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(spin_sync(c->stream));
+  if (c->h_plan->idx_overflow) return index_global(c, c->h_plan->n_chain, n_index, keys, vals, okeys, opacked);
   *n_index = c->h_plan->n_index;
   return 0;
 }
@@ -2140,7 +2185,8 @@ struct MShard {
   srd_device_result r{};
   bool proven = false;
   bool parted = false;
-  uint64_t cnt[PART_MAX_WORLD] = {};  // owner run lengths of the partitioned shard index
+  uint64_t cnt[PART_MAX_WORLD] = {};  // owner run lengths of the partitioned shard index (host counts)
+  const uint64_t* d_cnt = nullptr;     // or their device address (dev_counts: no host round trip)
 };
 
 static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_result* shards, srd_multi_summary* sum) {
@@ -2153,6 +2199,14 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
   std::vector<double> vms(nc, 0.0);
   uint32_t path = SRD_MULTI_COMPOSED, n_err = 0;
   std::string first_err;
+  // every owner can read every source's HBM (peer access, or one device):
+  // the partition counts stay on the devices and the owners' gather reads
+  // them (no host round trip per shard); otherwise host counts and copies
+  bool dev_counts = !merged && nc > 1;
+  for (uint32_t p = 0; p < nc && dev_counts; p++)
+    for (uint32_t q = 0; q < nc && dev_counts; q++)
+      if (in.ctxs[p]->device != in.ctxs[q]->device && !enable_peer(in.ctxs[p]->device, in.ctxs[q]->device))
+        dev_counts = false;
 
   // owner partition of shard i's index (by-owner layout, nc > 1)
   auto part = [&](uint32_t i) -> int {
@@ -2162,7 +2216,11 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
     const uint64_t n = s.r.n_index;
     TRY(ensure(c, B_XKEY, std::max<uint64_t>(n, 1) * 8));
     TRY(ensure(c, B_XVAL, std::max<uint64_t>(n, 1) * 8));
-    if (n) TRY(partition_impl(c, s.r.index_key_hash, s.r.index_packed, n, nc, P<uint64_t>(c, B_XKEY), P<uint64_t>(c, B_XVAL), s.cnt));
+    if (dev_counts)  // (n == 0 too: the owners read its zero counts)
+      TRY(partition_impl(c, s.r.index_key_hash, s.r.index_packed, n, nc, P<uint64_t>(c, B_XKEY), P<uint64_t>(c, B_XVAL),
+                         nullptr, &s.d_cnt));
+    else if (n)
+      TRY(partition_impl(c, s.r.index_key_hash, s.r.index_packed, n, nc, P<uint64_t>(c, B_XKEY), P<uint64_t>(c, B_XVAL), s.cnt));
     s.parted = true;
     HIPCHK(mark_ready(c));  // the owners' pulls wait on it
     return 0;
@@ -2336,10 +2394,53 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
     });
     for (uint32_t i = 0; i < nc; i++)
       if (erc[i]) { set_err(eerr[i]); return erc[i]; }
+    uint64_t ni_all = 0, ni_max1 = 0;  // pairs of every shard; the largest shard's
+    for (auto& x : sh) {
+      ni_all += x.r.n_index;
+      ni_max1 = std::max<uint64_t>(ni_max1, x.r.n_index);
+    }
     parallel_for(nc, on, [&](uint32_t p) {
       Ctx* c = in.ctxs[p];
       int& r = erc[p];
       if (hipSetDevice(c->device) != hipSuccess) { r = SRD_ERR_HIP; eerr[p] = "hipSetDevice"; return; }
+      if (dev_counts) {
+        // the owner's runs: lengths and offsets from the sources' partition
+        // counts in their HBM (gather_runs_kernel), the build's n on the
+        // device; sized by the bound ni_all, buckets for ni_all / nc pairs
+        // (owner = the key hash's top bits: an even split)
+        const uint64_t m1 = std::max<uint64_t>(ni_all, 1);
+        if (!r) r = ensure(c, B_GKEY, m1 * 8);
+        if (!r) r = ensure(c, B_GVAL, m1 * 8);
+        if (!r) r = ensure(c, B_GOKEY, m1 * 8);
+        if (!r) r = ensure(c, B_GOPACKED, m1 * 8);
+        if (!r) r = ensure(c, B_XTOT, 64);
+        GatherArgs ga{};
+        for (uint32_t s = 0; s < nc; s++) {
+          Ctx* cs = in.ctxs[s];
+          ga.src_k[s] = P<uint64_t>(cs, B_XKEY);
+          ga.src_v[s] = P<uint64_t>(cs, B_XVAL);
+          ga.src_cnt[s] = sh[s].d_cnt;
+          if (!r && cs != c && cs->ready_recorded && hipStreamWaitEvent(c->stream, cs->ev_ready, 0) != hipSuccess) {
+            set_err("index exchange: event wait failed");
+            r = SRD_ERR_HIP;
+          }
+        }
+        ga.dst_k = P<uint64_t>(c, B_GKEY);
+        ga.dst_v = P<uint64_t>(c, B_GVAL);
+        ga.d_total = P<uint64_t>(c, B_XTOT);
+        ga.owner = p;
+        ga.nsrc = nc;
+        if (!r) {
+          const uint64_t per = ni_max1 / nc + 1;  // ~ a source's run for one owner
+          const dim3 grid((unsigned)std::min<uint64_t>(std::max<uint64_t>((2 * per + 255) / 256, 1), 128), nc);
+          gather_runs_kernel<<<grid, 256, 0, c->stream>>>(ga);
+          if (hipGetLastError() != hipSuccess) { set_err("index exchange: gather launch failed"); r = SRD_ERR_HIP; }
+        }
+        if (!r) r = index_build_dev(c, ga.dst_k, ga.dst_v, ni_all, ga.d_total, ni_all / nc + 1, P<uint64_t>(c, B_GOKEY),
+                                    P<uint64_t>(c, B_GOPACKED), &ni[p]);
+        if (r) eerr[p] = g_err;
+        return;
+      }
       uint64_t NI = 0;
       for (auto& x : sh) NI += x.cnt[p];
       const uint64_t m1 = std::max<uint64_t>(NI, 1);
@@ -2440,6 +2541,7 @@ static int multi_device_impl(const MultiIn& in, uint32_t flags, srd_device_resul
   S.total_ms = ms_since(t_call);
   if (sum) *sum = S;
   in.ctxs[0]->last_multi = S;
+  in.ctxs[0]->last_shard_ms = vms;
   return 0;
 }
 
@@ -2462,6 +2564,13 @@ extern "C" int srd_validate_index_multi_device(srd_ctx* const* ctxs, uint32_t nc
   std::atomic<uint32_t> peer_fail{0};
   MultiIn in{ctxs, nc, d_spans, span_offs, cuts, flen, &peer_fail};
   return multi_device_impl(in, flags, shards, summary);
+}
+
+extern "C" int srd_ctx_multi_shard_ms(srd_ctx* c, double* out, int cap) {
+  if (!c || cap < 0 || (cap && !out)) { set_err("bad argument"); return SRD_ERR_ARG; }
+  const int n = (int)c->last_shard_ms.size();
+  for (int i = 0; i < std::min(n, cap); i++) out[i] = c->last_shard_ms[i];
+  return n;
 }
 
 extern "C" int srd_ctx_multi_summary(srd_ctx* c, srd_multi_summary* out) {
@@ -2555,6 +2664,35 @@ extern "C" int srd_validate_index_multi(srd_ctx* const* ctxs, uint32_t nc, const
   out->n_crc_bad = sum.n_crc_bad;
   out->n_candidates = sum.n_candidates;
   out->mode = sum.mode;
+  return 0;
+}
+
+extern "C" int srd_stream_probe_device(srd_ctx* c, const uint8_t* d_buf, uint64_t bytes, int reps, double* best_ms,
+                                       double* median_ms) {
+  if (!c || !d_buf || bytes < TILE || reps < 1 || !best_ms) { set_err("bad argument"); return SRD_ERR_ARG; }
+  HIPCHK(hipSetDevice(c->device));
+  const uint64_t ntiles = bytes / TILE;
+  TRY(ensure(c, B_PROBE, (uint64_t)c->scan_blocks * 16 * 4));
+  hipEvent_t e[2];
+  for (auto& x : e) HIPCHK(hipEventCreateWithFlags(&x, hipEventReleaseToDevice));
+  std::vector<float> ms;
+  int rc = 0;
+  for (int r = 0; r < reps + 1 && !rc; r++) {  // (the first run warms the code and the TLB)
+    hipExtLaunchKernelGGL(stream_probe_kernel, dim3(c->scan_blocks), dim3(1024), 0, c->stream, e[0], e[1], 0, d_buf,
+                          ntiles, P<uint32_t>(c, B_PROBE));
+    float t = 0;
+    if (hipGetLastError() != hipSuccess || hipEventSynchronize(e[1]) != hipSuccess ||
+        hipEventElapsedTime(&t, e[0], e[1]) != hipSuccess) {
+      set_err("stream probe launch failed");
+      rc = SRD_ERR_HIP;
+    }
+    if (r) ms.push_back(t);
+  }
+  for (auto& x : e) hipEventDestroy(x);
+  if (rc) return rc;
+  std::sort(ms.begin(), ms.end());
+  *best_ms = ms[0];
+  if (median_ms) *median_ms = ms[ms.size() / 2];
   return 0;
 }
 
@@ -3088,6 +3226,14 @@ extern "C" int srd_compact_device(srd_ctx* c, const uint8_t* d_file, uint64_t fl
   return 0;
 }
 
+#ifdef SRD_GLUE_STAMPS
+// timing-only build: the last fused chain_finalize's per-block phase stamps
+extern "C" int srd_debug_glue_stamps(uint64_t* out) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_glue_stamp), sizeof(uint64_t) * CHAIN_BLOCKS * 8));
+  return 0;
+}
+#endif
 #ifdef SRD_WAVE_STAMPS
 // timing-only build: the last scan's per-wave end stamps and per-block start
 // stamps (s_memrealtime, 100 MHz)

@@ -629,6 +629,13 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
 // dispatched before it, so the grid cannot deadlock; a bounded spin that runs
 // out sets ST_LOOKBACK and the host takes the full pass.
 constexpr uint32_t ST_LOOKBACK = 32;
+#ifdef SRD_GLUE_STAMPS  // timing-only build (tools/glue_stamps.py): per-block phase ends of chain_finalize<true>
+__device__ uint64_t g_glue_stamp[CHAIN_BLOCKS * 8];
+#define GLUE_STAMP(i) \
+  do { if (FUSED && threadIdx.x == 0) g_glue_stamp[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define GLUE_STAMP(i) do {} while (0)
+#endif
 constexpr uint64_t LB_CNT = (1ull << 35) - 1;
 __device__ __forceinline__ uint64_t lb_pack(uint32_t tag, uint32_t st, bool fail, uint32_t nr, uint64_t cnt) {
   return ((uint64_t)tag << 40) | ((uint64_t)st << 38) | ((uint64_t)fail << 37) | ((uint64_t)min(nr, 3u) << 35) |
@@ -679,6 +686,19 @@ __device__ bool lb_lookback(unsigned long long* desc, uint32_t b, uint32_t tag, 
   return true;
 }
 
+// the previous lane's value (DPP wave_shr:1), lane 0 taking `lane0` (the
+// previous pass's lane 63): record i's neighbour i - 1 in a pass of 64
+__device__ __forceinline__ uint32_t prev_lane(uint32_t v, uint32_t lane0) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint64_t prev_lane64(uint64_t v, uint64_t lane0) {
+  return (uint64_t)prev_lane((uint32_t)v, (uint32_t)lane0) | ((uint64_t)prev_lane((uint32_t)(v >> 32), (uint32_t)(lane0 >> 32)) << 32);
+}
+__device__ __forceinline__ uint64_t lane63_64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, 63) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), 63) << 32);
+}
+
 // FUSED (round 0 of the optimistic pass): check_kernel's shape test of the
 // block's own records first, the chain ranks from the look-back instead of
 // check_kernel's per-block totals, the plan written by the LAST block once
@@ -698,6 +718,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   // plan's dependent ones below (one round trip instead of a load -> store
   // loop after the plan)
   static_assert(CHAIN_THREADS == 1024, "one word of each 1024-word table per thread");
+  GLUE_STAMP(0);
   const uint32_t ti = threadIdx.x;
   const uint32_t r_tab = g_tabs.tab[ti >> 8][ti & 255],
                  r_m16k = (&g_tabs.m16k[0][0])[ti], r_m32k = (&g_tabs.m32k[0][0])[ti];
@@ -749,74 +770,97 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   if (st && !troot) return;
   // FUSED: the shape check of this block's records (check_kernel, round 0),
   // then the look-back; per-wave core counts in LDS
-  __shared__ uint32_t s_wcnt[CHAIN_WAVES];
+  __shared__ uint32_t s_vcnt[BW_MAX];  // FUSED: core records per scan wave of the block
   __shared__ uint64_t s_lb[2];
   __shared__ uint32_t s_fail, s_nroot, s_lbok;
   __shared__ unsigned long long s_root_t;
   if constexpr (FUSED) {
     if (!troot) {
       if (threadIdx.x == 0) { s_fail = 0; s_nroot = 0; s_root_t = 0; }
-      const uint32_t n = block_waves(a, s_pre);  // (barrier inside)
+      __syncthreads();
       const uint64_t tag = (uint64_t)a.gen << 32;
       const uint32_t wi = threadIdx.x >> 6, lane = threadIdx.x & 63;
-      const uint32_t chunk = (n + CHAIN_WAVES - 1) / CHAIN_WAVES;
-      const uint32_t c0 = min(n, wi * chunk), c1 = min(n, c0 + chunk);
-      uint32_t cnt = 0, nr = 0;
+      // chain wave wi takes the block's scan waves wi, wi + 16, ... whole:
+      // record r of scan wave w is slot w * wcap + r, so no slot map (the
+      // waves' record counts differ by the scan's wave shares, ~ +-15 %).
+      // The parent of a record is almost always the previous record (slot g
+      // - 1): its words come from the neighbour lane (prev_lane), not a load
+      uint32_t nr = 0;
       bool fail = false;
       constexpr int CR = 4;
-      for (uint32_t base = c0; base < c1; base += CR * 64) {
-        uint64_t g[CR], cg[CR], cp[CR];
-        int64_t par[CR], pp[CR];
-        bool in[CR];
+      for (uint32_t v = wi; v < a.wpb; v += CHAIN_WAVES) {
+        const uint64_t w = (uint64_t)blockIdx.x * a.wpb + v;
+        const uint32_t n = w < a.n_waves ? (uint32_t)min(a.wave_total[w] & ~(1ull << 63), a.wcap) : 0u;
+        const uint64_t gb = w * a.wcap;
+        int64_t c_par = PAR_MISS;  // the previous pass's lane-63 words
+        uint64_t c_cg = 0;
+        uint32_t cnt = 0;
+        for (uint32_t base = 0; base < n; base += CR * 64) {
+          uint64_t g[CR], cg[CR], cp[CR];
+          int64_t par[CR], pp[CR];
+          bool in[CR], need[CR];
 #pragma unroll
-        for (int r = 0; r < CR; r++) {
-          const uint32_t i = base + (uint32_t)r * 64 + lane;
-          in[r] = i < c1;
-          g[r] = slot_of(a, s_pre, in[r] ? i : c0);
-          par[r] = a.d_par[g[r]];
-          cg[r] = a.childof[g[r]];
-        }
+          for (int r = 0; r < CR; r++) {
+            const uint32_t i = base + (uint32_t)r * 64 + lane;
+            in[r] = i < n;
+            g[r] = gb + (in[r] ? i : 0u);
+            par[r] = a.d_par[g[r]];
+            cg[r] = a.childof[g[r]];
+          }
+          bool any = false;
 #pragma unroll
-        for (int r = 0; r < CR; r++) {
-          const uint64_t q = par[r] >= 0 ? (uint64_t)par[r] : g[r];
-          pp[r] = a.d_par[q];
-          cp[r] = a.childof[q];
-        }
+          for (int r = 0; r < CR; r++) {
+            const uint32_t i = base + (uint32_t)r * 64 + lane;
+            const int64_t l0p = r ? (int64_t)(int32_t)__builtin_amdgcn_readlane((uint32_t)par[r - 1], 63) : c_par;
+            const uint64_t l0c = r ? lane63_64(cg[r - 1]) : c_cg;
+            pp[r] = (int64_t)(int32_t)prev_lane((uint32_t)par[r], (uint32_t)l0p);
+            cp[r] = prev_lane64(cg[r], l0c);
+            need[r] = in[r] && par[r] >= 0 && !(i > 0 && (uint64_t)par[r] == g[r] - 1);
+            any = any || need[r];
+          }
+          if (__ballot(any)) {  // (uniform) a parent elsewhere: its words by a load
 #pragma unroll
-        for (int r = 0; r < CR; r++) {
-          if (!in[r]) break;
-          const int64_t p = par[r];
-          const bool linked = (cg[r] & ~0xffffffffull) == tag;
-          const bool core = g[r] == start || (linked && (p >= 0 || p == PAR_ROOT));  // is_core(g)
-          GST(a.flag[g[r]], (uint8_t)core);
-          if (!core) continue;
-          cnt++;
-          const bool plinked = (cp[r] & ~0xffffffffull) == tag;
-          if (p == PAR_ROOT) {
-            nr++;
-            const u32x4 r0 = a.c_rec[2 * g[r]];
-            s_root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);  // (any one: nroot != 1 fails the call)
-          } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
-            fail = true;  // dangling
-          } else if (cp[r] != claim_word(a.gen, g[r])) {
-            fail = true;  // branch
+            for (int r = 0; r < CR; r++)
+              if (need[r]) {
+                pp[r] = a.d_par[par[r]];
+                cp[r] = a.childof[par[r]];
+              }
+          }
+          c_par = (int64_t)(int32_t)__builtin_amdgcn_readlane((uint32_t)par[CR - 1], 63);
+          c_cg = lane63_64(cg[CR - 1]);
+#pragma unroll
+          for (int r = 0; r < CR; r++) {
+            if (!in[r]) break;
+            const int64_t p = par[r];
+            const bool linked = (cg[r] & ~0xffffffffull) == tag;
+            const bool core = g[r] == start || (linked && (p >= 0 || p == PAR_ROOT));  // is_core(g)
+            GST(a.flag[g[r]], (uint8_t)core);
+            if (!core) continue;
+            cnt++;
+            const bool plinked = (cp[r] & ~0xffffffffull) == tag;
+            if (p == PAR_ROOT) {
+              nr++;
+              const u32x4 r0 = a.c_rec[2 * g[r]];
+              s_root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);  // (any one: nroot != 1 fails the call)
+            } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
+              fail = true;  // dangling
+            } else if (cp[r] != claim_word(a.gen, g[r])) {
+              fail = true;  // branch
+            }
           }
         }
+#pragma unroll
+        for (int o = 32; o; o >>= 1) cnt += __shfl_xor(cnt, o);
+        if (lane == 0) s_vcnt[v] = cnt;
       }
 #pragma unroll
-      for (int o = 32; o; o >>= 1) {
-        cnt += __shfl_xor(cnt, o);
-        nr += __shfl_xor(nr, o);
-      }
-      if (lane == 0) {
-        s_wcnt[wi] = cnt;
-        if (nr) atomicAdd(&s_nroot, nr);
-      }
+      for (int o = 32; o; o >>= 1) nr += __shfl_xor(nr, o);
+      if (lane == 0 && nr) atomicAdd(&s_nroot, nr);
       if (__ballot(fail) && lane == 0) s_fail = 1;
       __syncthreads();
+      GLUE_STAMP(1);
       uint32_t btot = 0;
-#pragma unroll
-      for (int i = 0; i < CHAIN_WAVES; i++) btot += s_wcnt[i];
+      for (uint32_t v = 0; v < a.wpb; v++) btot += s_vcnt[v];
       const uint32_t ltag = lb_tag(a.gen);
       typedef __attribute__((address_space(1))) unsigned long long gu64;
       if (threadIdx.x == 0 && blockIdx.x > 0)
@@ -840,6 +884,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
         }
       }
       __syncthreads();
+      GLUE_STAMP(2);
       before = s_lb[0];
       total = s_lb[1];  // (this block's inclusive prefix; the last block's is the total)
       if (!s_lbok) return;
@@ -858,6 +903,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     lt.zero_crc[ti] = r_zc;
   }
   __syncthreads();
+  GLUE_STAMP(3);
   // the root entry (whole file: chain entry 0, no candidate record); its
   // CRC's slow path, if any, runs after the candidates
   bool root_slow = false;
@@ -870,7 +916,132 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     atomicAdd(&hist[idx_bucket(kh, log2_nbk)], 1u);
   }
   uint64_t bend = a.coff + before;  // the end of this block's chain positions
-  if (!troot) {
+  if (FUSED && !troot) {
+    // the same scan waves per chain wave as the check above; a scan wave's
+    // chain positions start at this block's prefix + the core records of the
+    // block's earlier scan waves
+    const uint32_t wi = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    uint32_t btot = 0;
+    for (uint32_t v = 0; v < a.wpb; v++) btot += s_vcnt[v];
+    bend += btot;
+    auto wave_sync = [&]() {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    const u32x4* t4 = (const u32x4*)f.tile;
+    for (uint32_t v = wi; v < a.wpb; v += CHAIN_WAVES) {
+      const uint64_t w = (uint64_t)blockIdx.x * a.wpb + v;
+      const uint32_t n = w < a.n_waves ? (uint32_t)min(a.wave_total[w] & ~(1ull << 63), a.wcap) : 0u;
+      const uint64_t gb = w * a.wcap;
+      uint32_t voff = 0;
+      for (uint32_t u = 0; u < v; u++) voff += s_vcnt[u];
+      uint64_t run = a.coff + before + voff;  // this scan wave's next chain position
+      const uint64_t run0 = run;
+      uint32_t nsq = 0;  // wave-uniform: entries in the wave's slow queue
+      auto flush_slow = [&]() {
+        if (!nsq) return;
+        wave_sync();
+        unsigned long long sbase = 0;
+        if (lane == 0) sbase = atomicAdd(f.n_slow, (unsigned long long)nsq);
+        sbase = __shfl(sbase, 0);
+        for (uint32_t q = lane; q < nsq; q += 64) f.slow_list[sbase + q] = run0 + wslow[wi][q];
+        wave_sync();
+      };
+      uint32_t c_fl = 3u << F_SUF_SHIFT, c_suf = 0;  // the previous pass's lane-63 record words
+      for (uint32_t base = 0; base < n; base += 64 * FIN_R) {
+        bool fl[FIN_R];
+        uint64_t gi[FIN_R], kh[FIN_R];
+        int64_t par[FIN_R];
+        uint32_t psuf[FIN_R];
+        FinIn e[FIN_R];
+        // level 1: core flag, parent and the record itself, all at the slot
+#pragma unroll
+        for (int r = 0; r < FIN_R; r++) {
+          const uint32_t i = base + (uint32_t)r * 64 + lane;
+          gi[r] = gb + (i < n ? i : 0u);
+          fl[r] = i < n && a.flag[gi[r]];
+          par[r] = a.d_par[gi[r]];
+          e[r].mo = f.c_m[gi[r]];
+          const u32x4 r0 = f.c_rec[2 * gi[r]], r1 = f.c_rec[2 * gi[r] + 1];
+          e[r].p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
+          kh[r] = (uint64_t)r0[2] | ((uint64_t)r0[3] << 32);
+          e[r].crc_st = r1[0];
+          e[r].sxv = r1[1];
+          e[r].fl = r1[3];
+          psuf[r] = r1[2];
+        }
+        uint32_t rank[FIN_R], tot = 0;
+#pragma unroll
+        for (int r = 0; r < FIN_R; r++) {
+          const uint64_t b = __ballot(fl[r]);
+          rank[r] = tot + (uint32_t)__popcll(b & lt_mask);
+          tot += (uint32_t)__popcll(b);
+        }
+        // level 2: the parent's record words -- the previous record's (the
+        // neighbour lane) when it is the parent, else a load -- and the tile
+        // values.  A root-linked candidate has no parent record (start 0)
+        bool any = false, need[FIN_R];
+#pragma unroll
+        for (int r = 0; r < FIN_R; r++) {
+          const uint32_t i = base + (uint32_t)r * 64 + lane;
+          const uint32_t l0f = r ? (uint32_t)__builtin_amdgcn_readlane(e[r - 1].fl, 63) : c_fl;
+          const uint32_t l0s = r ? (uint32_t)__builtin_amdgcn_readlane(psuf[r - 1], 63) : c_suf;
+          const uint32_t nf = prev_lane(e[r].fl, l0f), ns = prev_lane(psuf[r], l0s);
+          need[r] = fl[r] && par[r] >= 0 && !(i > 0 && (uint64_t)par[r] == gi[r] - 1);
+          any = any || need[r];
+          e[r].pfl = par[r] >= 0 ? nf : (3u << F_SUF_SHIFT);
+          e[r].psuf = ns;
+          // idle lanes read the last tile's values (resident in span mode too)
+          const uint64_t mo = fl[r] ? e[r].mo : f.flen - 1;
+          const uint64_t st0 = !fl[r] ? mo : (e[r].fl & F_TOMB) ? e[r].p : e[r].p + prepad64(e[r].p);
+          e[r].t0 = t4[st0 / TILE];
+          e[r].t1 = t4[mo / TILE];
+        }
+        if (__ballot(any)) {  // (uniform)
+#pragma unroll
+          for (int r = 0; r < FIN_R; r++)
+            if (need[r]) {
+              const u32x4 pr1 = f.c_rec[2 * (uint64_t)par[r] + 1];
+              e[r].pfl = pr1[3];
+              e[r].psuf = pr1[2];
+            }
+        }
+        c_fl = (uint32_t)__builtin_amdgcn_readlane(e[FIN_R - 1].fl, 63);
+        c_suf = (uint32_t)__builtin_amdgcn_readlane(psuf[FIN_R - 1], 63);
+        // the record's own outputs and the index histogram while those loads fly
+#pragma unroll
+        for (int r = 0; r < FIN_R; r++) {
+          if (!fl[r]) continue;
+          const uint64_t c = run + rank[r];
+          GST(f.o_mo[c], e[r].mo);
+          GST(f.o_kh[c], kh[r]);
+          GST(f.o_packed[c], ((kh[r] >> 48) << 48) | (e[r].mo & 0xFFFFFFFFFFFFull));  // key_indexer.rs:79-85
+          GST(f.o_prev[c], e[r].p);
+          GST(f.o_crc_st[c], e[r].crc_st);
+          atomicAdd(&hist[idx_bucket(kh[r], log2_nbk)], 1u);
+        }
+#pragma unroll
+        for (int r = 0; r < FIN_R; r++) {
+          const uint64_t c = run + rank[r];
+          const bool slow = fl[r] && finalize_in(f, c, e[r], lt);
+          const uint64_t sb = __ballot(slow);
+          const uint32_t k = (uint32_t)__popcll(sb);
+          if (k) {
+            if (nsq + k > WSLOW) {
+              flush_slow();
+              nsq = 0;
+            }
+            if (slow) wslow[wi][nsq + __popcll(sb & lt_mask)] = (uint32_t)(c - run0);
+            nsq += k;
+          }
+        }
+        run += tot;
+      }
+      flush_slow();
+    }
+  } else if (!troot) {
     const uint32_t n = block_waves(a, s_pre);
     // wave chunks as in check_kernel: wave wi ranks its records from its
     // chunk's offset (the per-chunk core counts) with ballots -- the waves
@@ -879,7 +1050,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     const uint64_t lt_mask = (1ull << lane) - 1;
     uint32_t woff, btot;
     {
-      const uint32_t v = lane < CHAIN_WAVES ? (FUSED ? s_wcnt[lane] : a.wpart[blockIdx.x * CHAIN_WAVES + lane]) : 0u;
+      const uint32_t v = lane < CHAIN_WAVES ? a.wpart[blockIdx.x * CHAIN_WAVES + lane] : 0u;
       uint32_t x = lane < wi ? v : 0u, y = v;
 #pragma unroll
       for (int o = 32; o; o >>= 1) {
@@ -992,6 +1163,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   }
   if (root_slow) f.slow_list[atomicAdd(f.n_slow, 1ull)] = 0;  // (block 0, thread 0 only)
   __syncthreads();
+  GLUE_STAMP(4);
   // KeyIndexer::build's scatter for this block's chain positions [clo, run)
   // (block 0 from 0: the root entry): claim the block's range of every
   // bucket, then one (key, position) record per entry into it; the keys are
@@ -1001,6 +1173,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     hist[k] = n ? atomicAdd(&ia.bfill[k], n) : 0u;
   }
   __syncthreads();
+  GLUE_STAMP(5);
   // this block's chain positions [clo, chi) (block 0 from 0: the root entry;
   // FUSED: the root block scatters position 0 on its own below)
   uint64_t clo, chi;
@@ -1035,6 +1208,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       if (pos < IDX_TCAP) ia.srec[(uint64_t)bk * IDX_TCAP + pos] = u64x2{k[r], c};  // else: idx_dedup flags the bucket
     }
   }
+  GLUE_STAMP(6);
 }
 
 // --------------------------------------------------------------------------
@@ -1312,18 +1486,42 @@ __global__ void part_counts_kernel(PartArgs a) {
 // source shard; its run read over xGMI straight from the source GPU's HBM,
 // peer access enabled) instead of two hipMemcpyPeerAsync per source: each
 // small copy cost a blit launch of ~5 us on the owner's stream
+// With src_cnt set, the run lengths come from the sources' partition counts
+// in their own HBM (part_counts_kernel's words, read over xGMI) instead of a
+// host round trip per source: source s's run for this owner starts at
+// sum(cnt_s[q], q < owner) in its partitioned arrays and lands at
+// sum(cnt_s'[owner], s' < s) here; *d_total = the owner's pair count (the
+// index build's n, on the device).
 struct GatherArgs {
   const uint64_t* src_k[PART_MAX_WORLD];
   const uint64_t* src_v[PART_MAX_WORLD];
+  const uint64_t* src_cnt[PART_MAX_WORLD];  // nullable: dst_off / src_k / src_v are final (host counts)
   uint64_t dst_off[PART_MAX_WORLD + 1];
   uint64_t* dst_k;
   uint64_t* dst_v;
+  uint64_t* d_total;
+  uint32_t owner, nsrc;
 };
 __global__ __launch_bounds__(256) void gather_runs_kernel(GatherArgs a) {
   const uint32_t s = blockIdx.y;
-  const uint64_t o = a.dst_off[s], n = a.dst_off[s + 1] - o;
-  const uint64_t* __restrict__ sk = a.src_k[s];
-  const uint64_t* __restrict__ sv = a.src_v[s];
+  __shared__ uint64_t s_run[3];  // source offset, length, destination offset
+  if (a.src_cnt[0]) {
+    if (threadIdx.x == 0) {
+      uint64_t off = 0, dst = 0;
+      for (uint32_t q = 0; q < a.owner; q++) off += a.src_cnt[s][q];
+      for (uint32_t t = 0; t < s; t++) dst += a.src_cnt[t][a.owner];
+      const uint64_t len = a.src_cnt[s][a.owner];
+      s_run[0] = off;
+      s_run[1] = len;
+      s_run[2] = dst;
+      if (blockIdx.x == 0 && s + 1 == a.nsrc) *a.d_total = dst + len;
+    }
+    __syncthreads();
+  }
+  const bool dev = a.src_cnt[0] != nullptr;
+  const uint64_t o = dev ? s_run[2] : a.dst_off[s], n = dev ? s_run[1] : a.dst_off[s + 1] - o;
+  const uint64_t* __restrict__ sk = a.src_k[s] + (dev ? s_run[0] : 0);
+  const uint64_t* __restrict__ sv = a.src_v[s] + (dev ? s_run[0] : 0);
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
     a.dst_k[o + j] = sk[j];
     a.dst_v[o + j] = sv[j];

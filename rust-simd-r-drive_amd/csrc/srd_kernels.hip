@@ -744,18 +744,23 @@ __global__ __launch_bounds__(256) void link2_kernel(ScanArgs a) {
 constexpr int scan_nw(int V) { return V == 20 ? 10 : V == 21 ? 12 : V == 23 ? 8 : 16; }
 constexpr int scan_bpc(int V) { return V == 20 || V == 21 || V == 23 ? 2 : 1; }
 constexpr int scan_wpe(int V) { return (scan_nw(V) * scan_bpc(V)) / 4; }
-constexpr bool scan_rot(int V) { return V >= 20 && V <= 24; }
+// 25: the rotated tables alone (the product's global loads, not 20-24's
+// buffer loads); 26: the product with the record stores' descriptors made
+// uniform (readfirstlane: no waterfall loop, no f64 min) as 20-25 have them.
+constexpr bool scan_rot(int V) { return V >= 20 && V <= 25; }
 
 template <bool FULL, bool WIDE, int V = 0>
 __global__ __launch_bounds__(scan_nw(V) * 64) __attribute__((amdgpu_waves_per_eu(scan_wpe(V), scan_wpe(V))))
 void scan_kernel(ScanArgs a) {
   constexpr int NW = scan_nw(V);
   constexpr bool ROT = scan_rot(V);
+  constexpr bool BUFLD = ROT && V != 25;       // tile loads as buffer loads (SGPR base, one lane offset)
+  constexpr bool UNISTORE = ROT || V == 26;    // uniform record-store descriptors
   constexpr bool F1 = (V == 1 || V == 2) ? !kFlag1 : kFlag1;
   constexpr bool F1_AFTER = V == 2;  // F1's staging + test after the CRC, at priority 2
-  constexpr bool CRC2 = V == 3;
+  // 3 = the line CRC as two 32-byte chains (crc_line2), 5 / 6 / 10 = each
+  // level's 16 lookups issued together (crc_line4_wide): line_crc below
   constexpr bool RING2 = V == 4 || V == 5 || V == 20 || V == 21 || V == 23 || V == 24;  // a 2-deep register ring (one tile in flight), 16 VGPRs fewer
-  constexpr bool WIDE16 = V == 5 || V == 6;  // crc_line4_wide: each level's 16 lookups issued together
   // timing-only ablations (wrong results; SRD_DEBUG_API's scan-only calls):
   // 7 = the ring's loads alone (each tile XOR-folded), 8 = the whole tile
   // body on two L1/L2-resident tiles per block (no HBM traffic)
@@ -764,7 +769,6 @@ void scan_kernel(ScanArgs a) {
   // per-tile LDS store by lane 63; the f == 0 window takes them from there),
   // 10 = 9 with the 16-wide CRC levels
   constexpr bool SCARRY = V == 9 || V == 10;
-  constexpr bool WIDE16B = V == 10;
   // timing-only ablations (results not checked): 11 = coalesced tile loads
   // (lane l, load j reads 16 B at 1024 j + 16 l), 12 = 11 memory-only
   constexpr bool COAL = V == 11 || V == 12;
@@ -878,7 +882,7 @@ void scan_kernel(ScanArgs a) {
   // lane weights, suffix XOR, filter) is one basic block.
   const uint64_t nohbm_k = (a.part.s_lo + part_block_start(a.part, blockIdx.x)) * SPAN_TILES;
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
-    if constexpr (ROT) {
+    if constexpr (BUFLD) {
       // buffer loads over the tile (base in SGPRs, one 32-bit lane offset):
       // no 64-bit lane address pair held across the loop (the occupancy
       // variants' VGPR budget)
@@ -1388,7 +1392,7 @@ void scan_kernel(ScanArgs a) {
       const bool wr = fl && ((rvalid >> lane) & 1);
       uint64_t rb = w * a.wcap + flushed;  // lane 0's record
       uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
-      if constexpr (ROT) {
+      if constexpr (UNISTORE) {
         // uniform by construction, but the compiler's divergence analysis
         // loses it: as VGPRs the three descriptors cost a waterfall loop
         // around each store (and registers the occupancy variants lack)

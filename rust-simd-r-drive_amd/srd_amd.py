@@ -63,6 +63,7 @@ EXPORTS = [
     "srd_iter_entries_device", "srd_estimate_compaction_savings_device", "srd_compact_device",
     "srd_shard_cuts", "srd_validate_index_multi", "srd_ctx_stage_info", "srd_index_hash_device",
     "srd_validate_index_multi_device", "srd_ctx_multi_summary", "srd_ctx_scan_list", "srd_ctx_set_timing_every",
+    "srd_stream_probe_device", "srd_ctx_multi_shard_ms",
 ]
 
 
@@ -158,6 +159,8 @@ def lib():
         L.srd_validate_index_multi_device.argtypes = [C.POINTER(vp), u32, C.POINTER(vp), vp, vp, u32,
                                                       C.POINTER(DeviceResult), C.POINTER(MultiSummary)]
         L.srd_ctx_multi_summary.argtypes = [vp, C.POINTER(MultiSummary)]
+        L.srd_ctx_multi_shard_ms.argtypes = [vp, C.POINTER(C.c_double), i32]
+        L.srd_stream_probe_device.argtypes = [vp, vp, u64, i32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         for f in EXPORTS:
             if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
                          "srd_padded_size", "srd_index_table_bytes"):
@@ -688,6 +691,15 @@ def _blob(parts):
         offs[1:] = np.cumsum(lens)[:-1]
     buf = np.frombuffer(b"".join(parts) or b"\x00", np.uint8)
     return buf, offs, lens
+
+
+def stream_probe_device(ptr: int, nbytes: int, reps: int = 8, ctx: Context | None = None):
+    """srd_stream_probe_device: (best_ms, median_ms) of the scan-geometry
+    streaming read of the first nbytes // 4096 tiles at device pointer ptr."""
+    ctx = ctx or default_ctx()
+    b, m = C.c_double(), C.c_double()
+    _check(lib().srd_stream_probe_device(ctx.h, C.c_void_p(ptr), nbytes, reps, C.byref(b), C.byref(m)))
+    return b.value, m.value
 
 
 def batch_layout(tail: int, keys, payloads, allow_null: bool = False):
