@@ -1246,7 +1246,8 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     }
 #endif
     // every record's node test, parent and claim (slot space), one block per scan wave
-    link2_kernel<<<(unsigned)total_waves, 256, 0, c->stream>>>(a);
+    link2_kernel<<<(unsigned)((total_waves + LINK_WPB - 1) / LINK_WPB), 256 * LINK_WPB, 0, c->stream>>>(
+        a, (uint32_t)total_waves);
     KCHK(c, "link2_kernel");
     // ---- shape check, chain, finalize, index; retried on device with more
     //      prune rounds when false candidates chained onto each other ----

@@ -737,13 +737,26 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   // whole file only: the start tail is itself a root tail (prev 0): one
   // entry spans [0, t) (recover_valid_chain's walk ends at once)
   const uint64_t top = a.counters[1];
-  const bool troot = a.coff && top >= 21 && ld_u64_unaligned(a.file, top - 12) == 0;
+  // (the prev field at top - 12 by two aligned dword pairs: the buffer is
+  // padded past file_len)
+  auto ld_prev_at = [&](uint64_t o) -> uint64_t {
+    const uint32_t* q = (const uint32_t*)(a.file + (o & ~3ull));
+    const uint32_t sh = (uint32_t)(o & 3) * 8, w0 = q[0], w1 = q[1], w2 = q[2];
+    return (uint64_t)alignb(w1, w0, sh) | ((uint64_t)alignb(w2, w1, sh) << 32);
+  };
+  const bool troot = a.coff && top >= 21 && ld_prev_at(top - 12) == 0;
   uint64_t root_t = troot ? top : FUSED ? 0 : pl->root_t;
   if (a.counters[2]) st |= ST_OVERFLOW;
-  const uint64_t start = incomplete ? NO_NODE : start_node(a);
-  if (start == NO_NODE) st |= ST_NOSTART;
+  // the start node: !FUSED now; FUSED lazily -- it can only be the last
+  // record (slot s1 - 1), so the shape check tests g == s1 - 1 and reads
+  // that record's c_m only there, and the last block settles ST_NOSTART /
+  // ST_OVERFLOW with the plan (the other blocks' work is discarded then)
+  const uint64_t s1 = a.Kp[1];
+  const uint64_t start = FUSED ? NO_NODE : incomplete ? NO_NODE : start_node(a);
+  if (!FUSED && start == NO_NODE) st |= ST_NOSTART;
   if (!FUSED && pl->nroot != 1) st |= ST_ROOTS;
-  __syncthreads();  // this block has read pl->status / nroot / root_t before block 0 rewrites them
+  if (FUSED) st = 0;  // (settled by the last block)
+  if (!FUSED) __syncthreads();  // this block has read pl->status / nroot / root_t before block 0 rewrites them
   const uint32_t nbk = 1u << log2_nbk;
   // the plan: !FUSED block 0 now; FUSED the last block, once the look-back
   // has every block's count (or now, when the counters alone decide)
@@ -759,14 +772,15 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       pl->root_t = top;
       pl->chain_core = 0;
     } else {
-      pl->start = start;
+      if (!FUSED) pl->start = start;
       pl->status = s2;
       pl->chain_core = tot;
       pl->n_chain = s2 ? 0 : a.coff + tot;
     }
   };
   const bool plan_block = FUSED ? blockIdx.x + 1 == gridDim.x : blockIdx.x == 0;
-  if ((!FUSED || st || troot) && plan_block && threadIdx.x == 0) write_plan(st, total);
+  if (!FUSED && plan_block && threadIdx.x == 0) write_plan(st, total);
+  if (FUSED && troot && plan_block && threadIdx.x == 0) write_plan(0, 0);
   if (st && !troot) return;
   // FUSED: the shape check of this block's records (check_kernel, round 0),
   // then the look-back; per-wave core counts in LDS
@@ -833,7 +847,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
             if (!in[r]) break;
             const int64_t p = par[r];
             const bool linked = (cg[r] & ~0xffffffffull) == tag;
-            const bool core = g[r] == start || (linked && (p >= 0 || p == PAR_ROOT));  // is_core(g)
+            // g == the start node: the last record, at the start tail's metadata
+            const bool is_st = s1 && g[r] == s1 - 1 && top >= 21 && a.c_m[g[r]] == top - 20;
+            const bool core = is_st || (linked && (p >= 0 || p == PAR_ROOT));  // is_core(g)
             GST(a.flag[g[r]], (uint8_t)core);
             if (!core) continue;
             cnt++;
@@ -842,8 +858,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
               nr++;
               const u32x4 r0 = a.c_rec[2 * g[r]];
               s_root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);  // (any one: nroot != 1 fails the call)
-            } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
-              fail = true;  // dangling
+            } else if (p < 0 || !(((uint64_t)p == s1 - 1 && a.c_m[p] == top - 20) ||
+                                  (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
+              fail = true;  // dangling (a parent that is the start node is core: never here in practice)
             } else if (cp[r] != claim_word(a.gen, g[r])) {
               fail = true;  // branch
             }
@@ -859,6 +876,19 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       if (__ballot(fail) && lane == 0) s_fail = 1;
       __syncthreads();
       GLUE_STAMP(1);
+      // the LDS tables and the bucket counts now: wave 0's look-back below
+      // overlaps the other waves' stores (one barrier for both)
+      for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
+      tab[ti] = r_tab;
+      lt.m16k[ti] = r_m16k;
+      lt.m32k[ti] = r_m32k;
+#pragma unroll
+      for (int j = 0; j < 4; j++) lt.invpow[ti + 1024 * j] = r_inv[j];
+      if (ti == 0) lt.invpow[4096] = r_inv_last;
+      if (ti < 64) {
+        lt.winit[ti] = r_winit;
+        lt.zero_crc[ti] = r_zc;
+      }
       uint32_t btot = 0;
       for (uint32_t v = 0; v < a.wpb; v++) btot += s_vcnt[v];
       const uint32_t ltag = lb_tag(a.gen);
@@ -879,8 +909,13 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
           s_lb[0] = pc;
           s_lb[1] = pc + btot;
           s_lbok = ok;
-          if (plan_block)  // every block's count, failure and root links are in the prefix
-            write_plan((ok ? 0u : ST_LOOKBACK) | (f2 ? ST_SHAPE : 0u) | (n2 != 1 ? ST_ROOTS : 0u), pc + btot);
+          if (plan_block) {  // every block's count, failure and root links are in the prefix
+            const uint64_t stn = incomplete ? NO_NODE : start_node(a);
+            pl->start = stn;
+            write_plan((ok ? 0u : ST_LOOKBACK) | (f2 ? ST_SHAPE : 0u) | (n2 != 1 ? ST_ROOTS : 0u) |
+                           (a.counters[2] ? ST_OVERFLOW : 0u) | (stn == NO_NODE ? ST_NOSTART : 0u),
+                       pc + btot);
+          }
         }
       }
       __syncthreads();
@@ -891,18 +926,20 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       root_t = s_root_t;
     }
   }
-  for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
-  tab[ti] = r_tab;
-  lt.m16k[ti] = r_m16k;
-  lt.m32k[ti] = r_m32k;
+  if (!FUSED || troot) {  // (FUSED: stored beside the look-back above)
+    for (uint32_t k = threadIdx.x; k < nbk; k += blockDim.x) hist[k] = 0;
+    tab[ti] = r_tab;
+    lt.m16k[ti] = r_m16k;
+    lt.m32k[ti] = r_m32k;
 #pragma unroll
-  for (int j = 0; j < 4; j++) lt.invpow[ti + 1024 * j] = r_inv[j];
-  if (ti == 0) lt.invpow[4096] = r_inv_last;
-  if (ti < 64) {
-    lt.winit[ti] = r_winit;
-    lt.zero_crc[ti] = r_zc;
+    for (int j = 0; j < 4; j++) lt.invpow[ti + 1024 * j] = r_inv[j];
+    if (ti == 0) lt.invpow[4096] = r_inv_last;
+    if (ti < 64) {
+      lt.winit[ti] = r_winit;
+      lt.zero_crc[ti] = r_zc;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   GLUE_STAMP(3);
   // the root entry (whole file: chain entry 0, no candidate record); its
   // CRC's slow path, if any, runs after the candidates
@@ -1247,6 +1284,18 @@ __global__ __launch_bounds__(256) void idx_hist_scatter_kernel(IdxArgs a) {
 // f.n_slow == nullptr: none) are spread over all the dedup blocks' waves --
 // balanced over the whole grid instead of queued behind their own
 // finalize block (C3: ~340K entries of 5-256 tiles)
+// The outcome words (PUB_WORDS, each (seq << 32) | value) to pinned host
+// memory with system-scope stores; the host accepts them once all carry this
+// call's seq
+__device__ __forceinline__ void publish_outcome(const IdxArgs& a, const Plan* pl, uint64_t n, uint64_t nl_total) {
+  const uint64_t tag = (uint64_t)a.pub_seq << 32;
+  const uint32_t fl = (pl->status & 0xffu) | (a.alias && nl_total == 0 ? 0x100u : 0u) | (pl->idx_overflow ? 0x200u : 0u);
+  const uint64_t w[PUB_WORDS] = {tag | fl, tag | (uint32_t)pl->n_chain, tag | (uint32_t)(n - nl_total),
+                                 tag | (uint32_t)pl->n_bad, tag | (uint32_t)pl->K, tag | (uint32_t)pl->top_gap};
+#pragma unroll
+  for (int i = 0; i < PUB_WORDS; i++) __hip_atomic_store(a.pub + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a, FinArgs f) {
   __shared__ unsigned long long keys[IDX_TSLOTS];
   __shared__ uint32_t vals[IDX_TSLOTS];
@@ -1335,20 +1384,8 @@ __global__ __launch_bounds__(256) void idx_emit_kernel(IdxArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.plan->n_index = n - nl_total;
     a.plan->idx_alias = a.alias && nl_total == 0;
-    if (a.pub) {
-      // every value < 2^31 (the dense capacity bounds K and the chain); one
-      // 8-byte system-scope store each: the host accepts the words once all
-      // carry this call's seq
-      const Plan* pl = a.plan;
-      const uint64_t tag = (uint64_t)a.pub_seq << 32;
-      const uint32_t fl = (pl->status & 0xffu) | (a.alias && nl_total == 0 ? 0x100u : 0u) |
-                          (pl->idx_overflow ? 0x200u : 0u);
-      const uint64_t w[PUB_WORDS] = {tag | fl, tag | (uint32_t)pl->n_chain, tag | (uint32_t)(n - nl_total),
-                                     tag | (uint32_t)pl->n_bad, tag | (uint32_t)pl->K, tag | (uint32_t)pl->top_gap};
-#pragma unroll
-      for (int i = 0; i < PUB_WORDS; i++)
-        __hip_atomic_store(a.pub + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    // (every value < 2^31: the dense capacity bounds K and the chain)
+    if (a.pub) publish_outcome(a, a.plan, n, nl_total);
   }
   // every entry the latest of its key (a store without overwrites): the
   // index is the chain's (key_hash, packed) arrays chain_finalize wrote

@@ -727,10 +727,14 @@ __device__ void link_record(const ScanArgs& a, uint64_t w, uint64_t r) {
 // block's: the early blocks' work hid, but the last block's ~4 K (C2) to
 // ~40 K (C3) records in one block sat on the scan's critical path, and the
 // scan ran 6 % (C2) to 11 % (C3) longer for a 22 us kernel saved.)
-__global__ __launch_bounds__(256) void link2_kernel(ScanArgs a) {
-  const uint64_t w = blockIdx.x;
+// LINK_WPB scan waves per block (256 threads each; 2: 20.7 -> 24.0 us at C2,
+// profiles/r05/kernel_stats_r5k.csv)
+constexpr uint32_t LINK_WPB = 1;
+__global__ __launch_bounds__(256 * LINK_WPB) void link2_kernel(ScanArgs a, uint32_t n_waves) {
+  const uint64_t w = (uint64_t)blockIdx.x * LINK_WPB + threadIdx.x / 256;
+  if (w >= n_waves) return;
   const uint64_t nrec = min(a.wave_total[w] & ~(1ull << 63), a.wcap);  // records past wcap: ST_OVERFLOW
-  for (uint64_t r = threadIdx.x; r < nrec; r += blockDim.x) link_record(a, w, r);
+  for (uint64_t r = threadIdx.x % 256; r < nrec; r += 256) link_record(a, w, r);
 }
 
 // The scan's geometry per variant (host and device): waves per block and
