@@ -668,7 +668,13 @@ __device__ void link_record(const ScanArgs& a, uint64_t w, uint64_t r) {
     hp = wt > 0 && wt <= a.wcap;  // an overflowed wave fails the pass anyway (ST_OVERFLOW)
     gprev = (w - 1) * a.wcap + (hp ? wt - 1 : 0);
   }
-  const uint64_t m = a.c_m[gi], mprev = hp ? a.c_m[gprev] : 0;
+  // the record two back too (the same cache line, beside the others): C2's
+  // false candidates sit one byte past a real record's metadata (a CRC whose
+  // low byte is 0), so the real child of that record finds its parent there
+  // instead of by a dependent search (~1/256 of the records; each one was
+  // a whole block's critical path)
+  const bool hp2 = r >= 2;
+  const uint64_t m = a.c_m[gi], mprev = hp ? a.c_m[gprev] : 0, mprev2 = hp2 ? a.c_m[gi - 2] : 0;
   const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
   const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
   bool node = true, tomb = false;
@@ -682,7 +688,7 @@ __device__ void link_record(const ScanArgs& a, uint64_t w, uint64_t r) {
   const uint64_t mp = p - 20;  // p >= 20 for nodes
   const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // span s holds m in [16 KiB s - 14, +16 KiB)
   // in a store without garbage the parent is the previous record: one load
-  int64_t par = hp && mprev == mp ? (int64_t)gprev : PAR_MISS;
+  int64_t par = hp && mprev == mp ? (int64_t)gprev : hp2 && mprev2 == mp ? (int64_t)(gi - 2) : PAR_MISS;
   // Otherwise a record at mp needs mp's prev field pp = u64 at p - 12 with
   // 20 <= pp < mp (every record is a strong node, data_store.rs:404-470).
   // One 8-byte file read settles most misses here: a false candidate's p is
