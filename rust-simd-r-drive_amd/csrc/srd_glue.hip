@@ -400,7 +400,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
 // builds the histogram, claims the bucket ranges and scatters its chain
 // positions itself)
 constexpr int IDX_HBLOCKS = 256;  // histogram / scatter blocks of the stand-alone build
-constexpr int IDX_TSLOTS = 4096;     // LDS open-addressing slots per bucket block (max)
 constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
 // the host picks the fewest buckets with <= IDX_BUCKET_AVG expected entries
 // each (fewer buckets, fewer range claims; a bucket of Poisson(1280) stays far
@@ -1296,16 +1295,22 @@ __device__ __forceinline__ void publish_outcome(const IdxArgs& a, const Plan* pl
   for (int i = 0; i < PUB_WORDS; i++) __hip_atomic_store(a.pub + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a, FinArgs f) {
-  __shared__ unsigned long long keys[IDX_TSLOTS];
-  __shared__ uint32_t vals[IDX_TSLOTS];
+// The table is sized for 4 blocks per CU (36 KiB of LDS; 512 threads each):
+// C2's 1024 buckets then run in one round instead of two.  DD_SLOTS = 1.5 x
+// IDX_TCAP, so any bucket that fits its capacity fits the table (load <= 2/3;
+// with the bucket count's average fill of 640-1280 entries, <= ~0.45)
+constexpr int DD_SLOTS = 3 * IDX_TCAP / 2;
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void idx_dedup_kernel(IdxArgs a, FinArgs f) {
+  __shared__ unsigned long long dd_lds[DD_SLOTS + DD_SLOTS / 2];
+  unsigned long long* const keys = dd_lds;
+  uint32_t* const vals = (uint32_t*)(dd_lds + DD_SLOTS);
   __shared__ uint32_t special;
   if (f.n_slow) {
     const unsigned long long ns = *f.n_slow;
     constexpr uint32_t NW = 512 / 64;
     if ((uint64_t)blockIdx.x * NW < ns) {
-      static_assert(sizeof(SlowLds) <= sizeof(keys), "the slow path's tables in the hash table's LDS");
-      SlowLds& L = *reinterpret_cast<SlowLds*>(keys);  // before the table's own use
+      static_assert(sizeof(SlowLds) <= sizeof(dd_lds), "the slow path's tables in the hash table's LDS");
+      SlowLds& L = *reinterpret_cast<SlowLds*>(dd_lds);  // before the table's own use
       load_slow_lds(L);
       __syncthreads();
       for (uint64_t q = (uint64_t)blockIdx.x * NW + (threadIdx.x >> 6); q < ns; q += (uint64_t)gridDim.x * NW)
@@ -1334,7 +1339,9 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a, FinArgs f) {
     rec[r] = a.srec[i < hi ? i : lo];
   }
   uint32_t slots = 64;
-  while (slots < 2 * (hi - lo)) slots <<= 1;  // load <= 1/2
+  while (slots < 2 * (hi - lo) && slots < 2048) slots <<= 1;  // load <= 1/2 up to 1024 entries
+  const bool pw2 = slots >= 2 * (hi - lo);  // else DD_SLOTS, the slot by a multiply-high
+  if (!pw2) slots = DD_SLOTS;
   const uint32_t M = slots - 1;
   for (uint32_t i = threadIdx.x; i < slots; i += blockDim.x) { keys[i] = IDX_EMPTY; vals[i] = 0; }
   if (threadIdx.x == 0) special = 0;
@@ -1345,11 +1352,12 @@ __global__ __launch_bounds__(512) void idx_dedup_kernel(IdxArgs a, FinArgs f) {
     const uint64_t key = rec[r][0];
     const uint32_t v = (uint32_t)rec[r][1] + 1;
     if (key == IDX_EMPTY) { atomicMax(&special, v); continue; }
-    uint32_t s = (uint32_t)xxh3_64_u64(key) & M;
+    const uint32_t h = (uint32_t)xxh3_64_u64(key);
+    uint32_t s = pw2 ? h & M : (uint32_t)(((uint64_t)h * DD_SLOTS) >> 32);
     while (true) {
       const unsigned long long old = atomicCAS(&keys[s], (unsigned long long)IDX_EMPTY, (unsigned long long)key);
       if (old == IDX_EMPTY || old == key) { atomicMax(&vals[s], v); break; }
-      s = (s + 1) & M;
+      s = s == M ? 0u : s + 1;
     }
     slot[r] = s;
   }
