@@ -411,6 +411,21 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
   } else if (a.variant == 26) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 26>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 26>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 32) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 32>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 32>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 31) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 31>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 31>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 30) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 30>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 30>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 27) {
+    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 27>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 28) {
+    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 28>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 29) {
+    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 29>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 22) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 22>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 22>, grid, block, 0, s, e0, e1, 0, a);

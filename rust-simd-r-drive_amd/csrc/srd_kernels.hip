@@ -602,6 +602,79 @@ __device__ __forceinline__ void load_rot_lds(ScanLdsR<NW>& lds) {
   __syncthreads();
 }
 
+// ---- the rotated last steps (scan_kernel V 30) ----
+// ScanLds's 12 last-step tables are unreplicated: their 12 lookups per line
+// make ~53 bank-conflict cycles of the tile's ~271 LDS cycles.  The rotation
+// of ScanLdsR applies to them as well (a last step is a slice-by-4 step over
+// shifted tables), at 8 replicas per table: 3 chains x 32 KiB.  Two 64 KiB
+// row arrays with 256-byte rows hold all rotated tables (the v_perm address:
+// byte 1 = the state byte = the row, byte 0 = Rr's word offset, + 128 for
+// words 32-63): x = T (words 0-31) and chain 2's last tables (32-63), y =
+// chain 0's (0-31) and chain 1's (32-63); the lane-weight nibble tables keep
+// ScanLds's layout.  One 16-wave block per CU as the product (146 KiB).
+template <int NW>
+struct alignas(4096) ScanLdsR3 {
+  uint32_t x[256 * 64];
+  uint32_t y[256 * 64];
+  uint32_t nib[8 * 16 * 32];  // 2 KiB-aligned (lane_weight_or)
+  uint32_t win[NW][24];
+  uint64_t s_root[NW], s_ovf[NW];
+  uint32_t s_last;
+};
+template <int NW>
+__device__ __forceinline__ void load_rot3_lds(ScanLdsR3<NW>& lds) {
+  static_assert(NW * 64 == 1024, "one word of each table per thread");
+  const uint32_t u = threadIdx.x;  // table word u: t = u >> 8, b = u & 255
+  const uint32_t tv = g_tabs.tab[u >> 8][u & 255];
+  const u32x4 nv = ((const u32x4*)g_tabs.nib)[u];
+  uint32_t lv[3];
+#pragma unroll
+  for (int q = 0; q < 3; q++) lv[q] = g_tabs.last[q][u >> 8][u & 255];  // chain q, byte position u >> 8
+  const uint32_t t = u >> 8, b = u & 255;
+  // T_t[b] -> row b word 8 t + r; last_q[i][b] (byte i) -> word 8 (3 - i) + r (+ 32 for chain 1 / 2)
+  u32x4* tr = (u32x4*)(lds.x + b * 64 + 8 * t);
+  tr[0] = u32x4{tv, tv, tv, tv};
+  tr[1] = u32x4{tv, tv, tv, tv};
+  const uint32_t wl = 8 * (3 - t);
+  u32x4* l0 = (u32x4*)(lds.y + b * 64 + wl);
+  l0[0] = u32x4{lv[0], lv[0], lv[0], lv[0]};
+  l0[1] = u32x4{lv[0], lv[0], lv[0], lv[0]};
+  u32x4* l1 = (u32x4*)(lds.y + b * 64 + 32 + wl);
+  l1[0] = u32x4{lv[1], lv[1], lv[1], lv[1]};
+  l1[1] = u32x4{lv[1], lv[1], lv[1], lv[1]};
+  u32x4* l2 = (u32x4*)(lds.x + b * 64 + 32 + wl);
+  l2[0] = u32x4{lv[2], lv[2], lv[2], lv[2]};
+  l2[1] = u32x4{lv[2], lv[2], lv[2], lv[2]};
+  ((u32x4*)lds.nib)[u] = nv;
+  __syncthreads();
+}
+// crc_line4 with every lookup rotated (conflict-free): chains 0-2's last
+// steps through their rotated shifted tables (Rr + 128 per byte: words 32-63)
+template <class L>
+__device__ __forceinline__ uint32_t crc_line4_rot3(const uint32_t (&d)[16], const L& lds, uint32_t Rr,
+                                                   const uint32_t (&SL)[4]) {
+  uint32_t s[4] = {d[0], d[4], d[8], d[12]};
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t t0 = rot_lookup(lds.x, s[q], Rr, SL[0]), t1 = rot_lookup(lds.x, s[q], Rr, SL[1]);
+      const uint32_t t2 = rot_lookup(lds.x, s[q], Rr, SL[2]), t3 = rot_lookup(lds.x, s[q], Rr, SL[3]);
+      s[q] = xor3(xor3(t0, t1, d[4 * q + j + 1]), t2, t3);
+    }
+  }
+  const uint32_t Rh = Rr + 0x80808080u;  // words 32-63 of the rows
+  const uint32_t* base[4] = {lds.y, lds.y, lds.x, lds.x};
+  const uint32_t rr[4] = {Rr, Rh, Rh, Rr};
+  uint32_t v[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    v[q] = xor3(rot_lookup(base[q], s[q], rr[q], SL[0]), rot_lookup(base[q], s[q], rr[q], SL[1]),
+                rot_lookup(base[q], s[q], rr[q], SL[2])) ^
+           rot_lookup(base[q], s[q], rr[q], SL[3]);
+  return xor3(v[0], v[1], v[2]) ^ v[3];
+}
+
 // recover_valid_chain's outer loop (data_store.rs:388-479) walks the cursor t
 // down from file_len and skips every t whose metadata fails its first test,
 // entry_start < metadata_offset (:390-420; entry_start = prev + prepad(prev),
@@ -743,6 +816,59 @@ __global__ __launch_bounds__(256 * LINK_WPB) void link2_kernel(ScanArgs a, uint3
   for (uint64_t r = threadIdx.x % 256; r < nrec; r += 256) link_record(a, w, r);
 }
 
+// ---- coalesced nontemporal tile loads (scan_kernel V 31) ----
+// The scan's line-per-lane loads (lane l: 16 B at 64 l + 16 j) stream at
+// ~6.0-6.1 TB/s; loads whose every instruction reads 1 KiB contiguous, with
+// the nontemporal bit, at ~6.75 TB/s (tools/stream_map_probe.hip,
+// profiles/r05/stream_cpol_probe.txt; nt on the line-per-lane pattern: 3.6).
+// The load puts lane l = 16A + 4B + C on 16 B at 1024 j + 256 A + 64 C + 16 B
+// (quarter B of line 16 j + 4 A + C; each 16-lane row reads 256 contiguous
+// bytes), and two register <-> lane field swaps move line L to lane L,
+// quarter q to dwords 4q..4q+3: the register field with lane bits 4-5 by
+// v_permlane16/32_swap, then with lane bits 2-3 by DPP row shifts under bank
+// masks (bank = lane bits 2-3): 16 + 32 VALU per tile, no selects.
+__device__ __forceinline__ uint32_t coal_lane_off(int lane, int j) {
+  return 1024u * (uint32_t)j + 256u * ((uint32_t)lane >> 4) + 64u * ((uint32_t)lane & 3u) +
+         16u * (((uint32_t)lane >> 2) & 3u);
+}
+template <int RB, bool P32>
+__device__ __forceinline__ void coal_pswap(uint32_t (&d)[16]) {  // register bit RB <-> lane bit 4 (P32: 5)
+#pragma unroll
+  for (int r0 = 0; r0 < 4; r0++) {
+    if (r0 & RB) continue;
+    const int r1 = r0 | RB;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const auto w = P32 ? __builtin_amdgcn_permlane32_swap(d[4 * r0 + i], d[4 * r1 + i], false, false)
+                         : __builtin_amdgcn_permlane16_swap(d[4 * r0 + i], d[4 * r1 + i], false, false);
+      d[4 * r0 + i] = w[0];
+      d[4 * r1 + i] = w[1];
+    }
+  }
+}
+template <int S, int RB>
+__device__ __forceinline__ void coal_bswap(uint32_t (&d)[16]) {  // register bit RB <-> lane bit S (4, 8)
+  constexpr int SHL = 0x100 + S, SHR = 0x110 + S;
+  constexpr int HI = S == 4 ? 0xA : 0xC, LO = S == 4 ? 0x5 : 0x3;  // banks with / without lane bit S
+#pragma unroll
+  for (int r0 = 0; r0 < 4; r0++) {
+    if (r0 & RB) continue;
+    const int r1 = r0 | RB;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int a = (int)d[4 * r0 + i], b = (int)d[4 * r1 + i];
+      d[4 * r0 + i] = (uint32_t)__builtin_amdgcn_update_dpp(a, b, SHR, 0xF, HI, false);  // lanes with bit S <- b[l - S]
+      d[4 * r1 + i] = (uint32_t)__builtin_amdgcn_update_dpp(b, a, SHL, 0xF, LO, false);  // lanes without <- a[l + S]
+    }
+  }
+}
+__device__ __forceinline__ void coal_to_lines(uint32_t (&d)[16]) {
+  coal_pswap<1, false>(d);
+  coal_pswap<2, true>(d);
+  coal_bswap<4, 1>(d);
+  coal_bswap<8, 2>(d);
+}
+
 // The scan's geometry per variant (host and device): waves per block and
 // blocks per CU.  20 / 21: the rotated tables (ScanLdsR, 78 KiB) and a
 // 2-deep register ring, two blocks of 10 / 12 waves per CU = 5 / 6 waves per
@@ -764,13 +890,15 @@ __global__ __launch_bounds__(scan_nw(V) * 64) __attribute__((amdgpu_waves_per_eu
 void scan_kernel(ScanArgs a) {
   constexpr int NW = scan_nw(V);
   constexpr bool ROT = scan_rot(V);
+  constexpr bool ROT3 = V == 30;  // every lookup rotated, the product's geometry and loads
+  constexpr bool COALT = V == 31 || V == 32;  // (32: with the 2-deep ring)  // coalesced nontemporal tile loads + the in-register transpose
   constexpr bool BUFLD = ROT && V != 25;       // tile loads as buffer loads (SGPR base, one lane offset)
   constexpr bool UNISTORE = ROT || V == 26;    // uniform record-store descriptors
   constexpr bool F1 = (V == 1 || V == 2) ? !kFlag1 : kFlag1;
   constexpr bool F1_AFTER = V == 2;  // F1's staging + test after the CRC, at priority 2
   // 3 = the line CRC as two 32-byte chains (crc_line2), 5 / 6 / 10 = each
   // level's 16 lookups issued together (crc_line4_wide): line_crc below
-  constexpr bool RING2 = V == 4 || V == 5 || V == 20 || V == 21 || V == 23 || V == 24;  // a 2-deep register ring (one tile in flight), 16 VGPRs fewer
+  constexpr bool RING2 = V == 4 || V == 5 || V == 20 || V == 21 || V == 23 || V == 24 || V == 32;  // a 2-deep register ring (one tile in flight), 16 VGPRs fewer
   // timing-only ablations (wrong results; SRD_DEBUG_API's scan-only calls):
   // 7 = the ring's loads alone (each tile XOR-folded), 8 = the whole tile
   // body on two L1/L2-resident tiles per block (no HBM traffic)
@@ -789,7 +917,7 @@ void scan_kernel(ScanArgs a) {
   // tile instead of after every ring round)
   constexpr bool TILE_SP = V == 14 || RING2;
   uint32_t memonly_acc = 0;
-  using Lds = std::conditional_t<ROT, ScanLdsR<NW>, ScanLds>;
+  using Lds = std::conditional_t<ROT, ScanLdsR<NW>, std::conditional_t<ROT3, ScanLdsR3<NW>, ScanLds>>;
   static_assert(ROT || NW == SCAN_WAVES_V2, "ScanLds holds 16 windows");
   __shared__ Lds lds;
   // lanes of the record queue rq: with F1 its lane 63 is scratch
@@ -803,6 +931,7 @@ void scan_kernel(ScanArgs a) {
   if (threadIdx.x == 0) g_wave_stamp[8192 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
   if constexpr (ROT) load_rot_lds(lds);
+  else if constexpr (ROT3) load_rot3_lds(lds);
   else load_crc_lds(lds);
 #ifdef SRD_WAVE_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < 256) g_wave_stamp[8192 + 256 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -814,7 +943,7 @@ void scan_kernel(ScanArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t R[4];
   uint32_t Rr = 0, SL[4] = {0, 0, 0, 0};
-  if constexpr (ROT) {
+  if constexpr (ROT || ROT3) {
     rot_lane_consts(Rr, SL, lane);
   } else {
 #pragma unroll
@@ -829,6 +958,7 @@ void scan_kernel(ScanArgs a) {
   // the line CRC and its lane weight (the variant's table layout)
   auto line_crc = [&](const uint32_t (&x)[16]) -> uint32_t {
     if constexpr (ROT) return crc_line4_rot(x, lds, Rr, SL);
+    else if constexpr (ROT3) return crc_line4_rot3(x, lds, Rr, SL);
     else if constexpr (V == 3) return crc_line2(x, lds, R);
     else if constexpr (V == 5 || V == 6 || V == 10) return crc_line4_wide(x, lds, R);
     else return crc_line4(x, lds, R);
@@ -905,6 +1035,15 @@ void scan_kernel(ScanArgs a) {
       }
       return;
     }
+    if constexpr (COALT) {
+      const uint8_t* tb = file + k * (uint64_t)TILE;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(tb + coal_lane_off(lane, j)));
+        o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
+      }
+      return;
+    }
     const u32x4* q = (const u32x4*)(file + (NOHBM ? nohbm_k + (k & 1) : k) * (uint64_t)TILE + (COAL ? 16ull : 64ull) * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -927,6 +1066,9 @@ void scan_kernel(ScanArgs a) {
   uint64_t rootmax = 0;
   // the previous tile's SX_63 (F1; uniform -- without F1 the window's win[22])
   uint32_t hxp_s = 0;
+  uint32_t probe_s[4] = {0, 0, 0, 0}, probe_v[4] = {0, 0, 0, 0};  // V 27-29 (issue-cost probes)
+  const uint32_t probe_la = lds_off(win) + 4u * ((uint32_t)lane & 15);
+  (void)probe_s; (void)probe_v; (void)probe_la;
   uint32_t carry_s[4] = {0, 0, 0, 0};  // SCARRY: the previous tile's line-63 tail (uniform)
   // lane-constant LDS addresses of the straight-line window test: lane b
   // reads dwords (b + 2) / 4 .. + 5 and the tombstone dword (b + 1) / 4
@@ -979,6 +1121,7 @@ void scan_kernel(ScanArgs a) {
       return;
     }
     constexpr bool tail_tile = decltype(tail_c)::value;
+    if constexpr (COALT) coal_to_lines(d);  // lane l <- line l
     const uint64_t B = k * (uint64_t)TILE;
     const uint64_t span = k / SPAN_TILES;
     // bytes left in the file from B (uniform, 32-bit: every in-tile test below
@@ -1107,6 +1250,30 @@ void scan_kernel(ScanArgs a) {
     const uint32_t c = line_crc(d);
     __builtin_amdgcn_s_setprio(0);
     const uint32_t hx = half_suffix_xor(lane_wt(c), lane);
+    // issue-cost probes (timing-only, results unchanged): 27 = +16 independent
+    // SALU per tile, 28 = +16 independent VALU, 29 = +8 LDS reads (the tile
+    // values' slot, results discarded by an XOR into a dead register)
+    if constexpr (V == 27) {
+      asm volatile(
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1"
+          : "+s"(probe_s[0]), "+s"(probe_s[1]), "+s"(probe_s[2]), "+s"(probe_s[3]));
+    } else if constexpr (V == 28) {
+      asm volatile(
+          "v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3\n\t"
+          "v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3\n\t"
+          "v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3\n\t"
+          "v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3"
+          : "+v"(probe_v[0]), "+v"(probe_v[1]), "+v"(probe_v[2]), "+v"(probe_v[3]));
+    } else if constexpr (V == 29) {
+      uint32_t x[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) x[i] = lds_ld(probe_la + 4u * (uint32_t)i);
+      probe_v[0] ^= x[0] ^ x[1] ^ x[2] ^ x[3] ^ x[4] ^ x[5] ^ x[6] ^ x[7];
+      asm volatile("" ::"v"(probe_v[0]));
+    }
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
     // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
     // tiles.  Every store of this loop is an UNCONDITIONAL buffer store whose
@@ -1551,6 +1718,7 @@ void scan_kernel(ScanArgs a) {
   constexpr int QR = 4;
   uint64_t* s_wsum;  // the CRC tables are dead now
   if constexpr (ROT) s_wsum = (uint64_t*)lds.tn;
+  else if constexpr (ROT3) s_wsum = (uint64_t*)lds.x;
   else s_wsum = (uint64_t*)lds.tab;
   uint64_t* s_smax = s_wsum + NW;
   uint64_t* s_root = lds.s_root;
