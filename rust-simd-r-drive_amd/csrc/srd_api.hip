@@ -354,6 +354,9 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
     (void)hipEventRecord(e0, s);
     launch_scan<FULL>(g, a, s);
     (void)hipEventRecord(e1, s);
+  } else if (a.variant == SCAN_LINES) {  // line-per-lane tile loads (large stores: scan_variant_for)
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, SCAN_LINES>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, SCAN_LINES>, grid, block, 0, s, e0, e1, 0, a);
 #ifdef SRD_DEBUG_API
   } else if (a.variant == 1) {  // A/B variants (scan_kernel's V) inside one context
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 1>, grid, block, 0, s, e0, e1, 0, a);
@@ -411,6 +414,9 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
   } else if (a.variant == 26) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 26>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 26>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 33) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 33>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 33>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 32) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 32>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 32>, grid, block, 0, s, e0, e1, 0, a);
@@ -601,7 +607,7 @@ static void scan_weights(uint32_t (&wq)[16]) {
 }
 #ifdef SRD_DEBUG_API  // timing builds: A/B of scan variants inside one context (one workspace)
 extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
-  if (!c || v < 0 || v > 30) return SRD_ERR_ARG;
+  if (!c || v < 0 || v > 34) return SRD_ERR_ARG;
   c->scan_variant = (uint32_t)v;
   return 0;
 }
@@ -965,6 +971,19 @@ static int next_scan_events(Ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
   return 0;
 }
 
+// The scan's tile loads (scan_kernel): coalesced nontemporal loads + an
+// in-register transpose (V 0) for resident spans up to kCoalMax bytes, round
+// 4's line-per-lane loads (SCAN_LINES) above.  Measured in the same contexts
+// (profiles/r05/variant_ab_coal_*.txt): C2-shaped stores of 4.4 / 8.7 / 17.4
+// GB -7.5 / -6.2 / -5.5 % scan with the coalesced loads, 70 GB +4 %; C3-
+// shaped 4.3 GB -2.5 %, 18 GB +2.4 %, 72.5 GB +4.8 %.  The debug build's
+// srd_debug_set_scan_variant overrides the choice.
+constexpr uint64_t kCoalMax = 32ull << 30;
+static uint32_t scan_variant_for(const Ctx* c, uint64_t resident_bytes) {
+  if (c->scan_variant) return c->scan_variant;
+  return resident_bytes > kCoalMax ? (uint32_t)SCAN_LINES : 0u;
+}
+
 static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uint64_t* K, uint64_t* h) {
   const uint64_t n_tiles = (flen + TILE - 1) / TILE;
   const uint64_t n_spans = (n_tiles + SPAN_TILES - 1) / SPAN_TILES;
@@ -977,7 +996,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     // the scan writes every span's count; only the scan sentinel needs a zero
     HIPCHK(hipMemsetAsync(P<uint32_t>(c, B_SPAN_COUNT) + n_spans, 0, 4, c->stream));
     ScanArgs a{};
-    a.variant = c->scan_variant;
+    a.variant = scan_variant_for(c, flen);
     a.file = d_file;
     a.flen = flen;
     a.n_tiles = n_tiles;
@@ -1220,7 +1239,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     // per-tile / per-span arrays hold the resident range only: their base
     // pointers are shifted so kernels index them by absolute tile / span
     ScanArgs a{};
-    a.variant = c->scan_variant;
+    a.variant = scan_variant_for(c, flen - span_off);
     a.part = part;
     a.file = d_file;
     a.flen = flen;

@@ -877,6 +877,8 @@ __device__ __forceinline__ void coal_to_lines(uint32_t (&d)[16]) {
 // 23: the rotated tables, 2-deep ring, two 8-wave blocks per CU (4 waves
 // per SIMD, as 0: the geometry at equal occupancy); 24: the rotated tables
 // and the 2-deep ring in today's geometry.
+// line-per-lane tile loads (round 4's product): the scan of large stores
+constexpr int SCAN_LINES = 34;
 constexpr int scan_nw(int V) { return V == 20 ? 10 : V == 21 ? 12 : V == 23 ? 8 : 16; }
 constexpr int scan_bpc(int V) { return V == 20 || V == 21 || V == 23 ? 2 : 1; }
 constexpr int scan_wpe(int V) { return (scan_nw(V) * scan_bpc(V)) / 4; }
@@ -891,7 +893,11 @@ void scan_kernel(ScanArgs a) {
   constexpr int NW = scan_nw(V);
   constexpr bool ROT = scan_rot(V);
   constexpr bool ROT3 = V == 30;  // every lookup rotated, the product's geometry and loads
-  constexpr bool COALT = V == 31 || V == 32;  // (32: with the 2-deep ring)  // coalesced nontemporal tile loads + the in-register transpose
+  // the product (V 0) and 31-33 load tiles coalesced + nontemporal and
+  // transpose them in registers (coal_to_lines); SCAN_LINES (34) = round 4's
+  // line-per-lane loads, the product's for large stores (srd_api.hip
+  // scan_variant_for); 1-30 keep those loads (earlier experiments)
+  constexpr bool COALT = V == 0 || (V >= 31 && V <= 33);  // (32: with the 2-deep ring)  // coalesced nontemporal tile loads + the in-register transpose
   constexpr bool BUFLD = ROT && V != 25;       // tile loads as buffer loads (SGPR base, one lane offset)
   constexpr bool UNISTORE = ROT || V == 26;    // uniform record-store descriptors
   constexpr bool F1 = (V == 1 || V == 2) ? !kFlag1 : kFlag1;
@@ -1563,7 +1569,7 @@ void scan_kernel(ScanArgs a) {
     }
     {
       // (optimistic pass only; the full pass stores its records directly)
-      constexpr uint64_t FLUSH_AT = 40;
+      constexpr uint64_t FLUSH_AT = V == 33 ? 60 : 40;  // (33: larger record bursts)
       const uint64_t pend = wtotal + count - flushed;  // records pending (lanes [0, min(pend, 64)))
       const bool fl = pend >= FLUSH_AT || last;  // uniform
       const bool wr = fl && ((rvalid >> lane) & 1);

@@ -6,10 +6,12 @@
 // done on the bytes.
 //
 // Geometry = the scan's: one 16-wave block per CU, every wave a contiguous,
-// balanced range of 4 KiB tiles, lane l reading line l (64 B as four 16-byte
-// loads), a 3-deep register ring (two tiles in flight while one is folded).
-// Each tile is XOR-folded into one register so the loads stay live; one word
-// per wave is stored only if the fold equals a magic value (never, in effect).
+// balanced range of 4 KiB tiles, the scan's loads (four 16-byte nontemporal
+// loads per lane, every instruction 1 KiB contiguous: coal_lane_off), a
+// 3-deep register ring (two tiles in flight while one is folded).  Each tile
+// is XOR-folded into one register so the loads stay live (the fold is
+// order-free: no transpose); one word per wave is stored only if the fold
+// equals a magic value (never, in effect).
 #pragma once
 
 namespace srd {
@@ -21,10 +23,10 @@ __global__ __launch_bounds__(1024, 1) void stream_probe_kernel(const uint8_t* __
   const uint64_t tw = (uint64_t)gridDim.x * 16, w = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
   const uint64_t k0 = w * ntiles / tw, k1 = (w + 1) * ntiles / tw;
   if (k0 >= k1) return;
-  auto ld = [&](uint64_t k, u32x4 (&o)[4]) {  // the product scan's loads: 16 B global loads at 64 l + 16 j
-    const u32x4* q = (const u32x4*)(f + k * (uint64_t)TILE + 64ull * lane);
+  auto ld = [&](uint64_t k, u32x4 (&o)[4]) {  // the product scan's loads (scan_kernel's load_tile)
+    const uint8_t* tb = f + k * (uint64_t)TILE;
 #pragma unroll
-    for (int j = 0; j < 4; j++) o[j] = q[j];
+    for (int j = 0; j < 4; j++) o[j] = __builtin_nontemporal_load((const u32x4*)(tb + coal_lane_off(lane, j)));
   };
   u32x4 ring[D][4];
 #pragma unroll

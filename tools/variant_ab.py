@@ -3,7 +3,7 @@
 context runs every variant (srd_debug_set_scan_variant) in interleaved rounds,
 so the per-context spread of the scan rate cancels out.  Each
 variant's results are checked against the store's closed form every batch.
-usage: python tools/variant_ab.py [variants, default 0,1]   env: NCTX, ROUNDS, CONFIG=c2|c3|c2torn"""
+usage: python tools/variant_ab.py [variants, default 0,1]   env: NCTX, ROUNDS, CONFIG=c2|c3|c2torn, N (entries)"""
 import ctypes as C, json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["SRD_LIB_PATH"] = os.path.join(ROOT, "rust-simd-r-drive_amd", "build", "var", "lib_dbg.so")
@@ -23,11 +23,11 @@ ctxs = [S.Context(0) for _ in range(int(os.environ.get("NCTX", 3)))]
 for c in ctxs:
     c.set_timing(S.TIMING_SCAN)
 if cfg == "c3":
-    n = 10_000_000
+    n = int(os.environ.get("N", 10_000_000))  # N: a smaller / larger C3-shaped store
     lens = S.zipf_lens(n)
     seed = 0x5EED0004
 else:
-    n, lens, seed = 1 << 20, None, 0x5EED0001
+    n, lens, seed = int(os.environ.get("N", 1 << 20)), None, 0x5EED0001  # N: C2-shaped stores of other sizes
 size = S.synth_store_len(n, 4096, lens)
 flen = size + (7 if cfg == "c2torn" else 0)
 t = torch.empty(S.padded_size(flen), dtype=torch.uint8, device="cuda")
