@@ -897,7 +897,11 @@ void scan_kernel(ScanArgs a) {
   // transpose them in registers (coal_to_lines); SCAN_LINES (34) = round 4's
   // line-per-lane loads, the product's for large stores (srd_api.hip
   // scan_variant_for); 1-30 keep those loads (earlier experiments)
-  constexpr bool COALT = V == 0 || (V >= 31 && V <= 33);  // (32: with the 2-deep ring)  // coalesced nontemporal tile loads + the in-register transpose
+  constexpr bool COALT = V == 0 || (V >= 31 && V <= 33) || (V >= 35 && V <= 37);  // (32: with the 2-deep ring)
+  // timing-only store ablations (results wrong; the store instructions stay,
+  // their lanes out of range): 35 = no record stores, 36 = no tile-value
+  // stores, 37 = no {p, key_hash} half of c_rec (records of 24 B instead of 40)
+  constexpr bool NO_REC = V == 35, NO_TV = V == 36, NO_PK = V == 37;  // coalesced nontemporal tile loads + the in-register transpose
   constexpr bool BUFLD = ROT && V != 25;       // tile loads as buffer loads (SGPR base, one lane offset)
   constexpr bool UNISTORE = ROT || V == 26;    // uniform record-store descriptors
   constexpr bool F1 = (V == 1 || V == 2) ? !kFlag1 : kFlag1;
@@ -1563,7 +1567,7 @@ void scan_kernel(ScanArgs a) {
     if constexpr (MEMONLY || NOSTORE) return;
     const bool last = kf + nt == k1;  // uniform
     {
-      const uint32_t off = tg_pend && (uint32_t)lane - tg_lo < tg_hi - tg_lo ? 4u * lane : OOB_OFF;
+      const uint32_t off = !NO_TV && tg_pend && (uint32_t)lane - tg_lo < tg_hi - tg_lo ? 4u * lane : OOB_OFF;
       __builtin_amdgcn_raw_buffer_store_b32(tg_par ? tacc1 : tacc0, out_rsrc(a.tile + 4 * tg_base, 256), off, 0, 0);
       tg_pend = false;
     }
@@ -1572,7 +1576,7 @@ void scan_kernel(ScanArgs a) {
       constexpr uint64_t FLUSH_AT = V == 33 ? 60 : 40;  // (33: larger record bursts)
       const uint64_t pend = wtotal + count - flushed;  // records pending (lanes [0, min(pend, 64)))
       const bool fl = pend >= FLUSH_AT || last;  // uniform
-      const bool wr = fl && ((rvalid >> lane) & 1);
+      const bool wr = !NO_REC && fl && ((rvalid >> lane) & 1);
       uint64_t rb = w * a.wcap + flushed;  // lane 0's record
       uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
       if constexpr (UNISTORE) {
@@ -1596,7 +1600,7 @@ void scan_kernel(ScanArgs a) {
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + rb, rn * 8),
                                             wr ? 8u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
-                                             wr ? 32u * lane : OOB_OFF, 0, 0);
+                                             wr && !NO_PK ? 32u * lane : OOB_OFF, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
                                              wr ? 32u * lane + 16u : OOB_OFF, 0, 0);
       }
