@@ -41,7 +41,13 @@ import torch  # noqa: E402
 import srd_amd as S  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-SCAN_SAMPLE = 2  # event-stamp every 2nd scan launch (roofline.kernel_ms: >= 10 launches at 20 steps)
+
+
+def scan_sample(steps: int) -> int:
+    """Stamp every k-th timed step: 10 stamped launches per run (k = steps // 10,
+    at least 1) -- enough for min / median, and a stamped launch's ~7 us of
+    extra wall time lands on a tenth of the steps, not half."""
+    return max(1, steps // 10) if steps >= 10 else 1
 PROBE_REPS = 8  # runs of the in-run streaming ceiling (srd_stream_probe_device; roofline.peak_measured)
 
 
@@ -429,12 +435,12 @@ def main():
     torch.cuda.set_device(local)
     ctx = S.Context(local)
     # the roofline's kernel time: HIP events stamped by the scan dispatch on
-    # the library's stream, inside the timed region, on every SCAN_SAMPLE-th
+    # the library's stream, inside the timed region, on every scan_sample()-th
     # launch (an event-stamped launch costs ~7 us more wall time than a plain
     # one: a systematic sample keeps that off the other steps; the product
     # default is no events)
     ctx.set_timing(S.TIMING_SCAN)
-    ctx.set_timing_every(SCAN_SAMPLE)
+    ctx.set_timing_every(scan_sample(args.steps))
 
     if args.config == "c5":
         return bench_c5(args, ctx, local)
@@ -472,7 +478,7 @@ def main():
         ctxs = [ctx] + [S.Context(d) for d in devs[1:]]
         for c in ctxs:
             c.set_timing(S.TIMING_SCAN)
-            c.set_timing_every(SCAN_SAMPLE)
+            c.set_timing_every(scan_sample(args.steps))
         spans, soffs, cuts, keep = [], [], [0], []
         for i, (first, cnt) in enumerate(SH.plan_entry_shards(n * world, world)):
             lo, hi = S.synth_span(None, 0, first, cnt, L, lens)
@@ -522,7 +528,7 @@ def main():
     # launch since its previous call)
     for c in (ctxs if multi is not None else [ctx]):
         c.timings()
-        c.set_timing_every(SCAN_SAMPLE)  # restarts the sample: timed steps 0, SCAN_SAMPLE, 2 SCAN_SAMPLE, ...
+        c.set_timing_every(scan_sample(args.steps))  # restarts the sample: timed steps 0, k, 2k, ...
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -612,7 +618,7 @@ def main():
             "kernel_ms_median": round(scan_each[len(scan_each) // 2], 4) if scan_each else None,
             "kernel_launches": len(scan_each),
             "kernel_timing": "HIP events stamped with the scan dispatch's own start / stop (hipExtLaunchKernel) "
-                             f"on the library stream, every {SCAN_SAMPLE}th timed step (a systematic sample: a "
+                             f"on the library stream, every {scan_sample(args.steps)}th timed step (a systematic sample: a "
                              "stamped launch costs ~7 us more wall time; read out after the timed region)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,

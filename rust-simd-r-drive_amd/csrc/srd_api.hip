@@ -148,6 +148,7 @@ struct Ctx {
   // 2^31; SRD_SLOT_LIMIT_LOG2 (10..31, read at srd_ctx_create) lowers it so the
   // SRD_FULL_SLOT_SPACE fallback can be tested on a small store
   uint64_t slot_limit = 1ull << 31;
+  uint64_t coal_max = 32ull << 30;  // scan_variant_for's size limit of the coalesced tile loads (SRD_SCAN_LOADS)
   // round 0 of the optimistic pass runs the shape check inside
   // chain_finalize_kernel<true> (look-back ranks) instead of check_kernel +
   // chain_finalize_kernel<false>; srd_debug_set_glue_fused A/Bs the two
@@ -670,6 +671,13 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
     const long v = strtol(e, nullptr, 10);
     if (v >= 10 && v <= 31) c->slot_limit = 1ull << v;
   }
+  // the scan's tile loads for every store size: "lines" (line-per-lane) or
+  // "coal" (coalesced + transpose); unset = by size (scan_variant_for).  The
+  // results are identical either way (tests/test_gpu_parity.py runs both)
+  if (const char* e = getenv("SRD_SCAN_LOADS")) {
+    if (!strcmp(e, "lines")) c->coal_max = 0;
+    else if (!strcmp(e, "coal")) c->coal_max = ~0ull;
+  }
   *out = c;
   return 0;
 }
@@ -978,16 +986,16 @@ static int next_scan_events(Ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
 }
 
 // The scan's tile loads (scan_kernel): coalesced nontemporal loads + an
-// in-register transpose (V 0) for resident spans up to kCoalMax bytes, round
+// in-register transpose (V 0) for resident spans up to coal_max bytes, round
 // 4's line-per-lane loads (SCAN_LINES) above.  Measured in the same contexts
 // (profiles/r05/variant_ab_coal_*.txt): C2-shaped stores of 4.4 / 8.7 / 17.4
 // GB -7.5 / -6.2 / -5.5 % scan with the coalesced loads, 70 GB +4 %; C3-
 // shaped 4.3 GB -2.5 %, 18 GB +2.4 %, 72.5 GB +4.8 %.  The debug build's
 // srd_debug_set_scan_variant overrides the choice.
-constexpr uint64_t kCoalMax = 32ull << 30;
+// (Ctx::coal_max = 32 GiB unless SRD_SCAN_LOADS pins one pattern.)
 static uint32_t scan_variant_for(const Ctx* c, uint64_t resident_bytes) {
   if (c->scan_variant) return c->scan_variant;
-  return resident_bytes > kCoalMax ? (uint32_t)SCAN_LINES : 0u;
+  return resident_bytes > c->coal_max ? (uint32_t)SCAN_LINES : 0u;
 }
 
 static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uint64_t* K, uint64_t* h) {

@@ -157,6 +157,40 @@ def test_full_reason_codes(ctx):
         c2.close()
 
 
+def _ctx_with_loads(mode):
+    os.environ["SRD_SCAN_LOADS"] = mode
+    try:
+        return S.Context(0)
+    finally:
+        del os.environ["SRD_SCAN_LOADS"]
+
+
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_scan_load_patterns_agree(golden_cases, flags):
+    """The scan loads a tile either coalesced + nontemporal with an in-register
+    transpose to line-per-lane order (stores up to 32 GiB) or line per lane
+    (above); SRD_SCAN_LOADS pins one pattern for a context.  Both must give
+    the oracle's outputs on every golden fixture and on mixed-size, tombstone,
+    torn and flipped stores, in both passes."""
+    rnd = random.Random(23)
+    lens = _zipf_lens(2500, seed=41)
+    mixed = O.synth_store(len(lens), lens=lens)
+    stores = {name: data for name, (data, m) in golden_cases.items()}
+    stores["zipf"] = mixed
+    stores["cut"] = mixed[: rnd.randrange(1, mixed.size)]
+    flip = mixed.copy()
+    flip[rnd.randrange(flip.size)] ^= 0x10
+    stores["flip"] = flip
+    stores["c1"] = O.synth_store(300)
+    for mode in ("coal", "lines"):
+        c = _ctx_with_loads(mode)
+        try:
+            for name, data in stores.items():
+                check_against_oracle(data, c, flags, f"{mode}:{name}")
+        finally:
+            c.close()
+
+
 @pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
 def test_mixed_sizes(ctx, flags):
     lens = _zipf_lens(3000)
