@@ -1653,6 +1653,11 @@ void scan_kernel(ScanArgs a) {
   load_tile(k0, A);
   if constexpr (TILE_SP) pad_stores(0);
   if constexpr (!RING2) {
+    // A's loads strictly before B's: the scheduler interleaved the two tiles'
+    // coalesced loads here, and the loop's first wait (the minimum over its
+    // entries) then waited for 3 of the next tile's loads too (vmcnt 11
+    // instead of 14): -0.2 to -1 % scan (profiles/r05/variant_ab_prologue_order*.txt)
+    if constexpr (COALT) __builtin_amdgcn_sched_barrier(0);
     load_tile(k0 + 1, Bv);
     pad_stores(1);
   }
