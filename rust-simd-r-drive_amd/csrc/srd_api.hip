@@ -415,6 +415,9 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
   } else if (a.variant == 26) {
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 26>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 26>, grid, block, 0, s, e0, e1, 0, a);
+  } else if (a.variant == 40) {
+    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 40>, grid, block, 0, s, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 40>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 35) {
     hipExtLaunchKernelGGL(scan_kernel<FULL, false, 35>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 36) {
@@ -614,7 +617,7 @@ static void scan_weights(uint32_t (&wq)[16]) {
 }
 #ifdef SRD_DEBUG_API  // timing builds: A/B of scan variants inside one context (one workspace)
 extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
-  if (!c || v < 0 || v > 37) return SRD_ERR_ARG;
+  if (!c || v < 0 || v > 40) return SRD_ERR_ARG;
   c->scan_variant = (uint32_t)v;
   return 0;
 }

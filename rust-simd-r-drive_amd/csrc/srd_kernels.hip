@@ -862,6 +862,16 @@ __device__ __forceinline__ void coal_bswap(uint32_t (&d)[16]) {  // register bit
     }
   }
 }
+// (V 40) the quarter in lane bits 4-5 instead: lane l = 16A + m loads 16 B at
+// 1024 j + 64 m + 16 A (quarter A of line 16 j + m; each instruction still
+// 1 KiB contiguous), and the permlane swaps alone put line L in lane L
+__device__ __forceinline__ uint32_t coal3_lane_off(int lane, int j) {
+  return 1024u * (uint32_t)j + 64u * ((uint32_t)lane & 15u) + 16u * ((uint32_t)lane >> 4);
+}
+__device__ __forceinline__ void coal3_to_lines(uint32_t (&d)[16]) {
+  coal_pswap<1, false>(d);
+  coal_pswap<2, true>(d);
+}
 __device__ __forceinline__ void coal_to_lines(uint32_t (&d)[16]) {
   coal_pswap<1, false>(d);
   coal_pswap<2, true>(d);
@@ -897,7 +907,8 @@ void scan_kernel(ScanArgs a) {
   // transpose them in registers (coal_to_lines); SCAN_LINES (34) = round 4's
   // line-per-lane loads, the product's for large stores (srd_api.hip
   // scan_variant_for); 1-30 keep those loads (earlier experiments)
-  constexpr bool COALT = V == 0 || (V >= 31 && V <= 33) || (V >= 35 && V <= 37);  // (32: with the 2-deep ring)
+  constexpr bool COALT = V == 0 || (V >= 31 && V <= 33) || (V >= 35 && V <= 37) || V == 40;
+  constexpr bool COAL3 = V == 40;  // the permlane-only transpose (coal3_lane_off)  // (32: with the 2-deep ring)
   // timing-only store ablations (results wrong; the store instructions stay,
   // their lanes out of range): 35 = no record stores, 36 = no tile-value
   // stores, 37 = no {p, key_hash} half of c_rec (records of 24 B instead of 40)
@@ -1049,7 +1060,7 @@ void scan_kernel(ScanArgs a) {
       const uint8_t* tb = file + k * (uint64_t)TILE;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(tb + coal_lane_off(lane, j)));
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(tb + (COAL3 ? coal3_lane_off(lane, j) : coal_lane_off(lane, j))));
         o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
       }
       return;
@@ -1131,7 +1142,8 @@ void scan_kernel(ScanArgs a) {
       return;
     }
     constexpr bool tail_tile = decltype(tail_c)::value;
-    if constexpr (COALT) coal_to_lines(d);  // lane l <- line l
+    if constexpr (COAL3) coal3_to_lines(d);  // lane l <- line l
+    else if constexpr (COALT) coal_to_lines(d);
     const uint64_t B = k * (uint64_t)TILE;
     const uint64_t span = k / SPAN_TILES;
     // bytes left in the file from B (uniform, 32-bit: every in-tile test below

@@ -100,6 +100,19 @@ __device__ __forceinline__ void coal2_to_lines(u32x4 (&o)[4]) {
   bswap<8, 2>(o);
 }
 
+// Quarter in lane bits 4-5: lane l = 16A + m loads 16 B at 1024 j + 64 m +
+// 16 A (quarter A of line 16 j + m; each instruction still reads 1 KiB
+// contiguous, a 16-lane row reads every 4th 16-byte piece of it), so one
+// register <-> lane-field swap (v_permlane16/32_swap, 16 instructions)
+// puts line L in lane L.
+__device__ __forceinline__ uint32_t coal3_off(int lane, int j) {
+  return 1024u * j + 64u * ((uint32_t)lane & 15u) + 16u * ((uint32_t)lane >> 4);
+}
+__device__ __forceinline__ void coal3_to_lines(u32x4 (&o)[4]) {
+  pswap<1, false>(o);
+  pswap<2, true>(o);
+}
+
 // verification: every lane's 16 dwords, loaded line-per-lane and coalesced + transposed
 __global__ __launch_bounds__(256) void verify_transpose(const uint8_t* f, uint64_t ntiles, unsigned long long* bad) {
   const int lane = threadIdx.x & 63;
@@ -110,7 +123,11 @@ __global__ __launch_bounds__(256) void verify_transpose(const uint8_t* f, uint64
   for (int j = 0; j < 4; j++) a[j] = ((const u32x4*)(t + 64ull * lane))[j];
 #pragma unroll
   for (int j = 0; j < 4; j++) c[j] = __builtin_nontemporal_load((const u32x4*)(t + 1024ull * j + 16ull * lane));
-  if (bad[1] == 1) {  // the cheaper pattern
+  if (bad[1] == 2) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) c[j] = __builtin_nontemporal_load((const u32x4*)(t + coal3_off(lane, j)));
+    coal3_to_lines(c);
+  } else if (bad[1] == 1) {  // the cheaper pattern
 #pragma unroll
     for (int j = 0; j < 4; j++) c[j] = __builtin_nontemporal_load((const u32x4*)(t + coal2_off(lane, j)));
     coal2_to_lines(c);
@@ -151,7 +168,11 @@ __global__ __launch_bounds__(1024, 1) void probe(const uint8_t* __restrict__ f, 
     // LD 0: the scan's 64 B per lane; 1: the same, nontemporal; 2: coalesced (1 KiB per
     // instruction, 16 B per lane at 1024 j + 16 l); 3: coalesced, nontemporal
     const uint8_t* t = f + (MAP == 3 ? 2 * blockIdx.x + (k & 1) : k) * TILE;
-    if constexpr (LD == 301) {
+    if constexpr (LD == 302 || LD == 303) {  // 303: the loads alone (no transpose)
+#pragma unroll
+      for (int j = 0; j < 4; j++) o[j] = __builtin_nontemporal_load((const u32x4*)(t + coal3_off(lane, j)));
+      if (LD == 302) coal3_to_lines(o);
+    } else if constexpr (LD == 301) {
 #pragma unroll
       for (int j = 0; j < 4; j++) o[j] = __builtin_nontemporal_load((const u32x4*)(t + coal2_off(lane, j)));
       coal2_to_lines(o);
@@ -260,6 +281,13 @@ static void row(const uint8_t* f, uint64_t nt, uint32_t* out, int blocks, double
   fflush(stdout);
 }
 
+template <int N, int LD>
+static void rowp(const uint8_t* f, uint64_t nt, uint32_t* out, int blocks, double bytes) {
+  const float m0 = run<0, N, 3, 0, 0, LD>(f, nt, out, blocks);
+  printf("N=%4d LD=%3d  %.4f ms (%.0f GB/s)\n", N, LD, m0, bytes / m0 / 1e6);
+  fflush(stdout);
+}
+
 int main(int argc, char** argv) {
   const uint64_t bytes = argc > 1 ? strtoull(argv[1], nullptr, 10) : 4362076116ull, nt = (bytes + TILE - 1) / TILE;
   uint8_t* f;
@@ -277,17 +305,28 @@ int main(int argc, char** argv) {
     hipMemcpy(f, h.data(), h.size() * 4, hipMemcpyHostToDevice);
     unsigned long long* bad;
     hipMalloc(&bad, 16);
-    for (unsigned long long mode = 0; mode < 2; mode++) {
+    for (unsigned long long mode = 0; mode < 3; mode++) {
       unsigned long long hb[2] = {0, mode};
       hipMemcpy(bad, hb, 16, hipMemcpyHostToDevice);
       verify_transpose<<<256, 256>>>(f, 1024, bad);
       hipMemcpy(hb, bad, 16, hipMemcpyDeviceToHost);
-      printf("transpose %s check over 1024 tiles: %llu mismatching dwords\n", mode ? "2-swap" : "3-swap", hb[0]);
+      printf("transpose %s check over 1024 tiles: %llu mismatching dwords\n", mode == 2 ? "permlane-only" : mode ? "2-swap" : "3-swap", hb[0]);
     }
   }
-  row<0, 0>(f, nt, out, blocks, b);
-  row<0, 301>(f, nt, out, blocks, b);
-  row<256, 0>(f, nt, out, blocks, b);
-  row<256, 301>(f, nt, out, blocks, b);
+  rowp<0, 0>(f, nt, out, blocks, b);
+  rowp<0, 3>(f, nt, out, blocks, b);
+  rowp<0, 301>(f, nt, out, blocks, b);
+  rowp<0, 302>(f, nt, out, blocks, b);
+  rowp<0, 303>(f, nt, out, blocks, b);
+  rowp<256, 0>(f, nt, out, blocks, b);
+  rowp<256, 3>(f, nt, out, blocks, b);
+  rowp<256, 301>(f, nt, out, blocks, b);
+  rowp<256, 302>(f, nt, out, blocks, b);
+  rowp<256, 303>(f, nt, out, blocks, b);
+  rowp<512, 0>(f, nt, out, blocks, b);
+  rowp<512, 3>(f, nt, out, blocks, b);
+  rowp<512, 301>(f, nt, out, blocks, b);
+  rowp<512, 302>(f, nt, out, blocks, b);
+  rowp<512, 303>(f, nt, out, blocks, b);
   return 0;
 }
