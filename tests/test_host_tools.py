@@ -111,3 +111,21 @@ def test_multi_composition_and_merge_restated(world):
         assert merged == want, name
         order = sorted(v & ((1 << 48) - 1) for v in merged.values())
         assert order == sorted(v & ((1 << 48) - 1) for v in want.values())
+
+
+def test_bench_scan_sample_and_traffic_tag():
+    """bench.py stamps one in ten timed steps (>= 10 stamped scan launches per
+    run), and profiles/traffic.json carries the hash of
+    the kernel sources it was measured on: the line reports `traffic` only
+    for those sources (the committed file matches the committed sources)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    for steps in (10, 20, 50, 100, 1000):
+        k = bench.scan_sample(steps)
+        assert k >= 1 and len(range(0, steps, k)) >= 10
+    assert bench.scan_sample(3) == 1
+    t = json.load(open(os.path.join(root, "profiles", "traffic.json")))
+    assert t["kernel_sources_sha256"] == bench.kernel_sources_hash()
+    assert t["scan_kernel_hbm_bytes_per_launch"] > 4_000_000_000
