@@ -4,7 +4,7 @@ DEFS="-DSRD_DEBUG_API -DSRD_GLUE_STAMPS"`) stamps each block's phase ends
 with s_memrealtime (100 MHz): 0 start, 1 shape check done, 2 look-back done,
 3 tables in LDS, 4 finalize loop done, 5 bucket ranges claimed, 6 end.
 Prints, per phase, the median / max over blocks of the time since the
-earliest block start (us), over REPS calls on the C2 store."""
+earliest block start (us), over REPS calls on the C2 store (CONFIG=c3: C3)."""
 import ctypes as C, json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["SRD_LIB_PATH"] = os.path.join(ROOT, "rust-simd-r-drive_amd", "build", "var", "lib_gstamps.so")
@@ -15,10 +15,15 @@ import srd_amd as S
 L = S.lib()
 L.srd_debug_glue_stamps.argtypes = [C.c_void_p]
 ctx = S.Context(0)
-n = 1 << 20
-size = S.synth_store_len(n)
+cfg = os.environ.get("CONFIG", "c2")  # c3: the 10 M Zipf-sized store
+if cfg == "c3":
+    n, lens, seed = 10_000_000, None, 0x5EED0004
+    lens = S.zipf_lens(n)
+else:
+    n, lens, seed = 1 << 20, None, 0x5EED0001
+size = S.synth_store_len(n, 4096, lens)
 t = torch.empty(S.padded_size(size), dtype=torch.uint8, device="cuda")
-S.synth_store_device(t.data_ptr(), n, 4096, ctx=ctx)
+S.synth_store_device(t.data_ptr(), n, 4096, lens, seed=seed, ctx=ctx)
 torch.cuda.synchronize()
 r = S.DeviceResult()
 buf = np.zeros(256 * 8, np.uint64)
