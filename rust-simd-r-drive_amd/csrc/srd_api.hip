@@ -297,6 +297,7 @@ int upload_tables() {
         }
         t.m4096[tb][b] = mulp(host_xpow8(g_host_tabs, 512), (uint32_t)b << (8 * tb));
         t.m32k[tb][b] = mulp(g_host_tabs.x32768, (uint32_t)b << (8 * tb));
+        for (int j = 0; j < 3; j++) t.mtk[j][tb][b] = mulp(host_xpow8(g_host_tabs, 4096 * (j + 2)), (uint32_t)b << (8 * tb));
       }
     for (int pos = 0; pos < 8; pos++)
       for (int nb = 0; nb < 16; nb++)

@@ -515,6 +515,7 @@ struct FinLds {
   uint32_t tab[1024];         // CRC slice-by-4
   uint32_t m16k[1024];        // v -> v * x^16384
   uint32_t m32k[1024];        // v -> v * x^32768 (a tile step)
+  uint32_t mtk[3 * 1024];     // v -> v * x^(32768 (j + 2)), j = 0..2 (2-4 tile steps)
   uint32_t winit[64], zero_crc[64];
   uint32_t invpow[4097];
 };
@@ -592,18 +593,27 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
       if (k0 == k1) {
         y = acc ^ sxm;
       } else {
-        // one tile step: v * x^32768, one table multiply (m32k); the whole
-        // tiles' values loaded 4 at a time (their loads do not wait for the
-        // chain)
+        // the whole tiles 4 at a time (their values loaded together): acc =
+        // acc * X^r ^ T_0 X^(r-1) ^ ... ^ T_(r-1) for the group's r <= 4
+        // tiles (X = x^32768, tile_T(k) = mul16k(T_lo) ^ SX_32), so the
+        // dependent chain is one table multiply per 4 tiles, not per tile
+        // (the same 32 lookups per 4 tiles; C3's 2-16-tile entries)
         const u32x4* t4 = (const u32x4*)a.tile;
         for (uint64_t kb = k0 + 1; kb < k1; kb += 4) {
           u32x4 tv[4];
 #pragma unroll
           for (int q = 0; q < 4; q++) tv[q] = t4[kb + q < k1 ? kb + q : k1];
+          const uint32_t r = (uint32_t)min<uint64_t>(k1 - kb, 4);
+          uint32_t T[4];
 #pragma unroll
-          for (int q = 0; q < 4; q++)
-            if (kb + q < k1)  // tile_T(k) = mul16k(T_lo) ^ SX_32
-              acc = mul16k_lds(t.m32k, acc) ^ mul16k_lds(m16k, tv[q][0]) ^ tv[q][2];
+          for (int q = 0; q < 4; q++) T[q] = mul16k_lds(m16k, tv[q][0]) ^ tv[q][2];
+          // X^j tables: j = 1 m32k, j = 2..4 mtk[j - 2]
+          auto xt = [&](uint32_t j) -> const uint32_t* { return j == 1 ? t.m32k : t.mtk + 1024 * (j - 2); };
+          uint32_t v = mul16k_lds(xt(r), acc) ^ T[r - 1];
+          if (r >= 2) v ^= mul16k_lds(t.m32k, T[r - 2]);
+          if (r >= 3) v ^= mul16k_lds(t.mtk, T[r - 3]);
+          if (r >= 4) v ^= mul16k_lds(t.mtk + 1024, T[0]);
+          acc = v;
         }
         y = mul16k_lds(t.m32k, acc) ^ (mul16k_lds(m16k, e.t1[0]) ^ e.t1[2]) ^ sxm;
       }
@@ -721,6 +731,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
   const uint32_t ti = threadIdx.x;
   const uint32_t r_tab = g_tabs.tab[ti >> 8][ti & 255],
                  r_m16k = (&g_tabs.m16k[0][0])[ti], r_m32k = (&g_tabs.m32k[0][0])[ti];
+  uint32_t r_mtk[3];
+#pragma unroll
+  for (int j = 0; j < 3; j++) r_mtk[j] = (&g_tabs.mtk[j][0][0])[ti];
   uint32_t r_inv[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) r_inv[j] = g_tabs.invpow[ti + 1024 * j];
@@ -882,6 +895,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       lt.m16k[ti] = r_m16k;
       lt.m32k[ti] = r_m32k;
 #pragma unroll
+      for (int j = 0; j < 3; j++) lt.mtk[1024 * j + ti] = r_mtk[j];
+#pragma unroll
       for (int j = 0; j < 4; j++) lt.invpow[ti + 1024 * j] = r_inv[j];
       if (ti == 0) lt.invpow[4096] = r_inv_last;
       if (ti < 64) {
@@ -930,6 +945,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     tab[ti] = r_tab;
     lt.m16k[ti] = r_m16k;
     lt.m32k[ti] = r_m32k;
+#pragma unroll
+    for (int j = 0; j < 3; j++) lt.mtk[1024 * j + ti] = r_mtk[j];
 #pragma unroll
     for (int j = 0; j < 4; j++) lt.invpow[ti + 1024 * j] = r_inv[j];
     if (ti == 0) lt.invpow[4096] = r_inv_last;

@@ -74,6 +74,7 @@ struct DevTables {
   alignas(16) uint32_t nib_c[8 * 16 * 32];  // c -> c * x^(128 (31 - l % 32))
   uint32_t m4096[4][256];                   // v -> v * x^4096 (512 bytes: the half-lanes' distance)
   uint32_t m32k[4][256];                    // v -> v * x^32768 (one tile step in one multiply)
+  uint32_t mtk[3][4][256];                  // v -> v * x^(32768 (j + 2)): 2-4 tile steps in one multiply
 };
 __device__ DevTables g_tabs;
 #ifdef SRD_WAVE_STAMPS
