@@ -524,17 +524,9 @@ __device__ __forceinline__ uint32_t mul16k_lds(const uint32_t* m16k, uint32_t v)
   return m16k[v & 0xff] ^ m16k[256 + ((v >> 8) & 0xff)] ^ m16k[512 + ((v >> 16) & 0xff)] ^ m16k[768 + (v >> 24)];
 }
 
-// crc_raw of bytes [floor64(m), m) (tail_crc) with the CRC table in LDS
+// crc_raw of bytes [floor64(m), m) (tail_crc_line) with the CRC table in LDS
 __device__ __forceinline__ uint32_t tail_crc_lds(const uint8_t* file, uint64_t m, const uint32_t* tab) {
-  const uint64_t L = m & ~63ull;
-  const uint32_t r = (uint32_t)(m - L);
-  uint32_t s = 0, q = 0;
-  for (; q + 4 <= r; q += 4) {
-    s ^= *(const uint32_t*)(file + L + q);
-    s = tab[768 + (s & 0xff)] ^ tab[512 + ((s >> 8) & 0xff)] ^ tab[256 + ((s >> 16) & 0xff)] ^ tab[s >> 24];
-  }
-  for (; q < r; q++) s = tab[(s ^ file[L + q]) & 0xff] ^ (s >> 8);
-  return s;
+  return tail_crc_line(file, m, [tab](int t, uint32_t b) { return tab[256 * t + b]; });
 }
 
 // finalize_core (srd_kernels.hip) for a candidate chain entry from its

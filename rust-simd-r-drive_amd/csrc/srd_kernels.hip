@@ -2090,19 +2090,37 @@ struct FinArgs {
   unsigned long long* n_bad;
 };
 
-// crc_raw of bytes [floor64(m), m) read from the file (<= 63 bytes)
-__device__ __forceinline__ uint32_t tail_crc(const uint8_t* file, uint64_t m) {
+// crc_raw of bytes [floor64(m), m) (<= 63 bytes) in one round trip: the
+// 64-byte line at floor64(m) by four independent 16-byte loads (the store is
+// readable to srd_padded_size, so the whole line is), then <= 15 slice-by-4
+// word steps and <= 3 byte steps from registers.  (A word load per step made
+// every step wait for its own HBM round trip: up to 18 dependent loads per
+// entry, which set C3's finalize pass time.)  tab(t, b) = slice table t, byte b.
+template <class Tab>
+__device__ __forceinline__ uint32_t tail_crc_line(const uint8_t* file, uint64_t m, Tab tab) {
   const uint64_t L = m & ~63ull;
   const uint32_t r = (uint32_t)(m - L);
+  if (r == 0) return 0;
+  const u32x4* lp = (const u32x4*)(file + L);
+  const u32x4 q0 = lp[0], q1 = lp[1], q2 = lp[2], q3 = lp[3];
+  const uint32_t w[16] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],
+                          q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3]};
   uint32_t s = 0;
-  uint32_t q = 0;
-  for (; q + 4 <= r; q += 4) {
-    s ^= *(const uint32_t*)(file + L + q);
-    s = g_tabs.tab[3][s & 0xff] ^ g_tabs.tab[2][(s >> 8) & 0xff] ^ g_tabs.tab[1][(s >> 16) & 0xff] ^
-        g_tabs.tab[0][s >> 24];
+#pragma unroll
+  for (int i = 0; i < 15; i++) {
+    if (4u * i + 4u <= r) {
+      s ^= w[i];
+      s = tab(3, s & 0xff) ^ tab(2, (s >> 8) & 0xff) ^ tab(1, (s >> 16) & 0xff) ^ tab(0, s >> 24);
+    }
   }
-  for (; q < r; q++) s = g_tabs.tab[0][(s ^ file[L + q]) & 0xff] ^ (s >> 8);
+  uint32_t pw = 0;  // the partial word w[r / 4] (selects: no indexed register access)
+#pragma unroll
+  for (int i = 0; i < 16; i++) pw = (uint32_t)i == (r >> 2) ? w[i] : pw;
+  for (uint32_t b = 0; b < (r & 3u); b++) s = tab(0, (s ^ (pw >> (8 * b))) & 0xff) ^ (s >> 8);
   return s;
+}
+__device__ __forceinline__ uint32_t tail_crc(const uint8_t* file, uint64_t m) {
+  return tail_crc_line(file, m, [](int t, uint32_t b) { return g_tabs.tab[t][b]; });
 }
 
 // per-tile values: tile[4k] / tile[4k+1] = half-tile partials of lines 0 / 1,
