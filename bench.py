@@ -586,6 +586,9 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (counter-mode splitmix64 payloads, keys bench-key-{i}), generated in HBM",
+        # the sha256 baked into the loaded libsrd_amd.so (srd_build_info), equal to
+        # the sources beside it (srd_amd.lib() refuses anything else)
+        "build": {"libsrd_amd_src_sha256": S.build_info()},
         "config": {
             "workload": (("C4 partition at N=1 (the weak-scaling base: 2^21 x 4 KiB per GPU, as at N = 2/4/8)"
                           if args.config == "c2" and n == 1 << 21 and L == 4096 else args.config.upper()) +

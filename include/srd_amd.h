@@ -72,6 +72,8 @@ extern "C" {
 #define SRD_FULL_NO_START 4   /* no strong node or root at the start tail (find_top): torn / corrupt end */
 #define SRD_FULL_UNPROVEN 5   /* the recorded nodes do not prove one chain (shape / root count) */
 #define SRD_FULL_CAP 6        /* the candidate slots per span could not grow further */
+#define SRD_FULL_LOOKBACK 7   /* the fused shape check's decoupled look-back timed out (a chain block
+                                 waited too long for a lower one): nothing it computed is used */
 
 /* option flags */
 #define SRD_FLAG_FORCE_FULL 1u   /* skip the optimistic (strong-candidate) pass */
@@ -92,6 +94,11 @@ void srd_ctx_destroy(srd_ctx *ctx);
 /* The HIP stream the context launches on (hipStream_t as void*). */
 void *srd_ctx_stream(srd_ctx *ctx);
 const char *srd_last_error(void);
+/* The sha256 of the sources this library was compiled from (csrc/ +
+ * include/srd_amd.h, rust-simd-r-drive_amd/src_hash.py), 64 hex digits;
+ * the Python mirror refuses a library whose hash differs from the sources
+ * beside it, and bench.py / smoke print it. */
+const char *srd_build_info(void);
 /* HIP-event timing of the validate calls on ctx: SRD_TIMING_NONE (the
  * default), SRD_TIMING_SCAN (the streaming scan's launches: events stamped by
  * the scan dispatch itself, hipExtLaunchKernel -- bench.py's roofline),

@@ -35,6 +35,10 @@ using namespace srd;
 static thread_local std::string g_err;
 static void set_err(const std::string& s) { g_err = s; }
 extern "C" const char* srd_last_error(void) { return g_err.c_str(); }
+#ifndef SRD_SOURCE_HASH
+#define SRD_SOURCE_HASH "unknown"  // (built without the Makefile)
+#endif
+extern "C" const char* srd_build_info(void) { return SRD_SOURCE_HASH; }
 
 #define HIPCHK(x)                                                                         \
   do {                                                                                    \
@@ -153,6 +157,10 @@ struct Ctx {
   // chain_finalize_kernel<true> (look-back ranks) instead of check_kernel +
   // chain_finalize_kernel<false>; srd_debug_set_glue_fused A/Bs the two
   bool glue_fused = true;
+  // test knobs read at srd_ctx_create: SRD_GLUE_FUSED=0 (round 0 through
+  // check_kernel + chain_finalize_kernel<false>, the retry rounds' shape) and
+  // SRD_LB_FAIL_BLOCK=b (chain block b's look-back treated as timed out)
+  uint32_t lb_fail = ~0u;
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -681,6 +689,12 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   if (const char* e = getenv("SRD_SCAN_LOADS")) {
     if (!strcmp(e, "lines")) c->coal_max = 0;
     else if (!strcmp(e, "coal")) c->coal_max = ~0ull;
+  }
+  if (const char* e = getenv("SRD_GLUE_FUSED")) c->glue_fused = strcmp(e, "0") != 0;
+  if (const char* e = getenv("SRD_LB_FAIL_BLOCK")) {
+    char* end = nullptr;
+    const unsigned long v = strtoul(e, &end, 10);
+    if (end != e && v < CHAIN_BLOCKS) c->lb_fail = (uint32_t)v;
   }
   *out = c;
   return 0;
@@ -1228,8 +1242,10 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const uint32_t log2_nbk = index_log2_buckets(n_est);
     // the scan's partition (ScanPart): total_waves waves of at most spw
     // spans; each wave's records are dense in its region of wcap = spw * cap slots
+    // (the variant once: its geometry sizes the partition and the launch)
+    const uint32_t var = scan_variant_for(c, flen - span_off);
     uint32_t nw;
-    const unsigned g = scan_grid(c, c->scan_variant, ns_rel, &nw);
+    const unsigned g = scan_grid(c, var, ns_rel, &nw);
     const ScanPart part = scan_part(c, s_lo, ns_rel, g, nw);
     const uint64_t total_waves = (uint64_t)g * nw;
     const uint64_t spw = part_max_wave_spans(part);
@@ -1257,7 +1273,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     // per-tile / per-span arrays hold the resident range only: their base
     // pointers are shifted so kernels index them by absolute tile / span
     ScanArgs a{};
-    a.variant = scan_variant_for(c, flen - span_off);
+    a.variant = var;
     a.part = part;
     a.file = d_file;
     a.flen = flen;
@@ -1329,6 +1345,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       sa.counters = (const unsigned long long*)cnt;
       sa.plan = pl;
       sa.zero = index_zero_words(c, log2_nbk, &sa.n_zero);  // child2 zeroes the index's bucket fills
+      sa.lb_fail = c->lb_fail;
       if (rounds == 0) {
         // round 0: the link phase's claims (every node claims its parent) are the
         // core flags and the branch test; no marks
@@ -1451,7 +1468,9 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       continue;
     }
     if (hp.status) {  // not provable here -> full pass (whole file) / unproven (span)
-      out->full_reason = (hp.status & ST_NOSTART) ? SRD_FULL_NO_START : SRD_FULL_UNPROVEN;
+      out->full_reason = (hp.status & ST_LOOKBACK) ? SRD_FULL_LOOKBACK
+                         : (hp.status & ST_NOSTART) ? SRD_FULL_NO_START
+                                                    : SRD_FULL_UNPROVEN;
       return 0;
     }
     out->full_reason = SRD_FULL_NONE;

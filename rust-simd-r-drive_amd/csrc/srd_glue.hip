@@ -209,6 +209,9 @@ struct ShapeArgs {
   uint32_t coff;     // chain entries before the first candidate (1 whole file, 0 span mode)
   uint32_t* zero;    // child2_kernel zeroes [zero, zero + n_zero): the index's bucket fills and chunk counts
   uint32_t n_zero;
+  // FUSED chain_finalize: the chain block whose look-back is treated as timed
+  // out (SRD_LB_FAIL_BLOCK at context creation, a test knob); ~0u = none
+  uint32_t lb_fail;
 };
 
 // the slot of the node at the start tail find_top chose (the scan's
@@ -628,7 +631,11 @@ __device__ __forceinline__ bool finalize_in(const FinArgs& a, uint64_t c, const 
 // agent-scope atomic stores and loads, no fence, no per-call memset (a stale
 // granule carries another call's tag).  A block only waits for LOWER blocks,
 // dispatched before it, so the grid cannot deadlock; a bounded spin that runs
-// out sets ST_LOOKBACK and the host takes the full pass.
+// out publishes state 3 (a POISONED inclusive prefix): every later block's
+// look-back stops there and fails too, so the plan (the last block) carries
+// ST_LOOKBACK and the host takes the full pass -- a timed-out block never
+// passes a partial prefix on as if it were complete (ShapeArgs::lb_fail forces
+// the timeout in one block: tests/test_gpu_parity.py::test_lookback_fallback).
 constexpr uint32_t ST_LOOKBACK = 32;
 #ifdef SRD_GLUE_STAMPS  // timing-only build (tools/glue_stamps.py): per-block phase ends of chain_finalize<true>
 __device__ uint64_t g_glue_stamp[CHAIN_BLOCKS * 8];
@@ -644,7 +651,8 @@ __device__ __forceinline__ uint64_t lb_pack(uint32_t tag, uint32_t st, bool fail
 }
 __device__ __forceinline__ uint32_t lb_tag(uint32_t gen) { return gen % 0xFFFFFFu + 1u; }
 // wave 0 of block b: the exclusive prefix of blocks [0, b) -- core count,
-// failure, root-linked nodes; false when the spin bound ran out
+// failure, root-linked nodes; false when the spin bound ran out or the
+// inclusive prefix it stops at is poisoned (state 3: a lower block timed out)
 __device__ bool lb_lookback(unsigned long long* desc, uint32_t b, uint32_t tag, uint64_t* cnt, bool* fail,
                             uint32_t* nr) {
   typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -664,9 +672,11 @@ __device__ bool lb_lookback(unsigned long long* desc, uint32_t b, uint32_t tag, 
       if (++spins > (1u << 22)) return false;  // uniform
       __builtin_amdgcn_s_sleep(2);
     }
-    const uint64_t inc = __ballot(((v >> 38) & 3) == 2);
+    const uint32_t stv = (uint32_t)(v >> 38) & 3u;
+    const uint64_t inc = __ballot(stv >= 2);
     const uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
     const bool take = lane <= first;
+    if (__ballot(take && stv == 3)) return false;  // (uniform) a poisoned prefix
     uint64_t c = take ? (v & LB_CNT) : 0;
     uint32_t r = take ? (uint32_t)((v >> 35) & 3) : 0u;
     uint32_t fl = take ? (uint32_t)((v >> 37) & 1) : 0u;
@@ -906,11 +916,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
         uint64_t pc = 0;
         bool pf = false;
         uint32_t pn = 0;
-        const bool ok = lb_lookback(lb_desc, blockIdx.x, ltag, &pc, &pf, &pn);
+        const bool ok = blockIdx.x != a.lb_fail && lb_lookback(lb_desc, blockIdx.x, ltag, &pc, &pf, &pn);
         if (lane == 0) {
           const bool f2 = pf || s_fail;
           const uint32_t n2 = pn + s_nroot;
-          __hip_atomic_store((gu64*)(lb_desc + blockIdx.x), lb_pack(ltag, 2, f2, n2, pc + btot), __ATOMIC_RELAXED,
+          __hip_atomic_store((gu64*)(lb_desc + blockIdx.x),
+                             ok ? lb_pack(ltag, 2, f2, n2, pc + btot) : lb_pack(ltag, 3, true, 0, 0), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
           s_lb[0] = pc;
           s_lb[1] = pc + btot;

@@ -39,7 +39,7 @@ SRD_MODE_FULL = 1
 SRD_MODE_SPAN_UNPROVEN = 3
 # srd_device_result.full_reason (include/srd_amd.h)
 SRD_FULL_NONE, SRD_FULL_FORCED, SRD_FULL_SLOT_SPACE, SRD_FULL_WAVES = 0, 1, 2, 3
-SRD_FULL_NO_START, SRD_FULL_UNPROVEN, SRD_FULL_CAP = 4, 5, 6
+SRD_FULL_NO_START, SRD_FULL_UNPROVEN, SRD_FULL_CAP, SRD_FULL_LOOKBACK = 4, 5, 6, 7
 SRD_FLAG_MERGE_INDEX = 16  # multi-GPU open: the whole index on ctxs[0] (default: by owner)
 SRD_MULTI_COMPOSED, SRD_MULTI_NEIGHBOUR, SRD_MULTI_WHOLE_FILE = 0, 1, 2  # srd_multi_summary.path
 SPAN_ALIGN = 16384  # span_off granularity of srd_validate_span_device
@@ -50,7 +50,7 @@ OFFSET_MASK = (1 << 48) - 1
 
 # symbols include/srd_amd.h declares
 EXPORTS = [
-    "srd_ctx_create", "srd_ctx_destroy", "srd_ctx_stream", "srd_last_error", "srd_ctx_timings",
+    "srd_ctx_create", "srd_ctx_destroy", "srd_ctx_stream", "srd_last_error", "srd_build_info", "srd_ctx_timings",
     "srd_ctx_set_timing",
     "srd_validate_index_device", "srd_validate_index", "srd_result_free",
     "srd_recover_valid_chain", "srd_key_indexer_build", "srd_crc32_batch",
@@ -91,6 +91,12 @@ class MultiSummary(C.Structure):
     ]
 
 
+def build_info() -> str:
+    """srd_build_info(): the sha256 of the sources the loaded library was
+    compiled from (equal to src_hash.source_hash(), or lib() refused it)."""
+    return lib().srd_build_info().decode()
+
+
 def build() -> str:
     """Compile the HIP library in-tree (hipcc --offload-arch=gfx950)."""
     subprocess.check_call(["make", "-s", "-C", HERE])
@@ -115,6 +121,16 @@ def lib():
             pass
         L = C.CDLL(LIB_PATH)
         vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+        L.srd_build_info.restype = C.c_char_p
+        if not os.environ.get("SRD_LIB_PATH"):  # (timing tools load variant builds by path)
+            import importlib.util
+            spec = importlib.util.spec_from_file_location("srd_src_hash", os.path.join(HERE, "src_hash.py"))
+            sh = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(sh)
+            want, got = sh.source_hash(), L.srd_build_info().decode()
+            if got != want:
+                raise RuntimeError(f"{LIB_PATH} was built from other sources (sha256 {got}, the sources here "
+                                   f"{want}): run `make -C {HERE}`")
         L.srd_ctx_create.argtypes = [i32, C.POINTER(vp)]
         L.srd_ctx_destroy.argtypes = [vp]
         L.srd_ctx_stream.argtypes = [vp]
@@ -162,7 +178,7 @@ def lib():
         L.srd_ctx_multi_shard_ms.argtypes = [vp, C.POINTER(C.c_double), i32]
         L.srd_stream_probe_device.argtypes = [vp, vp, u64, i32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         for f in EXPORTS:
-            if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error",
+            if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error", "srd_build_info",
                          "srd_padded_size", "srd_index_table_bytes"):
                 getattr(L, f).restype = i32
         _lib = L

@@ -13,7 +13,8 @@ the store to the whole-file path; `summary.path` says which decided.
 
 Full C4 (BASELINE configs[3]: 16M x 4 KiB = 69,793,218,516 B, 8 shards of 2^21
 entries): by size-independent properties -- final_len, counts, the chain's
-offsets, sampled CRCs against zlib, one flipped byte = one bad CRC, the
+offsets, every CRC against the oracle's host CRC (plus sampled zlib), one
+flipped byte = one bad CRC, the
 index's key set = the chain's key set = the bench-key-{i} hashes sampled, every
 key at its owner, merged == union of the owners' parts.
 """
@@ -248,8 +249,31 @@ def test_full_c4_eight_shards():
         st = torch.cat([S.device_view(r.crc_stored, r.n_chain, np.uint32) for r in shards])
         assert torch.equal(crc, st)
         kh = torch.cat([S.device_view(r.key_hash, r.n_chain) for r in shards])
-        # sampled CRCs against zlib, straight from the shards' HBM
         per = C4_N // C4_W
+        # every one of the 2^24 computed CRCs against the oracle's independent
+        # PCLMUL CRC (entry_handle.rs:260-275 / compute_checksum.rs:15-20) over
+        # each shard's bytes streamed D2H in ~2 GiB groups of whole entries:
+        # crc_stored was written by the device's synth kernel, which shares the
+        # scan's CRC machinery, so crc == st alone could hide a common bug
+        grp = 1 << 19
+        host = torch.empty(4160 * grp, dtype=torch.uint8, pin_memory=True)
+        hn = host.numpy()
+        crc_h = crc.cpu().numpy().view(np.uint32)
+        checked = 0
+        for s_i in range(C4_W):
+            for i0 in range(s_i * per, (s_i + 1) * per, grp):
+                i1 = min(i0 + grp, (s_i + 1) * per)
+                b0 = 4160 * i0 - soffs[s_i]
+                nb = 4160 * (i1 - i0) - 64  # through the last entry's payload
+                host[:nb].copy_(keep[s_i][b0:b0 + nb])
+                starts = np.arange(i1 - i0, dtype=np.uint64) * np.uint64(4160)
+                got = O.crc32_ranges(hn[:nb], starts, np.full(i1 - i0, 4096, np.uint64), threads=16)
+                bad = np.nonzero(got != crc_h[i0:i1])[0]
+                assert bad.size == 0, ("crc_computed differs from the host CRC", s_i, int(i0 + bad[0]), bad.size)
+                checked += i1 - i0
+        assert checked == C4_N
+        del host, hn, crc_h
+        # sampled CRCs against zlib, straight from the shards' HBM
         for i in np.random.default_rng(4).integers(0, C4_N, 200).tolist():
             s = i // per
             off = 4160 * i - soffs[s]

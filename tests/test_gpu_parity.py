@@ -157,6 +157,84 @@ def test_full_reason_codes(ctx):
         c2.close()
 
 
+def _ctx_with_env(**env):
+    """A context created under the given SRD_* environment knobs (read once at
+    srd_ctx_create)."""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return S.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("block", [0, 100, 255])
+def test_lookback_fallback(ctx, block):
+    """The fused shape check's decoupled look-back (chain_finalize_kernel<true>)
+    falls back safely when a chain block's spin bound runs out:
+    SRD_LB_FAIL_BLOCK=b treats block b's look-back as timed out.  The block
+    publishes a poisoned prefix, every later block's look-back fails on it, and
+    the plan carries ST_LOOKBACK, so the call goes to the full pass
+    (SRD_FULL_LOOKBACK) and still returns the oracle's outputs
+    (data_store.rs:383-482, key_indexer.rs:98-124).  A normal context's next
+    call decides optimistically again (stale granules carry another tag)."""
+    lens = _zipf_lens(1500, seed=77)
+    stores = {"c1": O.synth_store(1000), "zipf": O.synth_store(len(lens), lens=lens)}
+    c = _ctx_with_env(SRD_LB_FAIL_BLOCK=block)
+    try:
+        for name, st in stores.items():
+            r = check_against_oracle(st, c, 0, f"lb{block}:{name}")
+            assert (r.mode, r.full_reason) == (S.SRD_MODE_FULL, S.SRD_FULL_LOOKBACK), (name, r.mode, r.full_reason)
+    finally:
+        c.close()
+    r = check_against_oracle(stores["c1"], ctx, 0, "after")
+    assert (r.mode, r.full_reason) == (S.SRD_MODE_OPTIMISTIC, S.SRD_FULL_NONE)
+
+
+def test_unfused_glue_agrees(golden_cases):
+    """Round 0 of the optimistic pass runs the shape check fused into
+    chain_finalize_kernel<true> (neighbour-lane parent words, lazy start node,
+    per-block root tail); SRD_GLUE_FUSED=0 runs check_kernel +
+    chain_finalize_kernel<false>, the shape the retry rounds use.  Both must
+    give the oracle's outputs on the golden, torn, flipped, tombstone and
+    false-chain stores."""
+    rnd = random.Random(31)
+    lens = _zipf_lens(2000, seed=43)
+    mixed = O.synth_store(len(lens), lens=lens)
+    stores = {name: data for name, (data, m) in golden_cases.items()}
+    stores["zipf"] = mixed
+    for i in range(6):
+        stores[f"cut{i}"] = mixed[: rnd.randrange(1, mixed.size)]
+        flip = mixed.copy()
+        flip[rnd.randrange(flip.size)] ^= 1 << rnd.randrange(8)
+        stores[f"flip{i}"] = flip
+    stores["corrupt"] = np.concatenate([mixed, np.frombuffer(b"CORRUPT", np.uint8)])
+    buf = bytearray()
+    t = 0
+    for step in range(300):
+        kh = xxhash.xxh3_64_intdigest(b"key%d" % rnd.randrange(40))
+        if rnd.random() < 0.2:
+            t = O.write_entries(buf, t, [(kh, b"\x00")], allow_null=True)
+        else:
+            t = O.write_entries(buf, t, [(kh, rnd.randbytes(rnd.choice([1, 20, 64, 700, 4096])) or b"\x01")])
+    stores["tomb"] = bytes(buf)
+    for fused in ("1", "0"):
+        c = _ctx_with_env(SRD_GLUE_FUSED=fused)
+        try:
+            for name, data in stores.items():
+                check_against_oracle(data, c, 0, f"fused{fused}:{name}")
+            for rv in (False, True):
+                data = _false_chain_store(rv)
+                r = check_against_oracle(data, c, 0, f"fused{fused}:false{rv}")
+                assert r.mode == S.SRD_MODE_OPTIMISTIC, (fused, rv, r.mode)
+        finally:
+            c.close()
+
+
 def _ctx_with_loads(mode):
     os.environ["SRD_SCAN_LOADS"] = mode
     try:
@@ -314,6 +392,20 @@ def test_full_size_c2_properties(ctx):
     host = t[:size].cpu().numpy()
     st = O.validate_index(host, 8)
     assert (st.final_len, st.n_chain, st.n_index, st.n_crc_bad) == (size, n, n, 0)
+    # the full index against KeyIndexer::build (key_indexer.rs:98-124) of the
+    # oracle: every (key_hash, packed) pair, not just the count
+    keys, packed = O.key_indexer_arrays(host, size)
+    ik = S.device_to_numpy(r.index_key_hash, n, np.uint64)
+    iv = S.device_to_numpy(r.index_packed, n, np.uint64)
+    o = np.argsort(ik, kind="stable")
+    assert np.array_equal(ik[o], keys) and np.array_equal(iv[o], packed)
+    # and every chain entry's computed CRC against the oracle's independent
+    # PCLMUL CRC (entry_handle.rs:260-275)
+    mo = S.device_to_numpy(r.meta_off, n, np.uint64)
+    ln = S.device_to_numpy(r.payload_len, n, np.uint64)
+    crc = S.device_to_numpy(r.crc_computed, n, np.uint32)
+    assert np.array_equal(O.crc32_ranges(host, mo - ln, ln, threads=16), crc)
+    del ik, iv, keys, packed, mo, ln, crc
     # flip one payload byte deep in the store -> exactly one bad CRC
     pos = 4160 * 777_777 + 1234
     t[pos] ^= 0x40
@@ -330,26 +422,21 @@ def _fake_record(key: int, prev: int, crc: int) -> bytes:
     return struct.pack("<QQI", key, prev, crc)
 
 
-@pytest.mark.parametrize("root_variant", [False, True])
-def test_false_candidate_chain_is_pruned(ctx, root_variant):
+def _false_chain_store(root_variant):
     """Payload bytes that look like a chain of two metadata records (B links
-    to A, A links nowhere -- or to a zero region, i.e. the root rule): the
-    reference never visits them (it only follows back-pointers from the
-    tail); the optimistic pass must prune them and stay optimistic."""
+    to A, A links nowhere -- or to a zero region, i.e. the root rule)."""
     buf = bytearray()
     t = 0
     t = O.write_entries(buf, t, [(0x1111, bytes(3000))])  # zero payload: a zero region for the root variant
     for i in range(5):
         t = O.write_entries(buf, t, [(0x2000 + i, random.Random(i).randbytes(700))])
-    # fake A inside a payload: its "prev" is 25 (no record there) or a zero region
-    a_pos = len(buf) + 64 + 100  # payload start is the next 64-aligned offset; A sits 100 bytes in
+    # fake A inside a payload (100 bytes into it): its "prev" is 25 (no record
+    # there) or a zero region
     pl = bytearray(random.Random(99).randbytes(400))
     prev_a = 2000 if root_variant else 25
     pl[100:120] = _fake_record(0xAAAA, prev_a, 0x12345678)
     pad = (64 - len(buf) % 64) % 64
-    assert len(buf) + pad + 100 == a_pos - 64 + pad or True
-    start = len(buf) + pad
-    a_pos = start + 100
+    a_pos = len(buf) + pad + 100
     t = O.write_entries(buf, t, [(0x3000, bytes(pl))])
     # fake B in a later payload, linking to A's tail
     pl2 = bytearray(random.Random(98).randbytes(500))
@@ -357,8 +444,17 @@ def test_false_candidate_chain_is_pruned(ctx, root_variant):
     t = O.write_entries(buf, t, [(0x3001, bytes(pl2))])
     for i in range(5):
         t = O.write_entries(buf, t, [(0x4000 + i, random.Random(50 + i).randbytes(300))])
-    r = check_against_oracle(bytes(buf), ctx, 0, "fakechain")
-    assert r.mode == S.SRD_MODE_OPTIMISTIC and r.final_len == len(buf)
+    return bytes(buf)
+
+
+@pytest.mark.parametrize("root_variant", [False, True])
+def test_false_candidate_chain_is_pruned(ctx, root_variant):
+    """A false chain in payload bytes (_false_chain_store): the reference never
+    visits it (it only follows back-pointers from the tail); the optimistic
+    pass must prune it and stay optimistic."""
+    data = _false_chain_store(root_variant)
+    r = check_against_oracle(data, ctx, 0, "fakechain")
+    assert r.mode == S.SRD_MODE_OPTIMISTIC and r.final_len == len(data)
 
 
 def test_c3_shape_200k_stays_optimistic(ctx):
@@ -377,6 +473,20 @@ def test_c3_shape_200k_stays_optimistic(ctx):
     host = t[:size].cpu().numpy()
     st = O.validate_index(host, 8)
     assert (st.final_len, st.n_chain, st.n_index, st.n_crc_bad) == (size, n, n, 0)
+    # the full index against KeyIndexer::build (key_indexer.rs:98-124) of the
+    # oracle: every (key_hash, packed) pair, not just the count
+    keys, packed = O.key_indexer_arrays(host, size)
+    ik = S.device_to_numpy(r.index_key_hash, n, np.uint64)
+    iv = S.device_to_numpy(r.index_packed, n, np.uint64)
+    o = np.argsort(ik, kind="stable")
+    assert np.array_equal(ik[o], keys) and np.array_equal(iv[o], packed)
+    # and every chain entry's computed CRC against the oracle's independent
+    # PCLMUL CRC (entry_handle.rs:260-275)
+    mo = S.device_to_numpy(r.meta_off, n, np.uint64)
+    ln = S.device_to_numpy(r.payload_len, n, np.uint64)
+    crc = S.device_to_numpy(r.crc_computed, n, np.uint32)
+    assert np.array_equal(O.crc32_ranges(host, mo - ln, ln, threads=16), crc)
+    del ik, iv, keys, packed, mo, ln, crc
     crc = S.device_to_numpy(r.crc_computed, n, np.uint32)
     mo = S.device_to_numpy(r.meta_off, n, np.uint64)
     ln = S.device_to_numpy(r.payload_len, n, np.uint64)
