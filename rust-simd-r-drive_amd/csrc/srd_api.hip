@@ -368,92 +368,10 @@ static void launch_scan(unsigned g, const ScanArgs& a, hipStream_t s, hipEvent_t
     if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, SCAN_LINES>, grid, block, 0, s, e0, e1, 0, a);
     else hipExtLaunchKernelGGL(scan_kernel<FULL, false, SCAN_LINES>, grid, block, 0, s, e0, e1, 0, a);
 #ifdef SRD_DEBUG_API
-  } else if (a.variant == 1) {  // A/B variants (scan_kernel's V) inside one context
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 1>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 1>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 2) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 2>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 2>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 3) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 3>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 3>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 4) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 4>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 4>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 5) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 5>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 5>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 6) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 6>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 6>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 7) {
+  } else if (a.variant == 7) {  // timing-only ablations (scan_kernel's V) inside one context
     hipExtLaunchKernelGGL(scan_kernel<FULL, false, 7>, grid, block, 0, s, e0, e1, 0, a);
   } else if (a.variant == 8) {
     hipExtLaunchKernelGGL(scan_kernel<FULL, false, 8>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 9) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 9>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 9>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 11) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 11>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 11>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 12) {
-    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 12>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 13) {
-    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 13>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 14) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 14>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 14>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 10) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 10>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 10>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 20) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 20>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 20>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 21) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 21>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 21>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 23) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 23>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 23>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 24) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 24>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 24>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 25) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 25>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 25>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 26) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 26>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 26>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 40) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 40>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 40>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 35) {
-    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 35>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 36) {
-    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 36>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 37) {
-    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 37>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 33) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 33>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 33>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 32) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 32>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 32>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 31) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 31>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 31>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 30) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 30>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 30>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 27) {
-    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 27>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 28) {
-    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 28>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 29) {
-    hipExtLaunchKernelGGL(scan_kernel<FULL, false, 29>, grid, block, 0, s, e0, e1, 0, a);
-  } else if (a.variant == 22) {
-    if (a.flen > kWide) hipExtLaunchKernelGGL(scan_kernel<FULL, true, 22>, grid, block, 0, s, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(scan_kernel<FULL, false, 22>, grid, block, 0, s, e0, e1, 0, a);
 #endif
   } else if (e0) {
     if (a.flen > kWide)
@@ -626,7 +544,7 @@ static void scan_weights(uint32_t (&wq)[16]) {
 }
 #ifdef SRD_DEBUG_API  // timing builds: A/B of scan variants inside one context (one workspace)
 extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
-  if (!c || v < 0 || v > 40) return SRD_ERR_ARG;
+  if (!c || !(v == 0 || v == 7 || v == 8 || v == SCAN_LINES)) return SRD_ERR_ARG;
   c->scan_variant = (uint32_t)v;
   return 0;
 }
@@ -751,7 +669,7 @@ static void grow_cap(CandCap& k, uint64_t bytes) {
 // CU x CUs) and waves per block (scan_nw / scan_bpc)
 static unsigned scan_grid(const Ctx* c, uint32_t variant, uint64_t ns, uint32_t* nw) {
   *nw = (uint32_t)scan_nw((int)variant);
-  return (unsigned)std::min<uint64_t>((ns + *nw - 1) / *nw, (uint64_t)c->scan_blocks * scan_bpc((int)variant));
+  return (unsigned)std::min<uint64_t>((ns + *nw - 1) / *nw, (uint64_t)c->scan_blocks);
 }
 static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g, uint32_t nw) {
   ScanPart p{};
@@ -801,6 +719,10 @@ static int alloc_scan(Ctx* c, uint64_t n_tiles, uint64_t n_spans, uint32_t cap) 
   TRY(ensure(c, B_WALK, sizeof(WalkState)));
   return 0;
 }
+
+// the second half of every candidate record (ScanArgs::c_rec1): B_CREC's
+// upper half (its lower half is c_rec), fixed while the buffer is
+static u32x4* crec1(Ctx* c) { return P<u32x4>(c, B_CREC) + c->bufs[B_CREC].n / 32; }
 
 static int alloc_dense(Ctx* c, uint64_t K) {
   TRY(ensure(c, B_DM, K * 8));
@@ -932,6 +854,7 @@ static int finish(Ctx* c, const uint8_t* d_file, uint64_t flen, uint64_t n, uint
   f.ws = P<WalkState>(c, B_WALK);
   f.c_m = P<uint64_t>(c, B_CM);
   f.c_rec = P<u32x4>(c, B_CREC);
+  f.c_rec1 = crec1(c);
   f.tile = P<uint32_t>(c, B_TILE);
   f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
   f.coff = 1;
@@ -1038,6 +961,7 @@ static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uin
     a.span_count = P<uint32_t>(c, B_SPAN_COUNT);
     a.c_m = P<uint64_t>(c, B_CM);
     a.c_rec = P<u32x4>(c, B_CREC);
+    a.c_rec1 = crec1(c);
     a.counters = (unsigned long long*)cnt;
     a.filt_hb = (uint32_t)((flen ? flen - 1 : 0) >> 32);
     TRY(ensure(c, B_SPAN_FIRST, (n_spans + 1) * 4));
@@ -1131,7 +1055,7 @@ static int set_single_root(Ctx* c, uint64_t t) {
 static int alloc_index(Ctx* c, uint64_t n_cap, uint32_t log2_nbk) {
   const uint64_t nbk = (uint64_t)1 << log2_nbk;
   TRY(ensure(c, B_HOFF, (nbk + GLUE_BLOCKS) * 4));
-  TRY(ensure(c, B_SKEY, nbk * IDX_TCAP * 16));
+  TRY(ensure(c, B_SKEY, nbk * IDX_TCAP * 8));
   TRY(ensure_z(c, B_LATEST8, n_cap + 1));  // zero on (re)allocation: no entry carries a live generation
   return 0;
 }
@@ -1160,7 +1084,7 @@ static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
   ia.log2_nbk = log2_nbk;
   ia.bfill = P<uint32_t>(c, B_HOFF);
   ia.ccount = ia.bfill + ((size_t)1 << log2_nbk);
-  ia.srec = P<u64x2>(c, B_SKEY);
+  ia.srec = P<uint64_t>(c, B_SKEY);
   ia.latest = P<uint8_t>(c, B_LATEST8);
   ia.lgen = c->lgen;
   return ia;
@@ -1284,6 +1208,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     a.span_count = P<uint32_t>(c, B_SPAN_COUNT) - s_lo;
     a.c_m = P<uint64_t>(c, B_CM);  // wave regions, indexed by the wave of this launch
     a.c_rec = P<u32x4>(c, B_CREC);
+    a.c_rec1 = crec1(c);
     a.span_first = P<uint32_t>(c, B_SPAN_FIRST) - s_lo;
     a.wcap = wcap;
     a.counters = (unsigned long long*)cnt;
@@ -1383,6 +1308,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       f.flen = flen;
       f.c_m = a.c_m;
       f.c_rec = a.c_rec;
+      f.c_rec1 = a.c_rec1;
       f.tile = a.tile;
       f.no_crc = (flags & SRD_FLAG_NO_CRC) ? 1 : 0;
       f.coff = coff;

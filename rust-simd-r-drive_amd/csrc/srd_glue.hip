@@ -379,7 +379,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void check_kernel(ShapeArgs a) {
       const bool plinked = marks ? hp[r] == a.gen : (cp[r] & ~0xffffffffull) == tag;
       if (p == PAR_ROOT) {
         atomicAdd(&a.plan->nroot, 1u);
-        const u32x4 r0 = a.c_rec[2 * g[r]];
+        const u32x4 r0 = a.c_rec[g[r]];
         a.plan->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
       } else if (p < 0 || !((uint64_t)p == start || (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
         fail = true;  // dangling: the chain through g is broken (only the start node can get here)
@@ -421,7 +421,7 @@ struct IdxArgs {
   // Each block claims a range per bucket with one atomicAdd on bfill[k] (no
   // histogram scan).  bfill (nbk) is zero before the claims.
   uint32_t* bfill;
-  u64x2* srec;           // (key, chain index) per entry, in its bucket's range
+  uint64_t* srec;        // idx_rec(key, chain index) per entry, in its bucket's range
   uint8_t* latest;       // [n] == lgen: NOT the latest entry of its key (idx_dedup writes only those)
   uint8_t lgen;          // this build's generation (1..255; the host clears the array on wrap)
   uint32_t alias;        // fused pass: with no non-latest entry idx_emit writes nothing (Plan::idx_alias)
@@ -464,6 +464,15 @@ __device__ __forceinline__ void block_prefix_n(const uint32_t* part, uint32_t np
 __device__ __forceinline__ uint32_t idx_bucket(uint64_t key, uint32_t log2_nbk) {
   return (uint32_t)(xxh3_64_u64(key) >> (64 - log2_nbk));
 }
+// A bucket record in 8 bytes: the chain index in the high word, the low word
+// of the key's Xxh3BuildHasher hash (xxh3_64_u64, key_indexer.rs:98-124 hashes
+// with it; its top bits are the bucket) in the low word.  idx_dedup
+// deduplicates by that 32-bit partial key and checks every entry that loses to
+// another one against the full key_hash (the chain's key array): a partial
+// match of two different keys is detected there and the bucket is redone with
+// the full keys.  16-byte (key, index) records wrote and read 8 bytes more per
+// entry.
+__device__ __forceinline__ uint64_t idx_rec(uint64_t hh, uint64_t c) { return (c << 32) | (uint32_t)hh; }
 
 // block ranks of R rounds of flags at once (one LDS exchange): round r's
 // flags rank after every flag of rounds < r; wsum is LDS[R * NW]
@@ -870,7 +879,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
             const bool plinked = (cp[r] & ~0xffffffffull) == tag;
             if (p == PAR_ROOT) {
               nr++;
-              const u32x4 r0 = a.c_rec[2 * g[r]];
+              const u32x4 r0 = a.c_rec[g[r]];
               s_root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);  // (any one: nroot != 1 fails the call)
             } else if (p < 0 || !(((uint64_t)p == s1 - 1 && a.c_m[p] == top - 20) ||
                                   (plinked && (pp[r] >= 0 || pp[r] == PAR_ROOT)))) {
@@ -1020,13 +1029,13 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
           fl[r] = i < n && a.flag[gi[r]];
           par[r] = a.d_par[gi[r]];
           e[r].mo = f.c_m[gi[r]];
-          const u32x4 r0 = f.c_rec[2 * gi[r]], r1 = f.c_rec[2 * gi[r] + 1];
+          const u32x4 r0 = f.c_rec[gi[r]], r1 = f.c_rec1[gi[r]];
           e[r].p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-          kh[r] = (uint64_t)r0[2] | ((uint64_t)r0[3] << 32);
-          e[r].crc_st = r1[0];
-          e[r].sxv = r1[1];
-          e[r].fl = r1[3];
-          psuf[r] = r1[2];
+          kh[r] = (uint64_t)r1[0] | ((uint64_t)r1[1] << 32);
+          e[r].crc_st = r0[3];
+          e[r].sxv = r1[2];
+          e[r].fl = r0[2];
+          psuf[r] = r1[3];
         }
         uint32_t rank[FIN_R], tot = 0;
 #pragma unroll
@@ -1059,9 +1068,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
 #pragma unroll
           for (int r = 0; r < FIN_R; r++)
             if (need[r]) {
-              const u32x4 pr1 = f.c_rec[2 * (uint64_t)par[r] + 1];
-              e[r].pfl = pr1[3];
-              e[r].psuf = pr1[2];
+              e[r].pfl = f.c_rec[par[r]][2];
+              e[r].psuf = f.c_rec1[par[r]][3];
             }
         }
         c_fl = (uint32_t)__builtin_amdgcn_readlane(e[FIN_R - 1].fl, 63);
@@ -1154,12 +1162,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
         fl[r] = i < c1 && a.flag[gi[r]];
         par[r] = a.d_par[gi[r]];
         e[r].mo = f.c_m[gi[r]];
-        const u32x4 r0 = f.c_rec[2 * gi[r]], r1 = f.c_rec[2 * gi[r] + 1];
+        const u32x4 r0 = f.c_rec[gi[r]], r1 = f.c_rec1[gi[r]];
         e[r].p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-        kh[r] = (uint64_t)r0[2] | ((uint64_t)r0[3] << 32);
-        e[r].crc_st = r1[0];
-        e[r].sxv = r1[1];
-        e[r].fl = r1[3];
+        kh[r] = (uint64_t)r1[0] | ((uint64_t)r1[1] << 32);
+        e[r].crc_st = r0[3];
+        e[r].sxv = r1[2];
+        e[r].fl = r0[2];
       }
       uint32_t rank[FIN_R], tot = 0;
 #pragma unroll
@@ -1174,9 +1182,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
       // parent record: its suffix comes from the per-tile values (start 0)
 #pragma unroll
       for (int r = 0; r < FIN_R; r++) {
-        const u32x4 pr1 = f.c_rec[2 * (fl[r] && par[r] >= 0 ? (uint64_t)par[r] : gi[r]) + 1];
-        e[r].pfl = par[r] >= 0 ? pr1[3] : (3u << F_SUF_SHIFT);
-        e[r].psuf = pr1[2];
+        const uint64_t pg = fl[r] && par[r] >= 0 ? (uint64_t)par[r] : gi[r];
+        e[r].pfl = par[r] >= 0 ? f.c_rec[pg][2] : (3u << F_SUF_SHIFT);
+        e[r].psuf = f.c_rec1[pg][3];
         // idle lanes read the last tile's values (resident in span mode too)
         const uint64_t mo = fl[r] ? e[r].mo : f.flen - 1;
         const uint64_t st0 = !fl[r] ? mo : (e[r].fl & F_TOMB) ? e[r].p : e[r].p + prepad64(e[r].p);
@@ -1237,10 +1245,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     clo = troot ? 0 : a.coff + before;
     chi = troot ? (blockIdx.x == 0 ? 1 : 0) : bend;
     if (!troot && root_block && a.coff && threadIdx.x == 0) {
-      const uint64_t k0 = f.o_kh[0];
-      const uint32_t bk = idx_bucket(k0, log2_nbk);
+      const uint64_t h0 = xxh3_64_u64(f.o_kh[0]);
+      const uint32_t bk = (uint32_t)(h0 >> (64 - log2_nbk));
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
-      if (pos < IDX_TCAP) ia.srec[(uint64_t)bk * IDX_TCAP + pos] = u64x2{k0, 0};
+      if (pos < IDX_TCAP) ia.srec[(uint64_t)bk * IDX_TCAP + pos] = idx_rec(h0, 0);
     }
   } else {
     const uint64_t n_chain = troot ? 1 : a.coff + total;
@@ -1259,9 +1267,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_finalize_kernel(ShapeArgs
     for (int r = 0; r < SR; r++) {
       const uint64_t c = base + (uint64_t)r * CHAIN_THREADS + threadIdx.x;
       if (c >= chi) break;
-      const uint32_t bk = idx_bucket(k[r], log2_nbk);
+      const uint64_t hh = xxh3_64_u64(k[r]);
+      const uint32_t bk = (uint32_t)(hh >> (64 - log2_nbk));
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
-      if (pos < IDX_TCAP) ia.srec[(uint64_t)bk * IDX_TCAP + pos] = u64x2{k[r], c};  // else: idx_dedup flags the bucket
+      if (pos < IDX_TCAP) ia.srec[(uint64_t)bk * IDX_TCAP + pos] = idx_rec(hh, c);  // else: idx_dedup flags the bucket
     }
   }
   GLUE_STAMP(6);
@@ -1291,10 +1300,10 @@ __global__ __launch_bounds__(256) void idx_hist_scatter_kernel(IdxArgs a) {
   }
   __syncthreads();
   for (uint64_t c = lo + threadIdx.x; c < hi; c += blockDim.x) {
-    const uint64_t k = a.kh[c];
-    const uint32_t bk = (uint32_t)(xxh3_64_u64(k) >> (64 - a.log2_nbk));
+    const uint64_t hh = xxh3_64_u64(a.kh[c]);
+    const uint32_t bk = (uint32_t)(hh >> (64 - a.log2_nbk));
     const uint32_t pos = atomicAdd(&lds_u32[bk], 1u);
-    if (pos < IDX_TCAP) a.srec[(uint64_t)bk * IDX_TCAP + pos] = u64x2{k, c};  // else: idx_dedup flags the bucket
+    if (pos < IDX_TCAP) a.srec[(uint64_t)bk * IDX_TCAP + pos] = idx_rec(hh, c);  // else: idx_dedup flags the bucket
   }
 }
 
@@ -1320,11 +1329,12 @@ __device__ __forceinline__ void publish_outcome(const IdxArgs& a, const Plan* pl
 // IDX_TCAP, so any bucket that fits its capacity fits the table (load <= 2/3;
 // with the bucket count's average fill of 640-1280 entries, <= ~0.45)
 constexpr int DD_SLOTS = 3 * IDX_TCAP / 2;
+constexpr uint32_t DD_EMPTY32 = 0xFFFFFFFFu;  // an empty partial-key slot (a partial key equal to it is stored as - 1)
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void idx_dedup_kernel(IdxArgs a, FinArgs f) {
   __shared__ unsigned long long dd_lds[DD_SLOTS + DD_SLOTS / 2];
   unsigned long long* const keys = dd_lds;
   uint32_t* const vals = (uint32_t*)(dd_lds + DD_SLOTS);
-  __shared__ uint32_t special;
+  __shared__ uint32_t special, collide;
   if (f.n_slow) {
     const unsigned long long ns = *f.n_slow;
     constexpr uint32_t NW = 512 / 64;
@@ -1351,53 +1361,94 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   // cleared) and their slots stay in registers between the insert and the
   // lookup pass
   constexpr int DR = IDX_TCAP / 512;
-  u64x2 rec[DR];
+  uint64_t rec[DR];
   uint32_t slot[DR];
+  bool in[DR], mark[DR];
 #pragma unroll
   for (int r = 0; r < DR; r++) {
     const uint64_t i = lo + (uint64_t)r * 512 + threadIdx.x;
-    rec[r] = a.srec[i < hi ? i : lo];
+    in[r] = i < hi;
+    rec[r] = a.srec[in[r] ? i : lo];
+    mark[r] = false;
   }
   uint32_t slots = 64;
   while (slots < 2 * (hi - lo) && slots < 2048) slots <<= 1;  // load <= 1/2 up to 1024 entries
   const bool pw2 = slots >= 2 * (hi - lo);  // else DD_SLOTS, the slot by a multiply-high
   if (!pw2) slots = DD_SLOTS;
   const uint32_t M = slots - 1;
-  for (uint32_t i = threadIdx.x; i < slots; i += blockDim.x) { keys[i] = IDX_EMPTY; vals[i] = 0; }
-  if (threadIdx.x == 0) special = 0;
+  auto slot_of = [&](uint32_t h) { return pw2 ? h & M : (uint32_t)(((uint64_t)h * DD_SLOTS) >> 32); };
+  // pass 1: latest-wins by the 32-bit partial key (the records' low words)
+  uint32_t* const hkeys = (uint32_t*)dd_lds;  // (the exact pass's 64-bit key words reused)
+  for (uint32_t i = threadIdx.x; i < slots; i += blockDim.x) { hkeys[i] = DD_EMPTY32; vals[i] = 0; }
+  if (threadIdx.x == 0) { special = 0; collide = 0; }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < DR; r++) {
-    if (lo + (uint64_t)r * 512 + threadIdx.x >= hi) break;
-    const uint64_t key = rec[r][0];
-    const uint32_t v = (uint32_t)rec[r][1] + 1;
-    if (key == IDX_EMPTY) { atomicMax(&special, v); continue; }
-    const uint32_t h = (uint32_t)xxh3_64_u64(key);
-    uint32_t s = pw2 ? h & M : (uint32_t)(((uint64_t)h * DD_SLOTS) >> 32);
+    if (!in[r]) break;
+    const uint32_t h = (uint32_t)rec[r], hk = h == DD_EMPTY32 ? DD_EMPTY32 - 1 : h;
+    const uint32_t v = (uint32_t)(rec[r] >> 32) + 1;
+    uint32_t s = slot_of(h);
     while (true) {
-      const unsigned long long old = atomicCAS(&keys[s], (unsigned long long)IDX_EMPTY, (unsigned long long)key);
-      if (old == IDX_EMPTY || old == key) { atomicMax(&vals[s], v); break; }
+      const uint32_t old = atomicCAS(&hkeys[s], DD_EMPTY32, hk);
+      if (old == DD_EMPTY32 || old == hk) { atomicMax(&vals[s], v); break; }
       s = s == M ? 0u : s + 1;
     }
     slot[r] = s;
   }
   __syncthreads();
-  // latest flags, and the per-chunk count of the entries that are NOT the
-  // latest of their key (idx_emit's prefix: position = c - non-latest before
-  // c; a store without overwrites makes no atomics here)
+  // an entry that lost to a later one is NOT its key's latest only if the
+  // winner carries the same full key (the chain's key array); otherwise two
+  // keys share the partial key: the bucket is redone with the full keys
+#pragma unroll
+  for (int r = 0; r < DR; r++) {
+    if (!in[r]) break;
+    const uint32_t c = (uint32_t)(rec[r] >> 32), best = vals[slot[r]];
+    if (best != c + 1) {
+      if (a.kh[c] == a.kh[best - 1]) mark[r] = true;
+      else collide = 1;
+    }
+  }
+  __syncthreads();
+  if (collide) {  // (uniform) pass 2: the full keys, gathered
+    uint64_t key[DR];
+#pragma unroll
+    for (int r = 0; r < DR; r++) key[r] = in[r] ? a.kh[(uint32_t)(rec[r] >> 32)] : 0;
+    for (uint32_t i = threadIdx.x; i < slots; i += blockDim.x) { keys[i] = IDX_EMPTY; vals[i] = 0; }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < DR; r++) {
+      if (!in[r]) break;
+      const uint32_t v = (uint32_t)(rec[r] >> 32) + 1;
+      if (key[r] == IDX_EMPTY) { atomicMax(&special, v); continue; }
+      uint32_t s = slot_of((uint32_t)xxh3_64_u64(key[r]));
+      while (true) {
+        const unsigned long long old = atomicCAS(&keys[s], (unsigned long long)IDX_EMPTY, (unsigned long long)key[r]);
+        if (old == IDX_EMPTY || old == key[r]) { atomicMax(&vals[s], v); break; }
+        s = s == M ? 0u : s + 1;
+      }
+      slot[r] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < DR; r++) {
+      if (!in[r]) break;
+      const uint32_t c = (uint32_t)(rec[r] >> 32);
+      mark[r] = (key[r] == IDX_EMPTY ? special : vals[slot[r]]) != c + 1;
+    }
+  }
+  // the per-chunk count of the entries that are NOT the latest of their key
+  // (idx_emit's prefix: position = c - non-latest before c; a store without
+  // overwrites makes no atomics here).  Only the (rare) non-latest entries are
+  // marked: a byte store per entry, scattered over the chain, costs
+  // partial-line writes for every key
   const uint64_t n = idx_n(a);
   const uint64_t ch = n ? (n + GLUE_BLOCKS - 1) / GLUE_BLOCKS : 1;  // chunk_of's chunk at GLUE_BLOCKS blocks
 #pragma unroll
   for (int r = 0; r < DR; r++) {
-    if (lo + (uint64_t)r * 512 + threadIdx.x >= hi) break;
-    const uint32_t c = (uint32_t)rec[r][1];
-    const uint32_t best = rec[r][0] == IDX_EMPTY ? special : vals[slot[r]];
-    // only the (rare) non-latest entries are marked: a byte store per entry,
-    // scattered over the chain, costs partial-line writes for every key
-    if (best != c + 1) {
-      a.latest[c] = a.lgen;
-      atomicAdd(&a.ccount[c / ch], 1u);
-    }
+    if (!mark[r]) continue;
+    const uint32_t c = (uint32_t)(rec[r] >> 32);
+    a.latest[c] = a.lgen;
+    atomicAdd(&a.ccount[c / ch], 1u);
   }
 }
 

@@ -134,7 +134,10 @@ struct ScanArgs {
   uint32_t* tile;                  // [4*n_tiles]: half-tile partials h_0, h_1, SX_32 (tile_sx())
   uint32_t* span_count;
   uint64_t* c_m;                   // [n_spans*cap] candidate metadata offsets
-  u32x4* c_rec;                    // [2*n_spans*cap] {p, key_hash}, {crc, sxm, suf, flags}
+  // the records in two 16-byte halves (structure of arrays): c_rec[g] = {p,
+  // flags, crc_stored} -- all link2 reads --, c_rec1[g] = {key_hash, sxm, suf}
+  u32x4* c_rec;                    // [slots] {p_lo, p_hi, flags, crc}
+  u32x4* c_rec1;                   // [slots] {kh_lo, kh_hi, sxm, suf}
   unsigned long long* counters;    // [0] max root tail, [1] find_top's tail (optimistic pass), [2] overflow
   uint32_t filt_hb;               // (file_len-1) >> 32: bound of a node's p-byte 4 (p < file_len < 2^40)
   // span mode (entry-range shard): tiles [k_lo, n_tiles) are resident, k_lo a
@@ -264,11 +267,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // ((pos*16+nib)*64 + l): every lane its own bank, conflict-free) and one
 // 24-dword window per wave for the cooperative candidate check.
 constexpr int SCAN_WAVES_V2 = 16;
-// scan_kernel's F1 (straight-line first flagged line) default
-#ifndef SRD_FLAG1
-#define SRD_FLAG1 0
-#endif
-constexpr bool kFlag1 = SRD_FLAG1 != 0;
 struct alignas(2048) ScanLds {
   // the last slice-by-4 step of 16-byte chain q (q < 3) with the chain's
   // join shift folded in: byte i of s -> (b << 8i) * x^(32 + 128 (3 - q)),
@@ -295,24 +293,11 @@ __device__ __forceinline__ uint32_t tab_lookup(const ScanLds& L, uint32_t s, uin
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // one v_bitop3_b32
 }
-__device__ __forceinline__ uint32_t crc_line1(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
-  // byte j of S0 = selector 4+j; S1 bytes 0 and 2 = selectors 0 and 2; 0x0c = zero
-  constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
-  uint32_t s = d[0];
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    const uint32_t t3 = tab_lookup(L, s, R[3], SEL0), t2 = tab_lookup(L, s, R[2], SEL1);
-    const uint32_t t1 = tab_lookup(L, s, R[1], SEL2), t0 = tab_lookup(L, s, R[0], SEL3);
-    s = xor3(xor3(t3, t2, j < 15 ? d[j < 15 ? j + 1 : 15] : 0u), t1, t0);  // 2 VALU per step
-  }
-  return s;
-}
-
 __device__ __forceinline__ uint32_t mulfix(uint32_t v, const uint32_t* __restrict__ m) {
   return m[v & 0xff] ^ m[256 + ((v >> 8) & 0xff)] ^ m[512 + ((v >> 16) & 0xff)] ^ m[768 + (v >> 24)];
 }
-// Same CRC as crc_line1 with 4 independent 16-byte chains (4 dependent LDS
-// round trips instead of 16): raw(line) = a x^384 ^ b x^256 ^ c x^128 ^ d for
+// The raw CRC-32 of a lane's 64-byte line by slice-by-4 as 4 independent
+// 16-byte chains (4 dependent LDS round trips instead of 16): raw(line) = a x^384 ^ b x^256 ^ c x^128 ^ d for
 // the chains' raw CRCs a..d, and chain q's last step looks its bytes up in
 // tables that already carry the x^(128 (3 - q)) shift (ScanLds::last), so the
 // joins cost no lookups of their own.
@@ -337,28 +322,6 @@ __device__ __forceinline__ uint32_t crc_line4(const uint32_t (&d)[16], const Sca
   v[3] = xor3(tab_lookup(L, s[3], R[3], SEL0), tab_lookup(L, s[3], R[2], SEL1), tab_lookup(L, s[3], R[1], SEL2)) ^
          tab_lookup(L, s[3], R[0], SEL3);
   return xor3(v[0], v[1], v[2]) ^ v[3];
-}
-// Two 32-byte chains (8 dependent LDS round trips instead of 4, but 4
-// lookups per line in the unreplicated shifted tables instead of 12):
-// raw(line) = a x^256 ^ b; chain a's last step reads ScanLds::last's chain-1
-// tables (shift x^(128 (3 - 1)) = x^256)
-__device__ __forceinline__ uint32_t crc_line2(const uint32_t (&d)[16], const ScanLds& L, const uint32_t (&R)[4]) {
-  constexpr uint32_t SEL0 = 0x0c020400u, SEL1 = 0x0c020500u, SEL2 = 0x0c020600u, SEL3 = 0x0c020700u;
-  uint32_t s[2] = {d[0], d[8]};
-#pragma unroll
-  for (int j = 0; j < 7; j++) {
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const uint32_t t3 = tab_lookup(L, s[q], R[3], SEL0), t2 = tab_lookup(L, s[q], R[2], SEL1);
-      const uint32_t t1 = tab_lookup(L, s[q], R[1], SEL2), t0 = tab_lookup(L, s[q], R[0], SEL3);
-      s[q] = xor3(xor3(t3, t2, d[8 * q + j + 1]), t1, t0);
-    }
-  }
-  const uint32_t* m = L.last + 1024 * 1;
-  const uint32_t v0 = xor3(m[s[0] & 0xff], m[256 + ((s[0] >> 8) & 0xff)], m[512 + ((s[0] >> 16) & 0xff)]) ^ m[768 + (s[0] >> 24)];
-  const uint32_t v1 = xor3(tab_lookup(L, s[1], R[3], SEL0), tab_lookup(L, s[1], R[2], SEL1), tab_lookup(L, s[1], R[1], SEL2)) ^
-                      tab_lookup(L, s[1], R[0], SEL3);
-  return v0 ^ v1;
 }
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -499,183 +462,6 @@ __device__ __forceinline__ void crc_lane_bases(uint32_t (&R)[4], int lane) {
   for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
 }
 
-// ---- the rotated layout (the occupancy variants of scan_kernel) ----
-// ScanLds replicates each slice-by-4 table 32 times (lane l reads copy l % 32:
-// conflict-free, 128 KiB), so one 16-wave block fills the CU's LDS.  The four
-// lookups of one slice-by-4 step only have to go to 32 distinct banks per
-// 32-lane group, not to the same table: in lookup slot j lane l takes byte
-// k = (j + l) & 3 of the state and table T_(3-k), so the 32 lanes of a group
-// read 4 different tables, 8 lanes each, and 8 replicas per table suffice.
-// Row b (256 B) of `tn`: words 0-31 = T_t[b] replica r at word 8 t + r (bank
-// 8 t + r; r = (l >> 2) & 7); words 32-63 of rows 0-127 = the lane-weight
-// nibble table (row pos * 16 + nb, word 32 + l % 32: bank l % 32).  64 KiB
-// for both (ScanLds: 144 KiB), so two blocks fit a CU.
-template <int NW>
-struct alignas(4096) ScanLdsR {
-  uint32_t last[3 * 4 * 256];  // 12 KiB, unreplicated (as ScanLds::last), at offset 0
-  uint32_t tn[256 * 64];       // 64 KiB, 4 KiB-aligned (lane_weight_rot ORs nibble bits 8-11 into the base)
-  uint32_t win[NW][24];
-  uint64_t s_root[NW], s_ovf[NW];
-  uint32_t s_last;
-};
-// lane constants of the rotated lookups: Rr byte k = the row offset of
-// table T_(3-k), replica (l >> 2) & 7; SL[j] = v_perm selector of slot j
-// (address byte 0 = Rr byte k, byte 1 = state byte k, bytes 2-3 zero)
-__device__ __forceinline__ void rot_lane_consts(uint32_t& Rr, uint32_t (&SL)[4], int lane) {
-  const uint32_t r4 = 4u * (((uint32_t)lane >> 2) & 7u);
-  Rr = (96u + r4) | ((64u + r4) << 8) | ((32u + r4) << 16) | (r4 << 24);
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint32_t k = ((uint32_t)j + (uint32_t)lane) & 3u;
-    SL[j] = 0x0c0c0000u | ((4u + k) << 8) | k;
-  }
-}
-__device__ __forceinline__ uint32_t rot_lookup(const uint32_t* tn, uint32_t s, uint32_t Rr, uint32_t sel) {
-  return *(const uint32_t*)((const char*)tn + __builtin_amdgcn_perm(s, Rr, sel));
-}
-// crc_line4 over the rotated tables: the same four 16-byte chains, the same
-// shifted last steps (chains 0-2 through `last`), the same raw line CRC
-template <class L>
-__device__ __forceinline__ uint32_t crc_line4_rot(const uint32_t (&d)[16], const L& lds, uint32_t Rr,
-                                                  const uint32_t (&SL)[4]) {
-  uint32_t s[4] = {d[0], d[4], d[8], d[12]};
-#pragma unroll
-  for (int j = 0; j < 3; j++) {
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const uint32_t t0 = rot_lookup(lds.tn, s[q], Rr, SL[0]), t1 = rot_lookup(lds.tn, s[q], Rr, SL[1]);
-      const uint32_t t2 = rot_lookup(lds.tn, s[q], Rr, SL[2]), t3 = rot_lookup(lds.tn, s[q], Rr, SL[3]);
-      s[q] = xor3(xor3(t0, t1, d[4 * q + j + 1]), t2, t3);
-    }
-  }
-  uint32_t v[4];
-#pragma unroll
-  for (int q = 0; q < 3; q++) {
-    const uint32_t* m = lds.last + 1024 * q;
-    v[q] = xor3(m[s[q] & 0xff], m[256 + ((s[q] >> 8) & 0xff)], m[512 + ((s[q] >> 16) & 0xff)]) ^ m[768 + (s[q] >> 24)];
-  }
-  v[3] = xor3(rot_lookup(lds.tn, s[3], Rr, SL[0]), rot_lookup(lds.tn, s[3], Rr, SL[1]),
-              rot_lookup(lds.tn, s[3], Rr, SL[2])) ^
-         rot_lookup(lds.tn, s[3], Rr, SL[3]);
-  return xor3(v[0], v[1], v[2]) ^ v[3];
-}
-// lane_weight_or over the rotated layout's nibble rows: nibble pos of c at
-// address bits 8-11, pos in the ds_read offset (lbase = tn + 128 + 4 (l % 32))
-__device__ __forceinline__ uint32_t lane_weight_rot(uint32_t c, uint32_t lbase) {
-  uint32_t v[8];
-#pragma unroll
-  for (int pos = 0; pos < 8; pos++) {
-    const int sh = 4 * pos - 8;
-    const uint32_t x = sh < 0 ? c << (-sh) : c >> sh;
-    v[pos] = lds_ld(((x & 0xF00u) | lbase) + pos * 4096);
-  }
-  return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6] ^ v[7]);
-}
-// the rotated layout's tables into LDS (all NW * 64 threads; ends with a
-// block barrier): every thread's global loads first, then its LDS stores
-template <int NW>
-__device__ __forceinline__ void load_rot_lds(ScanLdsR<NW>& lds) {
-  constexpr uint32_t T = NW * 64, NT = (1024 + T - 1) / T, NL = (768 + T - 1) / T;
-  const uint32_t u = threadIdx.x;
-  uint32_t tv[NT];
-  u32x4 nv[NT], lv[NL];
-#pragma unroll
-  for (uint32_t i = 0; i < NT; i++) {
-    const uint32_t x = min(u + i * T, 1023u);
-    tv[i] = g_tabs.tab[x >> 8][x & 255];
-    nv[i] = ((const u32x4*)g_tabs.nib)[x];  // 16 B of row x >> 3 (32 words per row)
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < NL; i++) lv[i] = ((const u32x4*)&g_tabs.last[0][0][0])[min(u + i * T, 767u)];
-#pragma unroll
-  for (uint32_t i = 0; i < NT; i++) {
-    const uint32_t x = u + i * T;
-    if (x < 1024) {
-      u32x4* tr = (u32x4*)(lds.tn + (x & 255) * 64 + 8 * (x >> 8));  // T_t[b], replicas 0-7
-      tr[0] = u32x4{tv[i], tv[i], tv[i], tv[i]};
-      tr[1] = u32x4{tv[i], tv[i], tv[i], tv[i]};
-      *(u32x4*)(lds.tn + (x >> 3) * 64 + 32 + 4 * (x & 7)) = nv[i];
-    }
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < NL; i++)
-    if (u + i * T < 768) ((u32x4*)lds.last)[u + i * T] = lv[i];
-  __syncthreads();
-}
-
-// ---- the rotated last steps (scan_kernel V 30) ----
-// ScanLds's 12 last-step tables are unreplicated: their 12 lookups per line
-// make ~53 bank-conflict cycles of the tile's ~271 LDS cycles.  The rotation
-// of ScanLdsR applies to them as well (a last step is a slice-by-4 step over
-// shifted tables), at 8 replicas per table: 3 chains x 32 KiB.  Two 64 KiB
-// row arrays with 256-byte rows hold all rotated tables (the v_perm address:
-// byte 1 = the state byte = the row, byte 0 = Rr's word offset, + 128 for
-// words 32-63): x = T (words 0-31) and chain 2's last tables (32-63), y =
-// chain 0's (0-31) and chain 1's (32-63); the lane-weight nibble tables keep
-// ScanLds's layout.  One 16-wave block per CU as the product (146 KiB).
-template <int NW>
-struct alignas(4096) ScanLdsR3 {
-  uint32_t x[256 * 64];
-  uint32_t y[256 * 64];
-  uint32_t nib[8 * 16 * 32];  // 2 KiB-aligned (lane_weight_or)
-  uint32_t win[NW][24];
-  uint64_t s_root[NW], s_ovf[NW];
-  uint32_t s_last;
-};
-template <int NW>
-__device__ __forceinline__ void load_rot3_lds(ScanLdsR3<NW>& lds) {
-  static_assert(NW * 64 == 1024, "one word of each table per thread");
-  const uint32_t u = threadIdx.x;  // table word u: t = u >> 8, b = u & 255
-  const uint32_t tv = g_tabs.tab[u >> 8][u & 255];
-  const u32x4 nv = ((const u32x4*)g_tabs.nib)[u];
-  uint32_t lv[3];
-#pragma unroll
-  for (int q = 0; q < 3; q++) lv[q] = g_tabs.last[q][u >> 8][u & 255];  // chain q, byte position u >> 8
-  const uint32_t t = u >> 8, b = u & 255;
-  // T_t[b] -> row b word 8 t + r; last_q[i][b] (byte i) -> word 8 (3 - i) + r (+ 32 for chain 1 / 2)
-  u32x4* tr = (u32x4*)(lds.x + b * 64 + 8 * t);
-  tr[0] = u32x4{tv, tv, tv, tv};
-  tr[1] = u32x4{tv, tv, tv, tv};
-  const uint32_t wl = 8 * (3 - t);
-  u32x4* l0 = (u32x4*)(lds.y + b * 64 + wl);
-  l0[0] = u32x4{lv[0], lv[0], lv[0], lv[0]};
-  l0[1] = u32x4{lv[0], lv[0], lv[0], lv[0]};
-  u32x4* l1 = (u32x4*)(lds.y + b * 64 + 32 + wl);
-  l1[0] = u32x4{lv[1], lv[1], lv[1], lv[1]};
-  l1[1] = u32x4{lv[1], lv[1], lv[1], lv[1]};
-  u32x4* l2 = (u32x4*)(lds.x + b * 64 + 32 + wl);
-  l2[0] = u32x4{lv[2], lv[2], lv[2], lv[2]};
-  l2[1] = u32x4{lv[2], lv[2], lv[2], lv[2]};
-  ((u32x4*)lds.nib)[u] = nv;
-  __syncthreads();
-}
-// crc_line4 with every lookup rotated (conflict-free): chains 0-2's last
-// steps through their rotated shifted tables (Rr + 128 per byte: words 32-63)
-template <class L>
-__device__ __forceinline__ uint32_t crc_line4_rot3(const uint32_t (&d)[16], const L& lds, uint32_t Rr,
-                                                   const uint32_t (&SL)[4]) {
-  uint32_t s[4] = {d[0], d[4], d[8], d[12]};
-#pragma unroll
-  for (int j = 0; j < 3; j++) {
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const uint32_t t0 = rot_lookup(lds.x, s[q], Rr, SL[0]), t1 = rot_lookup(lds.x, s[q], Rr, SL[1]);
-      const uint32_t t2 = rot_lookup(lds.x, s[q], Rr, SL[2]), t3 = rot_lookup(lds.x, s[q], Rr, SL[3]);
-      s[q] = xor3(xor3(t0, t1, d[4 * q + j + 1]), t2, t3);
-    }
-  }
-  const uint32_t Rh = Rr + 0x80808080u;  // words 32-63 of the rows
-  const uint32_t* base[4] = {lds.y, lds.y, lds.x, lds.x};
-  const uint32_t rr[4] = {Rr, Rh, Rh, Rr};
-  uint32_t v[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++)
-    v[q] = xor3(rot_lookup(base[q], s[q], rr[q], SL[0]), rot_lookup(base[q], s[q], rr[q], SL[1]),
-                rot_lookup(base[q], s[q], rr[q], SL[2])) ^
-           rot_lookup(base[q], s[q], rr[q], SL[3]);
-  return xor3(v[0], v[1], v[2]) ^ v[3];
-}
-
 // recover_valid_chain's outer loop (data_store.rs:388-479) walks the cursor t
 // down from file_len and skips every t whose metadata fails its first test,
 // entry_start < metadata_offset (:390-420; entry_start = prev + prepad(prev),
@@ -718,12 +504,6 @@ __device__ __forceinline__ uint64_t find_top(const uint8_t* file, uint64_t flen,
   return 0;
 }
 
-// WIDE: stores above 2^40 bytes (prev offsets up to 48 bits, key_indexer.rs:12-15):
-// the level-1 filter looks for the two zero bytes m+14, m+15 at any alignment
-// V: the variant (0 = the product build; others are A/B'd inside one context
-// by SRD_DEBUG_API builds: 1 = F1 flipped, 2 = F1 flipped with its staging
-// and node test after the CRC at priority 2, 3 = the line CRC as two 32-byte
-// chains)
 // Link record r of scan wave w (slot w*wcap + r; the optimistic pass, after
 // the scan): the deferred node test of a single-candidate record
 // (data_store.rs:404-470), its parent -- the previous record in file order
@@ -749,14 +529,14 @@ __device__ void link_record(const ScanArgs& a, uint64_t w, uint64_t r) {
   // a whole block's critical path)
   const bool hp2 = r >= 2;
   const uint64_t m = a.c_m[gi], mprev = hp ? a.c_m[gprev] : 0, mprev2 = hp2 ? a.c_m[gi - 2] : 0;
-  const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
+  const u32x4 r0 = a.c_rec[gi];  // {p, flags, crc}: the record's half link2 needs
   const uint64_t p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
   bool node = true, tomb = false;
-  if (r1[3] & F_NT) {
+  if (r0[2] & F_NT) {
     // single-candidate record, deferred node test; F_ZB is the byte at m - 1,
     // the tombstone byte when p == m - 1
     const uint64_t dp = m - p;
-    tomb = dp == 1 && (r1[3] & F_ZB);
+    tomb = dp == 1 && (r0[2] & F_ZB);
     node = p >= 20 && p < m && (tomb || dp > prepad64(p));
   }
   const uint64_t mp = p - 20;  // p >= 20 for nodes
@@ -795,7 +575,7 @@ __device__ void link_record(const ScanArgs& a, uint64_t w, uint64_t r) {
       par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
     }
   }
-  if (tomb) a.c_rec[2 * gi + 1] = u32x4{r1[0], r1[1], r1[2], r1[3] | F_TOMB};
+  if (tomb) a.c_rec[gi] = u32x4{r0[0], r0[1], r0[2] | F_TOMB, r0[3]};
   a.d_par[gi] = (int32_t)par;
   if (par >= 0) atomicMax(&a.childof[par], claim_word(a.gen, gi));
 }
@@ -817,7 +597,7 @@ __global__ __launch_bounds__(256 * LINK_WPB) void link2_kernel(ScanArgs a, uint3
   for (uint64_t r = threadIdx.x % 256; r < nrec; r += 256) link_record(a, w, r);
 }
 
-// ---- coalesced nontemporal tile loads (scan_kernel V 31) ----
+// ---- coalesced nontemporal tile loads (the product scan's, round 5) ----
 // The scan's line-per-lane loads (lane l: 16 B at 64 l + 16 j) stream at
 // ~6.0-6.1 TB/s; loads whose every instruction reads 1 KiB contiguous, with
 // the nontemporal bit, at ~6.75 TB/s (tools/stream_map_probe.hip,
@@ -863,16 +643,6 @@ __device__ __forceinline__ void coal_bswap(uint32_t (&d)[16]) {  // register bit
     }
   }
 }
-// (V 40) the quarter in lane bits 4-5 instead: lane l = 16A + m loads 16 B at
-// 1024 j + 64 m + 16 A (quarter A of line 16 j + m; each instruction still
-// 1 KiB contiguous), and the permlane swaps alone put line L in lane L
-__device__ __forceinline__ uint32_t coal3_lane_off(int lane, int j) {
-  return 1024u * (uint32_t)j + 64u * ((uint32_t)lane & 15u) + 16u * ((uint32_t)lane >> 4);
-}
-__device__ __forceinline__ void coal3_to_lines(uint32_t (&d)[16]) {
-  coal_pswap<1, false>(d);
-  coal_pswap<2, true>(d);
-}
 __device__ __forceinline__ void coal_to_lines(uint32_t (&d)[16]) {
   coal_pswap<1, false>(d);
   coal_pswap<2, true>(d);
@@ -880,70 +650,32 @@ __device__ __forceinline__ void coal_to_lines(uint32_t (&d)[16]) {
   coal_bswap<8, 2>(d);
 }
 
-// The scan's geometry per variant (host and device): waves per block and
-// blocks per CU.  20 / 21: the rotated tables (ScanLdsR, 78 KiB) and a
-// 2-deep register ring, two blocks of 10 / 12 waves per CU = 5 / 6 waves per
-// SIMD (VGPR budget 96 / 80, amdgpu_waves_per_eu); 22: the rotated tables at
-// today's geometry (one 16-wave block per CU, 3-deep ring).
-// 23: the rotated tables, 2-deep ring, two 8-wave blocks per CU (4 waves
-// per SIMD, as 0: the geometry at equal occupancy); 24: the rotated tables
-// and the 2-deep ring in today's geometry.
 // line-per-lane tile loads (round 4's product): the scan of large stores
+// (scan_variant_for); one 16-wave block per CU for every variant
 constexpr int SCAN_LINES = 34;
-constexpr int scan_nw(int V) { return V == 20 ? 10 : V == 21 ? 12 : V == 23 ? 8 : 16; }
-constexpr int scan_bpc(int V) { return V == 20 || V == 21 || V == 23 ? 2 : 1; }
-constexpr int scan_wpe(int V) { return (scan_nw(V) * scan_bpc(V)) / 4; }
-// 25: the rotated tables alone (the product's global loads, not 20-24's
-// buffer loads); 26: the product with the record stores' descriptors made
-// uniform (readfirstlane: no waterfall loop, no f64 min) as 20-25 have them.
-constexpr bool scan_rot(int V) { return V >= 20 && V <= 25; }
+constexpr int scan_nw(int) { return SCAN_WAVES_V2; }
 
+// WIDE: stores above 2^40 bytes (prev offsets up to 48 bits, key_indexer.rs:12-15):
+// the level-1 filter looks for the two zero bytes m+14, m+15 at any alignment
 template <bool FULL, bool WIDE, int V = 0>
-__global__ __launch_bounds__(scan_nw(V) * 64) __attribute__((amdgpu_waves_per_eu(scan_wpe(V), scan_wpe(V))))
+__global__ __launch_bounds__(SCAN_WAVES_V2 * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void scan_kernel(ScanArgs a) {
-  constexpr int NW = scan_nw(V);
-  constexpr bool ROT = scan_rot(V);
-  constexpr bool ROT3 = V == 30;  // every lookup rotated, the product's geometry and loads
-  // the product (V 0) and 31-33 load tiles coalesced + nontemporal and
-  // transpose them in registers (coal_to_lines); SCAN_LINES (34) = round 4's
-  // line-per-lane loads, the product's for large stores (srd_api.hip
-  // scan_variant_for); 1-30 keep those loads (earlier experiments)
-  constexpr bool COALT = V == 0 || (V >= 31 && V <= 33) || (V >= 35 && V <= 37) || V == 40;
-  constexpr bool COAL3 = V == 40;  // the permlane-only transpose (coal3_lane_off)  // (32: with the 2-deep ring)
-  // timing-only store ablations (results wrong; the store instructions stay,
-  // their lanes out of range): 35 = no record stores, 36 = no tile-value
-  // stores, 37 = no {p, key_hash} half of c_rec (records of 24 B instead of 40)
-  constexpr bool NO_REC = V == 35, NO_TV = V == 36, NO_PK = V == 37;  // coalesced nontemporal tile loads + the in-register transpose
-  constexpr bool BUFLD = ROT && V != 25;       // tile loads as buffer loads (SGPR base, one lane offset)
-  constexpr bool UNISTORE = ROT || V == 26;    // uniform record-store descriptors
-  constexpr bool F1 = (V == 1 || V == 2) ? !kFlag1 : kFlag1;
-  constexpr bool F1_AFTER = V == 2;  // F1's staging + test after the CRC, at priority 2
-  // 3 = the line CRC as two 32-byte chains (crc_line2), 5 / 6 / 10 = each
-  // level's 16 lookups issued together (crc_line4_wide): line_crc below
-  constexpr bool RING2 = V == 4 || V == 5 || V == 20 || V == 21 || V == 23 || V == 24 || V == 32;  // a 2-deep register ring (one tile in flight), 16 VGPRs fewer
-  // timing-only ablations (wrong results; SRD_DEBUG_API's scan-only calls):
-  // 7 = the ring's loads alone (each tile XOR-folded), 8 = the whole tile
-  // body on two L1/L2-resident tiles per block (no HBM traffic)
-  constexpr bool MEMONLY = V == 7 || V == 12, NOHBM = V == 8;
-  // 9 = the previous tile's line-63 tail and SX_63 carried in SGPRs (no
-  // per-tile LDS store by lane 63; the f == 0 window takes them from there),
-  // 10 = 9 with the 16-wide CRC levels
-  constexpr bool SCARRY = V == 9 || V == 10;
-  // timing-only ablations (results not checked): 11 = coalesced tile loads
-  // (lane l, load j reads 16 B at 1024 j + 16 l), 12 = 11 memory-only
-  constexpr bool COAL = V == 11 || V == 12;
-  // 13 = timing-only: none of process()'s six per-tile stores (tile values,
-  // records, span counts) -- what their VMEM issue slots cost
-  constexpr bool NOSTORE = V == 13;
-  // 14 = the per-tile store points of round 3 (a store point after every
-  // tile instead of after every ring round)
-  constexpr bool TILE_SP = V == 14 || RING2;
+  constexpr int NW = SCAN_WAVES_V2;
+  // The product loads each tile coalesced + nontemporal and transposes it in
+  // registers (coal_to_lines); SCAN_LINES = round 4's line-per-lane loads
+  // (stores above Ctx::coal_max, srd_api.hip scan_variant_for).  Timing-only
+  // ablations of SRD_DEBUG_API builds (results wrong; tools/variant_ab.py):
+  // 7 = the ring's coalesced loads alone (each tile XOR-folded), 8 = the whole
+  // coalesced tile body on two L2-resident tiles per block (no HBM stream).
+  // Round 1-5's rejected variants (rotated tables, 2-deep ring, straight-line
+  // first flagged line, ...) are in git history.
+  static_assert(V == 0 || V == SCAN_LINES || V == 7 || V == 8, "scan variants: 0, SCAN_LINES, 7, 8");
+  constexpr bool COALT = V != SCAN_LINES;
+  constexpr bool MEMONLY = V == 7, NOHBM = V == 8;
   uint32_t memonly_acc = 0;
-  using Lds = std::conditional_t<ROT, ScanLdsR<NW>, std::conditional_t<ROT3, ScanLdsR3<NW>, ScanLds>>;
-  static_assert(ROT || NW == SCAN_WAVES_V2, "ScanLds holds 16 windows");
+  using Lds = ScanLds;
   __shared__ Lds lds;
-  // lanes of the record queue rq: with F1 its lane 63 is scratch
-  constexpr uint64_t RQ_LANES = F1 ? 63 : 64;
+  constexpr uint64_t RQ_LANES = 64;  // lanes of the record queue rq
   if (blockIdx.x == 0) {
     for (uint32_t i = threadIdx.x; i < a.n_zero_words; i += blockDim.x) a.zero_words[i] = 0;
     for (uint32_t i = threadIdx.x; i < a.n_zero2; i += blockDim.x) a.zero2[i] = 0;
@@ -952,9 +684,7 @@ void scan_kernel(ScanArgs a) {
 #ifdef SRD_WAVE_STAMPS
   if (threadIdx.x == 0) g_wave_stamp[8192 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
-  if constexpr (ROT) load_rot_lds(lds);
-  else if constexpr (ROT3) load_rot3_lds(lds);
-  else load_crc_lds(lds);
+  load_crc_lds(lds);
 #ifdef SRD_WAVE_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < 256) g_wave_stamp[8192 + 256 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -964,31 +694,13 @@ void scan_kernel(ScanArgs a) {
   // below (k, B, span, bounds) stays in SGPRs / scalar branches
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t R[4];
-  uint32_t Rr = 0, SL[4] = {0, 0, 0, 0};
-  if constexpr (ROT || ROT3) {
-    rot_lane_consts(Rr, SL, lane);
-  } else {
-#pragma unroll
-    for (int t = 0; t < 4; t++) R[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) * 128u + 4u * (lane & 31));
-  }
+  crc_lane_bases(R, lane);
   const uint8_t* __restrict__ file = a.file;
   const uint64_t flen = a.flen;
   uint32_t* win = lds.win[wv];
-  uint32_t nib_lane;
-  if constexpr (ROT) nib_lane = lds_off(lds.tn) + 128u + 4u * (lane & 31);  // 4 KiB-aligned rows, words 32-63
-  else nib_lane = lds_off(lds.nib) + 4u * (lane & 31);  // 2 KiB-aligned table base + the lane's bank
-  // the line CRC and its lane weight (the variant's table layout)
-  auto line_crc = [&](const uint32_t (&x)[16]) -> uint32_t {
-    if constexpr (ROT) return crc_line4_rot(x, lds, Rr, SL);
-    else if constexpr (ROT3) return crc_line4_rot3(x, lds, Rr, SL);
-    else if constexpr (V == 3) return crc_line2(x, lds, R);
-    else if constexpr (V == 5 || V == 6 || V == 10) return crc_line4_wide(x, lds, R);
-    else return crc_line4(x, lds, R);
-  };
-  auto lane_wt = [&](uint32_t c) -> uint32_t {
-    if constexpr (ROT) return lane_weight_rot(c, nib_lane);
-    else return lane_weight_or(c, nib_lane);
-  };
+  const uint32_t nib_lane = lds_off(lds.nib) + 4u * (lane & 31);  // 2 KiB-aligned table base + the lane's bank
+  auto line_crc = [&](const uint32_t (&x)[16]) -> uint32_t { return crc_line4(x, lds, R); };
+  auto lane_wt = [&](uint32_t c) -> uint32_t { return lane_weight_or(c, nib_lane); };
 
   // contiguous tile range per wave (whole spans, ScanPart)
   const uint64_t total_waves = (uint64_t)gridDim.x * NW;
@@ -1044,33 +756,20 @@ void scan_kernel(ScanArgs a) {
   // lane weights, suffix XOR, filter) is one basic block.
   const uint64_t nohbm_k = (a.part.s_lo + part_block_start(a.part, blockIdx.x)) * SPAN_TILES;
   auto load_tile = [&](uint64_t k, uint32_t (&o)[16]) {
-    if constexpr (BUFLD) {
-      // buffer loads over the tile (base in SGPRs, one 32-bit lane offset):
-      // no 64-bit lane address pair held across the loop (the occupancy
-      // variants' VGPR budget)
-      const __amdgpu_buffer_rsrc_t t = out_rsrc(file + k * (uint64_t)TILE, TILE);
-      const uint32_t vo = 64u * (uint32_t)lane;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(t, vo, 16 * j, 0));
-        o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
-      }
-      return;
-    }
     if constexpr (COALT) {
-      const uint8_t* tb = file + k * (uint64_t)TILE;
+      const uint8_t* tb = file + (NOHBM ? nohbm_k + (k & 1) : k) * (uint64_t)TILE;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(tb + (COAL3 ? coal3_lane_off(lane, j) : coal_lane_off(lane, j))));
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(tb + coal_lane_off(lane, j)));
         o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
       }
       return;
     }
-    const u32x4* q = (const u32x4*)(file + (NOHBM ? nohbm_k + (k & 1) : k) * (uint64_t)TILE + (COAL ? 16ull : 64ull) * lane);
+    const u32x4* q = (const u32x4*)(file + k * (uint64_t)TILE + 64ull * lane);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       // plain loads: this 64 B-per-lane pattern runs at ~3.8 TB/s with nt, ~6.1 without
-      const u32x4 v = q[COAL ? 64 * j : j];
+      const u32x4 v = q[j];
       o[4 * j] = v[0]; o[4 * j + 1] = v[1]; o[4 * j + 2] = v[2]; o[4 * j + 3] = v[3];
     }
   };
@@ -1086,18 +785,6 @@ void scan_kernel(ScanArgs a) {
   // tile's SX partial of line 63 (= its true SX_63).
   const uint32_t hb = a.filt_hb;
   uint64_t rootmax = 0;
-  // the previous tile's SX_63 (F1; uniform -- without F1 the window's win[22])
-  uint32_t hxp_s = 0;
-  uint32_t probe_s[4] = {0, 0, 0, 0}, probe_v[4] = {0, 0, 0, 0};  // V 27-29 (issue-cost probes)
-  const uint32_t probe_la = lds_off(win) + 4u * ((uint32_t)lane & 15);
-  (void)probe_s; (void)probe_v; (void)probe_la;
-  uint32_t carry_s[4] = {0, 0, 0, 0};  // SCARRY: the previous tile's line-63 tail (uniform)
-  // lane-constant LDS addresses of the straight-line window test: lane b
-  // reads dwords (b + 2) / 4 .. + 5 and the tombstone dword (b + 1) / 4
-  const uint32_t win_lds = lds_off(win);
-  const uint32_t f1_wa = win_lds + 4u * (((uint32_t)lane + 2) >> 2), f1_ta = win_lds + 4u * (((uint32_t)lane + 1) >> 2);
-  const uint32_t f1_sh = (((uint32_t)lane + 2) & 3) * 8;
-  (void)f1_wa; (void)f1_ta; (void)f1_sh;
   {
     // the line just before this wave's first tile: its tail bytes and its raw
     // CRC (= SX_63 of tile k0-1) seed the window; all lanes load it
@@ -1115,9 +802,6 @@ void scan_kernel(ScanArgs a) {
       for (int j = 0; j < 4; j++) win[j] = has_prev ? pl[12 + j] : 0u;
       win[22] = has_prev ? cp : 0u;
     }
-    hxp_s = __builtin_amdgcn_readfirstlane(has_prev ? cp : 0u);
-#pragma unroll
-    for (int j = 0; j < 4; j++) carry_s[j] = __builtin_amdgcn_readfirstlane(has_prev ? pl[12 + j] : 0u);
   }
 
   // first 8 bytes of tile k+1 (line 63's window) by a SCALAR load: the slow
@@ -1143,8 +827,7 @@ void scan_kernel(ScanArgs a) {
       return;
     }
     constexpr bool tail_tile = decltype(tail_c)::value;
-    if constexpr (COAL3) coal3_to_lines(d);  // lane l <- line l
-    else if constexpr (COALT) coal_to_lines(d);
+    if constexpr (COALT) coal_to_lines(d);  // lane l <- line l
     const uint64_t B = k * (uint64_t)TILE;
     const uint64_t span = k / SPAN_TILES;
     // bytes left in the file from B (uniform, 32-bit: every in-tile test below
@@ -1191,112 +874,15 @@ void scan_kernel(ScanArgs a) {
       }
       slow = __ballot(hz != 0);
     }
-    // ---- the tile's first flagged line (other than line 63), straight-line ----
-    // (optimistic pass) No loop and no branch: the loop's header had to drain
-    // every outstanding LDS read and the CRC's result before it, so the
-    // flagged line's LDS round trips ran after the CRC's instead of beside
-    // them.  Lane f stages the window by an exec-masked asm store here, before
-    // the CRC in program order; the window reads and the node test below
-    // interleave with the CRC's lookups; the record goes to the register
-    // queue once hx is known.  Line 63 (its window needs the next tile's
-    // head), further flagged lines and multi-candidate lines take the loop.
-    uint64_t f1_pm = 0;
-    uint32_t f1_f = 0, f1_f2 = 0, f1_f3 = 0, f1_f4 = 0, f1_s0 = 0, f1_s1 = 0, f1_tdw = 0;
-    uint32_t W[6] = {0, 0, 0, 0, 0, 0};
-    bool has0 = false;
-    // the node test of the staged line (lane b: m = B + 64 f + b - 14,
-    // data_store.rs:404-470's fields)
-    auto f1_test = [&]() {
-      f1_f2 = alignb(W[3], W[2], f1_sh);
-      f1_f3 = alignb(W[4], W[3], f1_sh);
-      f1_f4 = alignb(W[5], W[4], f1_sh);
-      f1_s0 = alignb(W[1], W[0], f1_sh);
-      f1_s1 = alignb(W[2], W[1], f1_sh);
-      const int r = 64 * (int)f1_f + lane - 14;  // m - B, in [-14, 4081]
-      const uint32_t u = (uint32_t)(r + 20);
-      const bool inrange = (u <= remu) && ((int64_t)B + r > (int64_t)a.m_lo);
-      f1_pm = __ballot(has0 && inrange && f1_f3 <= hb && (f1_f2 | f1_f3) != 0 && f1_f4 != 0);
-      // two or more possible nodes: the loop's general path takes the line
-      // (uniform selects, no branch)
-      const bool multi = (f1_pm & (f1_pm - 1)) != 0;
-      slow |= multi ? (1ull << f1_f) : 0ull;
-      f1_pm = multi ? 0ull : f1_pm;
-    };
-    auto f1_stage_test = [&]() {
-      // (room in the record queue for one more: else the loop takes the line)
-      const uint64_t s63 = slow & ~(1ull << 63);
-      has0 = s63 != 0 && wtotal + count - flushed < RQ_LANES - 1;  // uniform
-      f1_f = has0 ? (uint32_t)__builtin_ctzll(s63) : 0u;
-      slow = has0 ? (slow & ~(1ull << f1_f)) : slow;  // the loop's lines
-      const uint32_t p12 = dpp<DPP_WAVE_SHR1>(d[12]), p13 = dpp<DPP_WAVE_SHR1>(d[13]),
-                     p14 = dpp<DPP_WAVE_SHR1>(d[14]), p15 = dpp<DPP_WAVE_SHR1>(d[15]);
-      const uint32_t n0 = dpp<DPP_WAVE_SHL1>(d[0]), n1 = dpp<DPP_WAVE_SHL1>(d[1]);
-      // exec masks (SGPR pairs): the line + next head by lane f; the previous
-      // line's tail by lane f only when f > 0 (f == 0: win[0..3] holds the
-      // previous tile's line 63, carried below)
-      const uint64_t m1 = has0 ? (1ull << f1_f) : 0ull, m0 = f1_f ? m1 : 0ull;
-      uint64_t save;
-      asm volatile(
-          "s_mov_b64 %[sv], exec\n\t"
-          "s_mov_b64 exec, %[m0]\n\t"
-          "ds_write_b128 %[a], %[p]\n\t"
-          "s_mov_b64 exec, %[m1]\n\t"
-          "ds_write_b128 %[a], %[d0] offset:16\n\t"
-          "ds_write_b128 %[a], %[d1] offset:32\n\t"
-          "ds_write_b128 %[a], %[d2] offset:48\n\t"
-          "ds_write_b128 %[a], %[d3] offset:64\n\t"
-          "ds_write_b64 %[a], %[n] offset:80\n\t"
-          "s_mov_b64 exec, %[sv]"
-          : [sv] "=&s"(save)
-          : [m0] "s"(m0), [m1] "s"(m1), [a] "v"(win_lds), [p] "v"(u32x4{p12, p13, p14, p15}),
-            [d0] "v"(u32x4{d[0], d[1], d[2], d[3]}), [d1] "v"(u32x4{d[4], d[5], d[6], d[7]}),
-            [d2] "v"(u32x4{d[8], d[9], d[10], d[11]}), [d3] "v"(u32x4{d[12], d[13], d[14], d[15]}),
-            [n] "v"(u32x2{n0, n1})
-          : "memory");
-      // lane b's window dwords from its lane-constant address, in LDS issue
-      // order behind the stores (one wave: no wait between them)
-#pragma unroll
-      for (int i = 0; i < 6; i++) W[i] = lds_ld(f1_wa + 4 * i);
-      f1_tdw = lds_ld(f1_ta);
-      f1_test();
-    };
-    if constexpr (F1 && !F1_AFTER && !FULL) f1_stage_test();
     // ---- per-line raw CRC, lane weight, 64-lane suffix XOR ----
     // Wave priority over the LDS-latency chains (the CRC's lookups here, the
     // flagged-line window below): a wave in them wins the issue arbitration,
     // so its next round of lookups goes out as soon as the last returns,
     // while the other waves fill the gaps (same-box A/B: -4 %)
-    // (F1: the ring loop raised the priority before the tile's loads already;
-    // a setprio here would split the scheduling region between the window
-    // test above and the CRC's lookups)
-    if (!F1 || F1_AFTER || tail_tile) __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(3);
     const uint32_t c = line_crc(d);
     __builtin_amdgcn_s_setprio(0);
     const uint32_t hx = half_suffix_xor(lane_wt(c), lane);
-    // issue-cost probes (timing-only, results unchanged): 27 = +16 independent
-    // SALU per tile, 28 = +16 independent VALU, 29 = +8 LDS reads (the tile
-    // values' slot, results discarded by an XOR into a dead register)
-    if constexpr (V == 27) {
-      asm volatile(
-          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1\n\t"
-          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1\n\t"
-          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1\n\t"
-          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1"
-          : "+s"(probe_s[0]), "+s"(probe_s[1]), "+s"(probe_s[2]), "+s"(probe_s[3]));
-    } else if constexpr (V == 28) {
-      asm volatile(
-          "v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3\n\t"
-          "v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3\n\t"
-          "v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3\n\t"
-          "v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3"
-          : "+v"(probe_v[0]), "+v"(probe_v[1]), "+v"(probe_v[2]), "+v"(probe_v[3]));
-    } else if constexpr (V == 29) {
-      uint32_t x[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++) x[i] = lds_ld(probe_la + 4u * (uint32_t)i);
-      probe_v[0] ^= x[0] ^ x[1] ^ x[2] ^ x[3] ^ x[4] ^ x[5] ^ x[6] ^ x[7];
-      asm volatile("" ::"v"(probe_v[0]));
-    }
     // per-tile values: lanes 0, 1 their half partials, lane 32 the true SX_32.
     // Buffered in lanes 4(k%16) + {0,1,2} of tacc; one 256-B store per 16
     // tiles.  Every store of this loop is an UNCONDITIONAL buffer store whose
@@ -1324,50 +910,6 @@ void scan_kernel(ScanArgs a) {
         tg_lo = (uint32_t)(max(g, k0) - g) * 4;
         tg_hi = 4u * t + 4u;
       }
-    }
-
-    if constexpr (F1 && F1_AFTER && !FULL) {
-      __builtin_amdgcn_s_setprio(2);
-      f1_stage_test();
-    }
-    if constexpr (F1 && !FULL) {
-      // the first flagged line's record (at most one candidate: the node test
-      // is link_record', F_NT) into the register queue; lane 63 of rq is scratch
-      // (a tile without a record writes there), so the queue holds 63
-      const bool single = f1_pm != 0;  // uniform
-      const int bl = single ? __builtin_ctzll(f1_pm) : 0;
-      const int rs = 64 * (int)f1_f + bl - 14;
-      const uint64_t m = B + (int64_t)rs;
-      const uint32_t s2 = __builtin_amdgcn_readlane(f1_f2, bl), s3 = __builtin_amdgcn_readlane(f1_f3, bl);
-      const uint32_t s0 = __builtin_amdgcn_readlane(f1_s0, bl), s1 = __builtin_amdgcn_readlane(f1_s1, bl);
-      const uint32_t s4 = __builtin_amdgcn_readlane(f1_f4, bl);
-      const uint32_t os = (uint32_t)bl + 2;
-      const uint32_t stb = ((uint32_t)__builtin_amdgcn_readlane(f1_tdw, bl) >> (((os - 1) & 3) * 8)) & 0xffu;
-      const uint32_t us = (uint32_t)(rs + 20);
-      const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
-      const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
-      const int lm = rs >> 6;
-      const uint32_t hm = lm < 0 ? hxp_s : (uint32_t)__builtin_amdgcn_readlane(hx, lm & 63);
-      const uint32_t kind = js < 64 ? 0u : (js == 64 ? 1u : 2u);
-      const uint32_t fl = F_NT | (stb == 0 ? F_ZB : 0u) | ((rs & 63) == 0 ? F_TAIL : 0u) | F_SXM |
-                          (kind << F_SUF_SHIFT) | (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) |
-                          ((js & 63) < 32 ? F_SUF_LO : 0u);
-      const uint64_t rr = wtotal + count;  // the record's index in the wave's region
-      const bool inq = single && rr < a.wcap;  // room in the queue: checked before staging
-      const int li = inq ? (int)(rr - flushed) : (int)(RQ_LANES);
-      rq[0] = writelane_u32((uint32_t)m, li, rq[0]);
-      rq[1] = writelane_u32((uint32_t)(m >> 32), li, rq[1]);
-      rq[2] = writelane_u32(hm, li, rq[2]);
-      rq[3] = writelane_u32(hs, li, rq[3]);
-      rq[4] = writelane_u32(fl, li, rq[4]);
-      rq[5] = writelane_u32(s2, li, rq[5]);
-      rq[6] = writelane_u32(s3, li, rq[6]);
-      rq[7] = writelane_u32(s0, li, rq[7]);
-      rq[8] = writelane_u32(s1, li, rq[8]);
-      rq[9] = writelane_u32(s4, li, rq[9]);
-      rvalid |= inq ? (1ull << li) : 0ull;
-      ovf = ovf || (single && rr >= a.wcap);
-      count += single ? 1u : 0u;
     }
 
     // Re-define d by an empty asm once its loads have been consumed: a loop
@@ -1398,10 +940,7 @@ void scan_kernel(ScanArgs a) {
         }
       }
       if (lane == f) {
-        if constexpr (SCARRY)
-          *(u32x4*)&win[0] = f > 0 ? u32x4{p12, p13, p14, p15} : u32x4{carry_s[0], carry_s[1], carry_s[2], carry_s[3]};
-        else if (f > 0)
-          *(u32x4*)&win[0] = u32x4{p12, p13, p14, p15};
+        if (f > 0) *(u32x4*)&win[0] = u32x4{p12, p13, p14, p15};
 #pragma unroll
         for (int j = 0; j < 4; j++) *(u32x4*)&win[4 + 4 * j] = u32x4{d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]};
         *(u32x2*)&win[20] = u32x2{n0, n1};
@@ -1418,7 +957,7 @@ void scan_kernel(ScanArgs a) {
 #pragma unroll
       for (int i = 0; i < 6; i++) W[i] = win[base + i];
       const uint32_t tdw = win[(o - 1) >> 2];
-      const uint32_t hxp = (F1 || SCARRY) ? 0u : win[22];
+      const uint32_t hxp = win[22];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1454,7 +993,7 @@ void scan_kernel(ScanArgs a) {
           const uint32_t js = (us + ((0u - us) & 63u)) >> 6;
           const uint32_t hs = __builtin_amdgcn_readlane(hx, (int)(js & 63));
           const int lm = rs >> 6;
-          const uint32_t hm = lm < 0 ? ((F1 || SCARRY) ? hxp_s : (uint32_t)__builtin_amdgcn_readfirstlane(hxp))
+          const uint32_t hm = lm < 0 ? (uint32_t)__builtin_amdgcn_readfirstlane(hxp)
                                      : (uint32_t)__builtin_amdgcn_readlane(hx, lm & 63);
           const uint64_t r = wtotal + count;  // the record's index in the wave's region
           if (r < a.wcap) {
@@ -1479,8 +1018,8 @@ void scan_kernel(ScanArgs a) {
             } else if (lane == 0) {
               const uint64_t gi = w * a.wcap + r;
               a.c_m[gi] = m;
-              a.c_rec[2 * gi] = u32x4{s2, s3, s0, s1};
-              a.c_rec[2 * gi + 1] = u32x4{s4, hm, hs, fl};
+              a.c_rec[gi] = u32x4{s2, s3, fl, s4};
+              a.c_rec1[gi] = u32x4{s0, s1, hm, hs};
             }
           } else {
             ovf = true;
@@ -1509,7 +1048,7 @@ void scan_kernel(ScanArgs a) {
       const uint32_t hs = __shfl(hx, (int)(js & 63));
       const int lm = r >> 6;                             // m's line (-1: previous tile's line 63)
       const uint32_t hm0 = __shfl(hx, lm & 63);
-      const uint32_t hm = lm < 0 ? ((F1 || SCARRY) ? hxp_s : hxp) : hm0;
+      const uint32_t hm = lm < 0 ? hxp : hm0;
       if (FULL ? count + __popcll(cm) > a.cap : wtotal + count + __popcll(cm) > a.wcap) ovf = true;
       if (strong) {
         const uint32_t idx = count + __popcll(cm & ((1ull << lane) - 1));
@@ -1519,31 +1058,15 @@ void scan_kernel(ScanArgs a) {
           const uint32_t fl = (tomb ? F_TOMB : 0u) | ((r & 63) == 0 ? F_TAIL : 0u) | F_SXM | (kind << F_SUF_SHIFT) |
                               (lm >= 0 && lm < 32 ? F_SXM_LO : 0u) | ((js & 63) < 32 ? F_SUF_LO : 0u);
           a.c_m[gi] = m;
-          a.c_rec[2 * gi] = u32x4{f2, f3, f0, f1};
-          a.c_rec[2 * gi + 1] = u32x4{f4, hm, hs, fl};
+          a.c_rec[gi] = u32x4{f2, f3, fl, f4};
+          a.c_rec1[gi] = u32x4{f0, f1, hm, hs};
         }
       }
       count += __popcll(cm);
     }
     __builtin_amdgcn_s_setprio(0);
     // carry the last line's tail and SX_63 into the next tile's window
-    if constexpr (F1) {
-      // lane 63's tail by an exec-masked asm store (no branch), SX_63 in an SGPR
-      uint64_t save;
-      asm volatile(
-          "s_mov_b64 %[sv], exec\n\t"
-          "s_mov_b64 exec, %[m]\n\t"
-          "ds_write_b128 %[a], %[p]\n\t"
-          "s_mov_b64 exec, %[sv]"
-          : [sv] "=&s"(save)
-          : [m] "s"(1ull << 63), [a] "v"(win_lds), [p] "v"(u32x4{d[12], d[13], d[14], d[15]})
-          : "memory");
-      hxp_s = __builtin_amdgcn_readlane(hx, 63);
-    } else if constexpr (SCARRY) {
-      hxp_s = __builtin_amdgcn_readlane(hx, 63);
-#pragma unroll
-      for (int j = 0; j < 4; j++) carry_s[j] = __builtin_amdgcn_readlane(d[12 + j], 63);
-    } else if (lane == 63) {
+    if (lane == 63) {
 #pragma unroll
       for (int j = 0; j < 4; j++) win[j] = d[12 + j];
       win[22] = hx;
@@ -1577,46 +1100,28 @@ void scan_kernel(ScanArgs a) {
   // ring loop runs one store point per round of 3 tiles, not one per tile (a
   // round completes at most one group of either kind).
   auto store_point = [&](uint64_t kf, uint32_t nt) {
-    if constexpr (MEMONLY || NOSTORE) return;
+    if constexpr (MEMONLY) return;
     const bool last = kf + nt == k1;  // uniform
     {
-      const uint32_t off = !NO_TV && tg_pend && (uint32_t)lane - tg_lo < tg_hi - tg_lo ? 4u * lane : OOB_OFF;
+      const uint32_t off = tg_pend && (uint32_t)lane - tg_lo < tg_hi - tg_lo ? 4u * lane : OOB_OFF;
       __builtin_amdgcn_raw_buffer_store_b32(tg_par ? tacc1 : tacc0, out_rsrc(a.tile + 4 * tg_base, 256), off, 0, 0);
       tg_pend = false;
     }
     {
       // (optimistic pass only; the full pass stores its records directly)
-      constexpr uint64_t FLUSH_AT = V == 33 ? 60 : 40;  // (33: larger record bursts)
+      constexpr uint64_t FLUSH_AT = 40;  // (60: +-0, profiles/r05/variant_ab_store_ablations_coal.txt)
       const uint64_t pend = wtotal + count - flushed;  // records pending (lanes [0, min(pend, 64)))
       const bool fl = pend >= FLUSH_AT || last;  // uniform
-      const bool wr = !NO_REC && fl && ((rvalid >> lane) & 1);
-      uint64_t rb = w * a.wcap + flushed;  // lane 0's record
-      uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
-      if constexpr (UNISTORE) {
-        // uniform by construction, but the compiler's divergence analysis
-        // loses it: as VGPRs the three descriptors cost a waterfall loop
-        // around each store (and registers the occupancy variants lack)
-        rb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32)) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rb);
-        // (min<uint64_t> compiles to f64 VALU math here: a select instead)
-        const uint64_t left = a.wcap > flushed ? a.wcap - flushed : 0;
-        rn = __builtin_amdgcn_readfirstlane(left >= 64 ? 64u : (uint32_t)left);
-        const uint32_t o32 = wr ? 32u * lane : OOB_OFF;
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + rb, rn * 8),
-                                              wr ? 8u * lane : OOB_OFF, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
-                                               o32, 0, 0);
-        // (the second half through a descriptor 16 B further: one lane offset for both)
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]},
-                                               out_rsrc((const char*)(a.c_rec + 2 * rb) + 16, rn * 32), o32, 0, 0);
-      } else {
+      const bool wr = fl && ((rvalid >> lane) & 1);
+      const uint64_t rb = w * a.wcap + flushed;  // lane 0's record
+      const uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + rb, rn * 8),
                                             wr ? 8u * lane : OOB_OFF, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[7], rq[8]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
-                                             wr && !NO_PK ? 32u * lane : OOB_OFF, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[9], rq[2], rq[3], rq[4]}, out_rsrc(a.c_rec + 2 * rb, rn * 32),
-                                             wr ? 32u * lane + 16u : OOB_OFF, 0, 0);
-      }
+      // the record's halves: {p, flags, crc}, {key_hash, sxm, suf}
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[4], rq[9]}, out_rsrc(a.c_rec + rb, rn * 16),
+                                             wr ? 16u * lane : OOB_OFF, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[7], rq[8], rq[2], rq[3]}, out_rsrc(a.c_rec1 + rb, rn * 16),
+                                             wr ? 16u * lane : OOB_OFF, 0, 0);
       if (fl) {
         flushed = wtotal + count;
         rvalid = 0;
@@ -1649,7 +1154,7 @@ void scan_kernel(ScanArgs a) {
   // Dummy stores (out-of-range offsets: dropped by the hardware; distinct,
   // or the compiler merges them as dead stores) give the entry the same queue.
   auto pad_stores = [&](uint32_t g) {
-    constexpr uint32_t NST = (NOSTORE || MEMONLY) ? 0u : 6u;  // a store point's unconditional stores
+    constexpr uint32_t NST = MEMONLY ? 0u : 6u;  // a store point's unconditional stores
 #pragma unroll
     for (uint32_t i = 0; i < NST; i++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, out_rsrc(a.tile, 256), OOB_OFF - 64u * (NST * g + i), 0, 0);
@@ -1658,51 +1163,34 @@ void scan_kernel(ScanArgs a) {
   // reaches the loop latch, and that (never taken) latch -> header path
   // would shorten the compiler's wait counts as well.  The <= 2 remaining
   // ring tiles run in the unpipelined loop below with the file's tail tiles.
-  constexpr uint32_t RD = RING2 ? 2 : 3;  // ring depth
+  constexpr uint32_t RD = 3;  // ring depth
   const uint32_t nfull = nk / RD;
   // (the entry's queue = the loop latch's: with a store point per tile the
   // stores of one tile follow every load; with one per round, only tile
   // B's loads have a store point behind them before the loop comes round)
   load_tile(k0, A);
-  if constexpr (TILE_SP) pad_stores(0);
-  if constexpr (!RING2) {
-    // A's loads strictly before B's: the scheduler interleaved the two tiles'
-    // coalesced loads here, and the loop's first wait (the minimum over its
-    // entries) then waited for 3 of the next tile's loads too (vmcnt 11
-    // instead of 14): -0.2 to -1 % scan (profiles/r05/variant_ab_prologue_order*.txt)
-    if constexpr (COALT) __builtin_amdgcn_sched_barrier(0);
-    load_tile(k0 + 1, Bv);
-    pad_stores(1);
-  }
+  // A's loads strictly before B's: the scheduler interleaved the two tiles'
+  // coalesced loads here, and the loop's first wait (the minimum over its
+  // entries) then waited for 3 of the next tile's loads too (vmcnt 11
+  // instead of 14): -0.2 to -1 % scan (profiles/r05/variant_ab_prologue_order*.txt)
+  if constexpr (COALT) __builtin_amdgcn_sched_barrier(0);
+  load_tile(k0 + 1, Bv);
+  pad_stores(1);
   for (uint32_t i = 0; i < nfull; i++) {
     const uint32_t j = RD * i;
     // priority from the tile's prefetch loads through its CRC (process()
     // drops it after the lookups): -1.6 % same-box A/B over priority on the
     // CRC alone
-    if constexpr (RING2) {
-      __builtin_amdgcn_s_setprio(3);
-      load_tile(k0 + min(j + 1, nk), Bv);
-      process(k0 + j, A, body);
-      store_point(k0 + j, 1);
-      __builtin_amdgcn_s_setprio(3);
-      load_tile(k0 + min(j + 2, nk), A);
-      process(k0 + j + 1, Bv, body);
-      store_point(k0 + j + 1, 1);
-    } else {
-      __builtin_amdgcn_s_setprio(3);
-      load_tile(k0 + min(j + 2, nk), Cv);
-      process(k0 + j, A, body);
-      if constexpr (TILE_SP) store_point(k0 + j, 1);
-      __builtin_amdgcn_s_setprio(3);
-      load_tile(k0 + min(j + 3, nk), A);
-      process(k0 + j + 1, Bv, body);
-      if constexpr (TILE_SP) store_point(k0 + j + 1, 1);
-      __builtin_amdgcn_s_setprio(3);
-      load_tile(k0 + min(j + 4, nk), Bv);
-      process(k0 + j + 2, Cv, body);
-      if constexpr (TILE_SP) store_point(k0 + j + 2, 1);
-      else store_point(k0 + j, 3);
-    }
+    __builtin_amdgcn_s_setprio(3);
+    load_tile(k0 + min(j + 2, nk), Cv);
+    process(k0 + j, A, body);
+    __builtin_amdgcn_s_setprio(3);
+    load_tile(k0 + min(j + 3, nk), A);
+    process(k0 + j + 1, Bv, body);
+    __builtin_amdgcn_s_setprio(3);
+    load_tile(k0 + min(j + 4, nk), Bv);
+    process(k0 + j + 2, Cv, body);
+    store_point(k0 + j, 3);
   }
   const uint64_t kr = k0 + (uint64_t)RD * nfull;
   // the ring's remainder and the file's last <= 2 tiles (masked: a tail
@@ -1744,10 +1232,7 @@ void scan_kernel(ScanArgs a) {
   // registers (one round trip instead of 2q dependent ones: the last block's
   // epilogue is on the critical path of every call)
   constexpr int QR = 4;
-  uint64_t* s_wsum;  // the CRC tables are dead now
-  if constexpr (ROT) s_wsum = (uint64_t*)lds.tn;
-  else if constexpr (ROT3) s_wsum = (uint64_t*)lds.x;
-  else s_wsum = (uint64_t*)lds.tab;
+  uint64_t* s_wsum = (uint64_t*)lds.tab;  // the CRC tables are dead now
   uint64_t* s_smax = s_wsum + NW;
   uint64_t* s_root = lds.s_root;
   uint64_t* s_ovf = s_smax + NW;
@@ -1832,7 +1317,7 @@ __global__ __launch_bounds__(256) void link_kernel(LinkArgs a) {
   const uint64_t gb = a.span_base[sp];
   for (uint32_t i = threadIdx.x % LINK_LANES; i < n; i += LINK_LANES) {
     const uint64_t gi = sp * a.cap + i;
-    const u32x4 r0 = a.c_rec[2 * gi];
+    const u32x4 r0 = a.c_rec[gi];
     const uint64_t m = a.c_m[gi], p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
     const uint64_t mp = p - 20;  // p >= 20 by construction
     const uint64_t sp2 = (mp + 14) / SPAN_BYTES;  // span s holds m in [16 KiB s - 14, 16 KiB (s+1) - 14)
@@ -1896,7 +1381,7 @@ __global__ void walk_kernel(const int64_t* par, const uint32_t* runhead, const u
     len += x - h + 1;
     int64_t q = par[h];
     if (q == PAR_ROOT) {
-      const u32x4 r0 = c_rec[2 * slot[h]];
+      const u32x4 r0 = c_rec[slot[h]];
       ws->root_t = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
       break;
     }
@@ -2066,7 +1551,8 @@ struct FinArgs {
   const int64_t* par;        // dense g -> dense parent
   const WalkState* ws;
   const uint64_t* c_m;
-  const u32x4* c_rec;
+  const u32x4* c_rec;        // {p, flags, crc} (ScanArgs::c_rec)
+  const u32x4* c_rec1;       // {key_hash, sxm, suf}
   const uint32_t* tile;      // [4k..4k+2] per-tile values (tile_T / tile_SX1)
   int no_crc;
   // device-side plan (sync-free path): when set, n_chain / root_t come from
@@ -2218,23 +1704,23 @@ __device__ bool finalize_core(const FinArgs& a, uint64_t c, uint64_t gi, int64_t
     pieces = 1;
   } else {
     mo = a.c_m[gi];
-    const u32x4 r0 = a.c_rec[2 * gi], r1 = a.c_rec[2 * gi + 1];
+    const u32x4 r0 = a.c_rec[gi], r1 = a.c_rec1[gi];
     p = (uint64_t)r0[0] | ((uint64_t)r0[1] << 32);
-    kh = (uint64_t)r0[2] | ((uint64_t)r0[3] << 32);
-    crc_st = r1[0];
-    const uint32_t fl = r1[3];
+    kh = (uint64_t)r1[0] | ((uint64_t)r1[1] << 32);
+    crc_st = r0[3];
+    const uint32_t fl = r0[2];
     tomb = fl & F_TOMB;
     start = tomb ? p : p + prepad64(p);
     if (fl & F_SXM) {
-      sxm = (fl & F_SXM_LO) ? lo_fix(a.tile, mo / TILE, r1[1]) : r1[1];
+      sxm = (fl & F_SXM_LO) ? lo_fix(a.tile, mo / TILE, r1[2]) : r1[2];
       pieces |= 2;
     }
     if (fl & F_TAIL) { tail = 0; pieces |= 4; }
     if (pgi >= 0) {
-      const u32x4 pr1 = a.c_rec[2 * pgi + 1];
-      const uint32_t kind = (pr1[3] >> F_SUF_SHIFT) & 3;
+      const uint32_t pfl = a.c_rec[pgi][2], psuf = a.c_rec1[pgi][3];
+      const uint32_t kind = (pfl >> F_SUF_SHIFT) & 3;
       const uint64_t k0 = start / TILE;  // kind 0: the parent's tile; 1, 2: the next one
-      if (kind == 0) { suf = (pr1[3] & F_SUF_LO) ? lo_fix(a.tile, k0, pr1[2]) : pr1[2]; pieces |= 1; }
+      if (kind == 0) { suf = (pfl & F_SUF_LO) ? lo_fix(a.tile, k0, psuf) : psuf; pieces |= 1; }
       else if (kind == 1) { suf = tile_T(a.tile, k0); pieces |= 1; }
       else if (kind == 2) { suf = tile_SX1(a.tile, k0); pieces |= 1; }
     } else if (start == 0) {

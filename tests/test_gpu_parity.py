@@ -235,6 +235,47 @@ def test_unfused_glue_agrees(golden_cases):
             c.close()
 
 
+# key_hash pairs whose Xxh3BuildHasher hashes (XXH3-64 of the 8 LE bytes,
+# key_indexer.rs:98-124) share the low 32 bits and the top 14 bits: the same
+# index bucket at any bucket count and the same 32-bit partial key in the
+# bucket records (found by a search over 2^25 keys; checked below)
+PARTIAL_KEY_PAIRS = [(0x5A5A000000CC16BD, 0x5A5A000000E96736), (0x5A5A00000000992F, 0x5A5A0000003FE6D1),
+                     (0x5A5A00000030969B, 0x5A5A000001ED8F14)]
+
+
+@pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
+def test_index_partial_key_collisions(ctx, flags):
+    """The bucketed KeyIndexer::build keeps 8-byte bucket records (chain index
+    + the low word of the key's hash) and deduplicates by that partial key;
+    two different keys that share it must still both be indexed, each at its
+    own latest entry (key_indexer.rs:98-124 is latest-wins per full key_hash):
+    idx_dedup detects the mismatch against the full keys and redoes the
+    bucket exactly.  Cases: a pair written once each, a pair with interleaved
+    overwrites, a pair whose later key is a tombstone."""
+    for a, b in PARTIAL_KEY_PAIRS:
+        ha = xxhash.xxh3_64_intdigest(struct.pack("<Q", a))
+        hb = xxhash.xxh3_64_intdigest(struct.pack("<Q", b))
+        assert a != b and ha & 0xFFFFFFFF == hb & 0xFFFFFFFF and ha >> 50 == hb >> 50
+    rnd = random.Random(61)
+    (a1, b1), (a2, b2), (a3, b3) = PARTIAL_KEY_PAIRS
+    seq = [(a1, 1), (b1, 1)]                                   # once each: b1 wins the partial key
+    seq += [(a2, 1), (b2, 1), (a2, 1), (0x1234, 1), (b2, 1), (a2, 1)]  # overwrites interleaved
+    seq += [(b3, 1), (a3, 1), (b3, 0)]                          # the later b3 a tombstone
+    seq += [(rnd.getrandbits(64), 1) for _ in range(300)]
+    rnd.shuffle(seq[11:])
+    buf = bytearray()
+    t = 0
+    for kh, live in seq:
+        if live:
+            t = O.write_entries(buf, t, [(kh, rnd.randbytes(rnd.choice([5, 64, 700, 4096])) or b"\x01")])
+        else:
+            t = O.write_entries(buf, t, [(kh, b"\x00")], allow_null=True)
+    r = check_against_oracle(bytes(buf), ctx, flags, "partial-key pairs")
+    idx = r.index()
+    for a, b in PARTIAL_KEY_PAIRS:
+        assert a in idx and b in idx
+
+
 def _ctx_with_loads(mode):
     os.environ["SRD_SCAN_LOADS"] = mode
     try:

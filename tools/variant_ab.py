@@ -3,7 +3,7 @@
 context runs every variant (srd_debug_set_scan_variant) in interleaved rounds,
 so the per-context spread of the scan rate cancels out.  Each
 variant's results are checked against the store's closed form every batch.
-usage: python tools/variant_ab.py [variants, default 0,1]   env: NCTX, ROUNDS, CONFIG=c2|c3|c2torn, N (entries)"""
+usage: python tools/variant_ab.py [variants: 0 (product), 34 (line-per-lane loads), 7! / 8! (memory-only / compute-only ablations); default 0,34]   env: NCTX, ROUNDS, CONFIG=c2|c3|c2torn, N (entries)"""
 import ctypes as C, json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["SRD_LIB_PATH"] = os.path.join(ROOT, "rust-simd-r-drive_amd", "build", "var", "lib_dbg.so")
@@ -14,7 +14,7 @@ L = S.lib()
 L.srd_debug_set_scan_variant.argtypes = [C.c_void_p, C.c_int]
 # "7!": a timing-only ablation -- the optimistic scan alone (the library's
 # debug scan-only flag), results not checked
-spec = (sys.argv[1] if len(sys.argv) > 1 else "0,1").split(",")
+spec = (sys.argv[1] if len(sys.argv) > 1 else "0,34").split(",")
 variants = [int(v.rstrip("!")) for v in spec]
 timing_only = {int(v.rstrip("!")) for v in spec if v.endswith("!")}
 SCAN_ONLY = 1 << 30
