@@ -161,6 +161,12 @@ struct Ctx {
   // check_kernel + chain_finalize_kernel<false>, the retry rounds' shape) and
   // SRD_LB_FAIL_BLOCK=b (chain block b's look-back treated as timed out)
   uint32_t lb_fail = ~0u;
+  // XCD-aware block shares of the optimistic scan (XPart, B_XPART; SRD_XPART=0
+  // at srd_ctx_create turns them off): the parity of the table the next scan
+  // reads, and the span count / grid the table was made for
+  bool xpart_on = true, xp_valid = false;
+  uint32_t xp_par = 0, xp_g = 0;
+  uint64_t xp_ns = 0;
   srd_device_result res{};
   // host-input staging
   Buf file;
@@ -225,7 +231,7 @@ enum BufId {
   B_O_PIECES, B_O_SUF, B_O_SXM, B_O_TAIL, B_SLOW,
   B_HKEYS, B_HVALS, B_LATEST, B_IPOS, B_IKEY, B_IPACKED,
   B_CUB_TMP,
-  B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HOFF, B_SKEY, B_SIDX, B_LATEST8,
+  B_PLAN, B_HASCHILD, B_CHILDOF, B_FLAG, B_PART, B_PARTEX, B_HOFF, B_SKEY, B_SIDX, B_LATEST8, B_XPART,
   B_MPLAN, B_MKEY, B_MVAL, B_PCNT, B_POFF, B_HASCHILD2,
   B_WPAY0, B_WPAY1, B_WKEY0, B_WKEY1, B_WENT0, B_WENT1, B_WKH, B_WMO,
   B_IT_FLAG, B_IT_POS, B_IT_ST, B_IT_EN, B_IT_KEPT, B_IT_OST, B_IT_OEN, B_IT_OKH, B_IT_ENT, B_IT_RLEN, B_IT_PST,
@@ -548,6 +554,11 @@ extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
   c->scan_variant = (uint32_t)v;
   return 0;
 }
+extern "C" int srd_debug_set_xpart(srd_ctx* c, int on) {  // XCD-aware scan block shares on / off
+  if (!c) return SRD_ERR_ARG;
+  c->xpart_on = on != 0;
+  return 0;
+}
 extern "C" int srd_debug_set_glue_fused(srd_ctx* c, int fused) {
   if (!c) return SRD_ERR_ARG;
   c->glue_fused = fused != 0;
@@ -609,6 +620,7 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
     else if (!strcmp(e, "coal")) c->coal_max = ~0ull;
   }
   if (const char* e = getenv("SRD_GLUE_FUSED")) c->glue_fused = strcmp(e, "0") != 0;
+  if (const char* e = getenv("SRD_XPART")) c->xpart_on = strcmp(e, "0") != 0;
   if (const char* e = getenv("SRD_LB_FAIL_BLOCK")) {
     char* end = nullptr;
     const unsigned long v = strtoul(e, &end, 10);
@@ -686,11 +698,13 @@ static ScanPart scan_part(const Ctx* c, uint64_t s_lo, uint64_t ns, unsigned g, 
   part_fill_cw(p);
   return p;
 }
-// an upper bound on the spans of one wave
-static uint64_t part_max_wave_spans(const ScanPart& p) {
+// an upper bound on the spans of one wave; xpart: with XCD-aware block
+// shares, a block holds at most (1 + XP_CLAMP) / (1 - XP_CLAMP) < 1.25 of
+// the even share + 1 span (xpart_update)
+static uint64_t part_max_wave_spans(const ScanPart& p, bool xpart = false) {
   if (!p.g) return 1;
   const uint32_t wmax = *std::max_element(p.wq, p.wq + p.nw);
-  const uint64_t nb = (p.ns + p.g - 1) / p.g;
+  const uint64_t nb = xpart ? (p.ns * 5 + 4 * p.g - 1) / (4 * p.g) + 1 : (p.ns + p.g - 1) / p.g;
   return (nb * wmax + 65535) / 65536 + 1;
 }
 
@@ -1170,9 +1184,17 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const uint32_t var = scan_variant_for(c, flen - span_off);
     uint32_t nw;
     const unsigned g = scan_grid(c, var, ns_rel, &nw);
-    const ScanPart part = scan_part(c, s_lo, ns_rel, g, nw);
+    ScanPart part = scan_part(c, s_lo, ns_rel, g, nw);
+    const bool xpart = c->xpart_on && g <= XP_MAX_BLOCKS;
+    XPart* xp = nullptr;
+    if (xpart) {
+      TRY(ensure_z(c, B_XPART, sizeof(XPart)));
+      xp = P<XPart>(c, B_XPART);
+      // the table the previous scan's link2 wrote, if it was made for this span count and grid
+      if (c->xp_valid && c->xp_ns == ns_rel && c->xp_g == g) part.bs = &xp->bs[c->xp_par][0];
+    }
     const uint64_t total_waves = (uint64_t)g * nw;
-    const uint64_t spw = part_max_wave_spans(part);
+    const uint64_t spw = part_max_wave_spans(part, xpart);
     const uint64_t wcap = spw * c->copt.cap;
     // the glue works in slot space (slot = wave * wcap + record): its parent
     // words are 31-bit; stores above ~1 TiB (or a denser cap) take the full pass
@@ -1199,6 +1221,8 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     ScanArgs a{};
     a.variant = var;
     a.part = part;
+    a.xp = xp;
+    a.xp_next = c->xp_par ^ 1u;
     a.file = d_file;
     a.flen = flen;
     a.n_tiles = n_tiles;
@@ -1242,6 +1266,12 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     link2_kernel<<<(unsigned)((total_waves + LINK_WPB - 1) / LINK_WPB), 256 * LINK_WPB, 0, c->stream>>>(
         a, (uint32_t)total_waves);
     KCHK(c, "link2_kernel");
+    if (xp) {  // link2 wrote the next call's block starts into the other half
+      c->xp_par ^= 1u;
+      c->xp_valid = true;
+      c->xp_ns = ns_rel;
+      c->xp_g = g;
+    }
     // ---- shape check, chain, finalize, index; retried on device with more
     //      prune rounds when false candidates chained onto each other ----
     Plan hp{};

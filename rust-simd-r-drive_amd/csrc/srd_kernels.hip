@@ -79,7 +79,8 @@ struct DevTables {
 __device__ DevTables g_tabs;
 #ifdef SRD_WAVE_STAMPS
 __device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]: block b's start;
-                                                // [8192 + 256 + b]: its tables loaded; [8192 + 1023]: the epilogue's end
+                                                // [8192 + 256 + b]: its tables loaded; [8192 + 512 + b]: its
+                                                // XCC_ID; [8192 + 1023]: the epilogue's end
 #endif
 
 // The scan's wave partition (both passes; link_record inverts it).  Block b of g
@@ -89,7 +90,9 @@ __device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]
 // its oldest waves first, so with an even split waves 0-3 (the oldest on
 // each SIMD) finished ~15% before waves 12-15 (tools/wave_stamps.py); the
 // per-slot shares wq[v] (scan_weights: fitted to the wave stamps) even out
-// the finish times.
+// the finish times.  The optimistic pass replaces st(b) by a device table
+// (XPart, XCD-aware block shares) once a context has scanned a store of the
+// same span count and grid.
 struct ScanPart {
   uint64_t s_lo;   // first resident span
   uint64_t ns;     // resident spans
@@ -97,6 +100,28 @@ struct ScanPart {
   uint32_t nw;     // waves per scan block (<= 16; the launch's variant sets it, scan_geom)
   uint32_t wq[16];  // share of wave slot v of each block; wq[0] + .. + wq[nw-1] == 65536
   uint32_t cw[17];  // cumulative: cw[v] = wq[0] + .. + wq[v-1] (part_fill_cw)
+  const uint64_t* bs;  // device: st(0..g) (XPart::bs of this call), nullptr: st(b) = b*ns/g
+};
+
+// XCD-aware block shares (the optimistic scan).  The dispatcher hands block b
+// to XCD (b + r) mod 8, r fixed per HW queue, and the XCDs do not stream at
+// one speed: on a box the odd XCDs ran their blocks 4-5 % slower than the even
+// ones, the pattern the same for consecutive calls (tools/xcc_stamps.py,
+// profiles/r06/xcc_stamps_r6e.txt) -- with equal blocks the slow XCDs set the
+// scan's end.  Every scan block records the XCD it ran on (HW_REG_XCC_ID) and
+// its duration; link2_kernel's block 0 turns them into each XCD's speed (a
+// moving average over the calls) and the next call's block
+// starts, each block sized by its XCD's speed (clamped to +-XP_CLAMP), into
+// the other half of a double-buffered table: call k reads bs[k & 1], writes
+// bs[(k + 1) & 1] (the host flips the parity; it uses the table only for the
+// span count and grid it was made for).
+constexpr uint32_t XP_MAX_BLOCKS = 1024;
+constexpr float XP_CLAMP = 0.10f;
+struct XPart {
+  uint64_t bs[2][XP_MAX_BLOCKS + 1];  // block starts (resident-relative spans) per parity
+  uint32_t xcc[XP_MAX_BLOCKS];        // the XCD each block of the last scan ran on
+  uint32_t dur[XP_MAX_BLOCKS];        // its duration (s_memrealtime ticks, 10 ns)
+  float w[8];                         // each XCD's relative speed (0: none measured yet)
 };
 __host__ __device__ __forceinline__ void part_fill_cw(ScanPart& p) {
   p.cw[0] = 0;
@@ -105,6 +130,7 @@ __host__ __device__ __forceinline__ void part_fill_cw(ScanPart& p) {
 // cumulative share of the waves below v (v <= 16)
 __host__ __device__ __forceinline__ uint64_t part_cw(const ScanPart& p, uint32_t v) { return p.cw[v]; }
 __host__ __device__ __forceinline__ uint64_t part_block_start(const ScanPart& p, uint64_t b) {
+  if (p.bs) return p.bs[b];  // (device pointer: host code sizes with the even split, bs unset)
   return b * p.ns / p.g;
 }
 // wave v of block b: resident-relative spans [*r0, *r1)
@@ -116,8 +142,18 @@ __host__ __device__ __forceinline__ void part_wave_range(const ScanPart& p, uint
 }
 // the scan wave (b * nw + v) holding resident-relative span rel < ns
 __device__ __forceinline__ uint64_t part_span_wave(const ScanPart& p, uint64_t rel) {
-  uint64_t b = rel * p.g / p.ns;
-  while (b + 1 < p.g && part_block_start(p, b + 1) <= rel) b++;
+  uint64_t b;
+  if (p.bs) {  // the last block whose start is <= rel (empty blocks are skipped over)
+    uint64_t lo = 0, hi = p.g - 1;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) >> 1;
+      if (p.bs[mid] <= rel) lo = mid; else hi = mid - 1;
+    }
+    b = lo;
+  } else {
+    b = rel * p.g / p.ns;
+    while (b + 1 < p.g && part_block_start(p, b + 1) <= rel) b++;
+  }
   const uint64_t bs = part_block_start(p, b), nb = part_block_start(p, b + 1) - bs, o = rel - bs;
   uint32_t v = 0;
 #pragma unroll
@@ -180,6 +216,11 @@ struct ScanArgs {
   // host-side only: the scan variant to launch (0 = the build's default;
   // SRD_DEBUG_API builds A/B the others inside one context)
   uint32_t variant;
+  // XCD-aware block shares (optimistic pass; nullptr: off): the scan records
+  // each block's XCD and duration, link2's block 0 writes the next call's
+  // block starts into xp->bs[xp_next]
+  XPart* xp;
+  uint32_t xp_next;
 };
 
 __device__ __forceinline__ uint32_t ld_dw_guarded(const uint8_t* f, uint64_t n, uint64_t o) {
@@ -590,11 +631,88 @@ __device__ void link_record(const ScanArgs& a, uint64_t w, uint64_t r) {
 // LINK_WPB scan waves per block (256 threads each; 2: 20.7 -> 24.0 us at C2,
 // profiles/r05/kernel_stats_r5k.csv)
 constexpr uint32_t LINK_WPB = 1;
+// The next call's block starts (XPart, block 0 of link2_kernel, 256 threads,
+// after its own records: off the critical path of the call): each XCD's speed
+// = spans / ticks summed over its blocks of this scan, relative to the mean
+// over the XCDs, then w = 0.25 w + 0.75 that (the pattern changes over tens
+// of calls: profiles/r06/xcc_blocks_r6{e,g}.json), clamped to 1 +- XP_CLAMP; block b gets a
+// share of the spans proportional to the speed of the XCD it ran on (the
+// block -> XCD map is fixed per HW queue).  st(0) = 0, st(g) = ns, and no
+// block exceeds (1 + XP_CLAMP) / (1 - XP_CLAMP) of the even share + 1 span
+// (the host's slot-space bound, optimistic_pass).
+__device__ void xpart_update(const ScanArgs& a) {
+  __shared__ unsigned long long s_sp[8], s_du[8];
+  __shared__ float s_w[8];
+  __shared__ double s_pre[256 / 64 + 1];
+  XPart* xp = a.xp;
+  const ScanPart& p = a.part;
+  const uint32_t g = p.g, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t < 8) { s_sp[t] = 0; s_du[t] = 0; }
+  __syncthreads();
+  for (uint32_t b = t; b < g; b += 256) {
+    const uint32_t x = xp->xcc[b] & 7u;
+    atomicAdd(&s_sp[x], (unsigned long long)(part_block_start(p, b + 1) - part_block_start(p, b)));
+    atomicAdd(&s_du[x], (unsigned long long)xp->dur[b]);
+  }
+  __syncthreads();
+  if (t == 0) {
+    float sp[8], mean = 0;
+    int nx = 0;
+    for (int x = 0; x < 8; x++) {
+      sp[x] = s_du[x] && s_sp[x] ? (float)s_sp[x] / (float)s_du[x] : 0.f;
+      if (sp[x] > 0) { mean += sp[x]; nx++; }
+    }
+    mean = nx ? mean / nx : 1.f;
+    for (int x = 0; x < 8; x++) {
+      const float m = sp[x] > 0 ? sp[x] / mean : 1.f, old = xp->w[x];
+      float v = old > 0 ? 0.25f * old + 0.75f * m : m;
+      v = fminf(fmaxf(v, 1.f - XP_CLAMP), 1.f + XP_CLAMP);
+      xp->w[x] = v;
+      s_w[x] = v;
+    }
+  }
+  __syncthreads();
+  // st(b) = round(ns * (q_0 + .. + q_(b-1)) / sum q), q_b = the speed of b's XCD
+  auto q_of = [&](uint32_t b) -> double { return b < g ? (double)s_w[xp->xcc[b] & 7u] : 0.0; };
+  double part = 0;
+  for (uint32_t b = t; b < g; b += 256) part += q_of(b);
+#pragma unroll
+  for (int o = 32; o; o >>= 1) part += __shfl_xor(part, o);
+  if (lane == 0) s_pre[wv] = part;
+  __syncthreads();
+  const double tot = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
+  __syncthreads();
+  uint64_t* nb = xp->bs[a.xp_next];
+  double acc = 0;  // the prefix of the chunks before this one
+  for (uint32_t b0 = 0; b0 < g; b0 += 256) {
+    const uint32_t b = b0 + t;
+    const double q = q_of(b);
+    double x = q;  // inclusive wave prefix
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double y = __shfl_up(x, o);
+      if ((int)lane >= o) x += y;
+    }
+    if (lane == 63) s_pre[wv] = x;
+    __syncthreads();
+    double wpre = 0, ctot = 0;
+    for (uint32_t i = 0; i < 4; i++) {
+      wpre += i < wv ? s_pre[i] : 0.0;
+      ctot += s_pre[i];
+    }
+    __syncthreads();
+    if (b < g) nb[b] = b == 0 ? 0 : (uint64_t)((double)p.ns * ((acc + wpre + x - q) / tot) + 0.5);
+    acc += ctot;
+  }
+  if (t == 0) nb[g] = p.ns;
+}
 __global__ __launch_bounds__(256 * LINK_WPB) void link2_kernel(ScanArgs a, uint32_t n_waves) {
   const uint64_t w = (uint64_t)blockIdx.x * LINK_WPB + threadIdx.x / 256;
-  if (w >= n_waves) return;
-  const uint64_t nrec = min(a.wave_total[w] & ~(1ull << 63), a.wcap);  // records past wcap: ST_OVERFLOW
-  for (uint64_t r = threadIdx.x % 256; r < nrec; r += 256) link_record(a, w, r);
+  if (w < n_waves) {
+    const uint64_t nrec = min(a.wave_total[w] & ~(1ull << 63), a.wcap);  // records past wcap: ST_OVERFLOW
+    for (uint64_t r = threadIdx.x % 256; r < nrec; r += 256) link_record(a, w, r);
+  }
+  if (blockIdx.x == 0 && a.xp) xpart_update(a);
 }
 
 // ---- coalesced nontemporal tile loads (the product scan's, round 5) ----
@@ -681,8 +799,16 @@ void scan_kernel(ScanArgs a) {
     for (uint32_t i = threadIdx.x; i < a.n_zero2; i += blockDim.x) a.zero2[i] = 0;
     if (threadIdx.x == 0 && a.sentinel) *a.sentinel = 0;
   }
+  uint64_t xp_t0 = 0;  // (thread 0) the block's start, XCD-aware shares
+  if (a.xp && threadIdx.x == 0) xp_t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef SRD_WAVE_STAMPS
-  if (threadIdx.x == 0) g_wave_stamp[8192 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    g_wave_stamp[8192 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    uint32_t xcc, hwid;  // the physical XCD and CU the block runs on (tools/xcc_stamps.py)
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    if (blockIdx.x < 256) g_wave_stamp[8192 + 512 + blockIdx.x] = ((uint64_t)hwid << 32) | xcc;
+  }
 #endif
   load_crc_lds(lds);
 #ifdef SRD_WAVE_STAMPS
@@ -1218,6 +1344,12 @@ void scan_kernel(ScanArgs a) {
   __syncthreads();
   uint32_t& s_last = lds.s_last;
   if (threadIdx.x == 0) {
+    if (a.xp && blockIdx.x < XP_MAX_BLOCKS) {  // every wave of the block is done: its XCD and duration
+      uint32_t xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      a.xp->xcc[blockIdx.x] = xcc & 7u;
+      a.xp->dur[blockIdx.x] = (uint32_t)min<uint64_t>(__builtin_amdgcn_s_memrealtime() - xp_t0, 0xFFFFFFFFull);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     s_last = atomicAdd(a.done, 1u) == gridDim.x - 1;

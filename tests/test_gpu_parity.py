@@ -235,6 +235,34 @@ def test_unfused_glue_agrees(golden_cases):
             c.close()
 
 
+def test_xcd_block_shares_repeated_calls():
+    """The optimistic scan sizes its blocks by the measured speed of the XCD
+    each one ran on in the previous call (XPart, srd_kernels.hip): the table
+    is used from the second call on a store of the same span count and grid.
+    Repeated calls -- small grids (C1: 16 blocks) and the full 256-block grid
+    (20,000 x 4 KiB), a Zipf store, and a flipped byte between calls -- must
+    give the oracle's outputs every time, and equal a context with the shares
+    off (SRD_XPART=0)."""
+    rnd = random.Random(71)
+    lens = _zipf_lens(3000, seed=5)
+    stores = [O.synth_store(1000), O.synth_store(20_000), O.synth_store(len(lens), lens=lens)]
+    on, off = S.Context(0), _ctx_with_env(SRD_XPART=0)
+    try:
+        for st in stores:
+            for k in range(5):
+                data = st
+                if k == 3:
+                    data = st.copy()
+                    data[rnd.randrange(data.size)] ^= 0x20
+                r = check_against_oracle(data, on, 0, f"xpart{k}")
+                r2 = S.validate_index(data, 0, off)
+                assert (r.final_len, r.n_chain, r.n_crc_bad) == (r2.final_len, r2.n_chain, r2.n_crc_bad)
+                assert np.array_equal(r.crc_computed, r2.crc_computed) and r.index() == r2.index()
+    finally:
+        on.close()
+        off.close()
+
+
 # key_hash pairs whose Xxh3BuildHasher hashes (XXH3-64 of the 8 LE bytes,
 # key_indexer.rs:98-124) share the low 32 bits and the top 14 bits: the same
 # index bucket at any bucket count and the same 32-bit partial key in the
