@@ -660,6 +660,10 @@ def main():
                                 "the store composed (composed: every shard proven alone); peer_errors = cross-GPU "
                                 "copies staged by the runtime because peer access was refused (0: every exchange "
                                 "read the peers' HBM directly); step = max over shards by construction"}
+    if world == 1:  # the library context's device workspace after the run (srd_ctx_device_bytes)
+        out["workspace_bytes"] = ctx.device_bytes()
+        # the tile-load pattern the pass measured fastest for this store (srd_ctx_scan_loads)
+        out["roofline"]["scan_loads"] = {0: "coalesced + transpose", 1: "line per lane"}.get(ctx.scan_loads(), "none")
     if world == 1 and not args.no_cpu and args.config == "c2":
         out["cpu_baseline"] = cpu_baseline(store, size, bytes_alg, args.cpu_budget)
     if args.e2e and world == 1:

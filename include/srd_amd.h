@@ -93,6 +93,16 @@ int srd_ctx_create(int device, srd_ctx **out);
 void srd_ctx_destroy(srd_ctx *ctx);
 /* The HIP stream the context launches on (hipStream_t as void*). */
 void *srd_ctx_stream(srd_ctx *ctx);
+/* Device bytes the context holds now: its workspace buffers (candidate
+ * records, per-slot glue words, result arrays, index buckets, ...) plus its
+ * staging copy of a host store, if any.  The optimistic pass sizes its
+ * per-slot arrays by slot space (~S / 2048 slots of ~160 B for an S-byte
+ * store at the default 8 slots per 16 KiB span: DESIGN.md section 3). */
+uint64_t srd_ctx_device_bytes(srd_ctx *ctx);
+/* The tile-load pattern of the context's last optimistic scan: 0 coalesced
+ * loads + in-register transpose, 1 line per lane (the pass measures both on
+ * each new store and keeps the faster: DESIGN.md section 4.1); -1 before any. */
+int srd_ctx_scan_loads(srd_ctx *ctx);
 const char *srd_last_error(void);
 /* The sha256 of the sources this library was compiled from (csrc/ +
  * include/srd_amd.h, rust-simd-r-drive_amd/src_hash.py), 64 hex digits;

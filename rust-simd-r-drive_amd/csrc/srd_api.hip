@@ -152,7 +152,19 @@ struct Ctx {
   // 2^31; SRD_SLOT_LIMIT_LOG2 (10..31, read at srd_ctx_create) lowers it so the
   // SRD_FULL_SLOT_SPACE fallback can be tested on a small store
   uint64_t slot_limit = 1ull << 31;
-  uint64_t coal_max = 32ull << 30;  // scan_variant_for's size limit of the coalesced tile loads (SRD_SCAN_LOADS)
+  // the scan's tile loads: SRD_SCAN_LOADS pins one pattern (0 coalesced +
+  // transpose, SCAN_LINES line per lane); -1 = chosen per store by measuring
+  // both (LoadTune, scan_variant_tune)
+  int loads_pin = -1;
+  int last_loads = -1;  // srd_ctx_scan_loads: the last optimistic scan's pattern
+  struct LoadTune {
+    uint64_t ns = ~0ull;       // the store (resident spans, grid) the state is for
+    uint32_t g = 0;
+    uint32_t calls = 0;        // optimistic scans of this store so far
+    double sum[2] = {0, 0};    // measured scan ticks per pattern (0 coalesced, 1 line per lane)
+    uint32_t n[2] = {0, 0};
+    int choice = -1;           // -1: still measuring
+  } tune;
   // round 0 of the optimistic pass runs the shape check inside
   // chain_finalize_kernel<true> (look-back ranks) instead of check_kernel +
   // chain_finalize_kernel<false>; srd_debug_set_glue_fused A/Bs the two
@@ -616,8 +628,8 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   // "coal" (coalesced + transpose); unset = by size (scan_variant_for).  The
   // results are identical either way (tests/test_gpu_parity.py runs both)
   if (const char* e = getenv("SRD_SCAN_LOADS")) {
-    if (!strcmp(e, "lines")) c->coal_max = 0;
-    else if (!strcmp(e, "coal")) c->coal_max = ~0ull;
+    if (!strcmp(e, "lines")) c->loads_pin = SCAN_LINES;
+    else if (!strcmp(e, "coal")) c->loads_pin = 0;
   }
   if (const char* e = getenv("SRD_GLUE_FUSED")) c->glue_fused = strcmp(e, "0") != 0;
   if (const char* e = getenv("SRD_XPART")) c->xpart_on = strcmp(e, "0") != 0;
@@ -663,6 +675,13 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
 }
 
 extern "C" void* srd_ctx_stream(srd_ctx* c) { return c ? (void*)c->stream : nullptr; }
+extern "C" int srd_ctx_scan_loads(srd_ctx* c) { return c ? c->last_loads : -1; }
+extern "C" uint64_t srd_ctx_device_bytes(srd_ctx* c) {
+  if (!c) return 0;
+  uint64_t n = c->file.n;
+  for (const Buf& b : c->bufs) n += b.n;
+  return n;
+}
 
 // A store of another size starts at the default again; a store within 2x of
 // the size whose overflow grew the cap keeps that cap (a dense store would
@@ -941,16 +960,48 @@ static int next_scan_events(Ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
 }
 
 // The scan's tile loads (scan_kernel): coalesced nontemporal loads + an
-// in-register transpose (V 0) for resident spans up to coal_max bytes, round
-// 4's line-per-lane loads (SCAN_LINES) above.  Measured in the same contexts
-// (profiles/r05/variant_ab_coal_*.txt): C2-shaped stores of 4.4 / 8.7 / 17.4
-// GB -7.5 / -6.2 / -5.5 % scan with the coalesced loads, 70 GB +4 %; C3-
-// shaped 4.3 GB -2.5 %, 18 GB +2.4 %, 72.5 GB +4.8 %.  The debug build's
-// srd_debug_set_scan_variant overrides the choice.
-// (Ctx::coal_max = 32 GiB unless SRD_SCAN_LOADS pins one pattern.)
-static uint32_t scan_variant_for(const Ctx* c, uint64_t resident_bytes) {
+// in-register transpose (V 0) or round 4's line-per-lane loads (SCAN_LINES).
+// Which one streams faster depends on the store and on the box: in round 5's
+// same-context A/Bs (profiles/r05/variant_ab_coal_*.txt) the coalesced loads
+// were 7.5 % faster on C2, 4.8 % slower on C3 (72.5 GB), and on round 6's
+// boxes the line-per-lane loads were also faster on C2 in 2 of 3 contexts
+// (profiles/r06/variant_ab_body_stream_c2.txt).  So the optimistic pass
+// measures: for each store (span count, grid) its first scan runs coalesced
+// and is not counted, the next four alternate the patterns, each timed on the
+// device (the scan's first block start to its last block end, XPart::
+// scan_ticks, published with the outcome: no host wait, no event), and the
+// faster mean is kept for the store; it is measured again every 4096 calls.
+// SRD_SCAN_LOADS pins a pattern; the debug build's srd_debug_set_scan_variant
+// overrides both; the full pass takes the current choice (coalesced before one).
+constexpr uint32_t TUNE_WARM = 1, TUNE_TRIAL = 4, TUNE_EVERY = 4096;
+static uint32_t scan_variant_for(const Ctx* c, uint64_t) {
   if (c->scan_variant) return c->scan_variant;
-  return resident_bytes > c->coal_max ? (uint32_t)SCAN_LINES : 0u;
+  if (c->loads_pin >= 0) return (uint32_t)c->loads_pin;
+  return c->tune.choice == 1 ? (uint32_t)SCAN_LINES : 0u;
+}
+static uint32_t scan_variant_tune(Ctx* c, uint64_t ns, uint32_t g) {
+  if (c->scan_variant) return c->scan_variant;
+  if (c->loads_pin >= 0) return (uint32_t)c->loads_pin;
+  Ctx::LoadTune& t = c->tune;
+  if (t.ns != ns || t.g != g || (t.choice >= 0 && t.calls >= TUNE_WARM + TUNE_TRIAL + TUNE_EVERY)) {
+    t = Ctx::LoadTune{};
+    t.ns = ns;
+    t.g = g;
+  }
+  if (t.choice >= 0) return t.choice ? (uint32_t)SCAN_LINES : 0u;
+  const uint32_t i = t.calls;  // the trial's order: coalesced (warm-up), coalesced, lines, coalesced, lines
+  return i >= TUNE_WARM && ((i - TUNE_WARM) & 1) ? (uint32_t)SCAN_LINES : 0u;
+}
+// one optimistic scan of the tuned store done: its pattern and device ticks
+// (0: not measured -- XCD-aware shares off)
+static void scan_tune_feedback(Ctx* c, uint32_t var, uint64_t ticks) {
+  Ctx::LoadTune& t = c->tune;
+  const uint32_t i = t.calls++;
+  if (t.choice >= 0 || i < TUNE_WARM || !ticks || c->scan_variant || c->loads_pin >= 0) return;
+  const int k = var == SCAN_LINES ? 1 : 0;
+  t.sum[k] += (double)ticks;
+  t.n[k]++;
+  if (t.n[0] + t.n[1] >= TUNE_TRIAL && t.n[0] && t.n[1]) t.choice = t.sum[1] / t.n[1] < t.sum[0] / t.n[0] ? 1 : 0;
 }
 
 static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uint64_t* K, uint64_t* h) {
@@ -1108,13 +1159,15 @@ static IdxArgs index_args(Ctx* c, uint32_t log2_nbk) {
 // zeroed here, and idx_hist_scatter_kernel claims the ranges and fills them
 static int launch_index_bucketed(Ctx* c, const uint64_t* kh, const uint64_t* mo, const uint64_t* n_dev,
                                  const uint32_t* status, uint32_t log2_nbk, uint64_t* okey, uint64_t* opacked,
-                                 Plan* pl, bool fused = false, const FinArgs* slow = nullptr, bool zeroed = false) {
+                                 Plan* pl, bool fused = false, const FinArgs* slow = nullptr, bool zeroed = false,
+                                 const uint64_t* scan_ticks = nullptr) {
   TRY(next_lgen(c));
   IdxArgs ia = index_args(c, log2_nbk);
   ia.alias = fused ? 1u : 0u;
   if (fused) {
     ia.pub = c->h_pub;
     ia.pub_seq = ++c->pub_seq;
+    ia.scan_ticks = scan_ticks;  // (the optimistic scan's device time, XPart)
   }
   ia.kh = kh;
   ia.mo = mo;
@@ -1180,10 +1233,12 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
     const uint32_t log2_nbk = index_log2_buckets(n_est);
     // the scan's partition (ScanPart): total_waves waves of at most spw
     // spans; each wave's records are dense in its region of wcap = spw * cap slots
-    // (the variant once: its geometry sizes the partition and the launch)
-    const uint32_t var = scan_variant_for(c, flen - span_off);
+    // (the variant once: its geometry sizes the partition and the launch;
+    // every variant has the same grid)
     uint32_t nw;
-    const unsigned g = scan_grid(c, var, ns_rel, &nw);
+    const unsigned g = scan_grid(c, 0, ns_rel, &nw);
+    const uint32_t var = scan_variant_tune(c, ns_rel, g);
+    c->last_loads = var == SCAN_LINES ? 1 : var == 0 ? 0 : -1;
     ScanPart part = scan_part(c, s_lo, ns_rel, g, nw);
     const bool xpart = c->xpart_on && g <= XP_MAX_BLOCKS;
     XPart* xp = nullptr;
@@ -1370,7 +1425,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
       // ---- KeyIndexer::build (bucketed; the global table in SRD_INDEX_GLOBAL timing builds) ----
       if (!index_global_env()) {
         TRY(launch_index_bucketed(c, f.o_kh, f.o_mo, &pl->n_chain, &pl->status, log2_nbk, P<uint64_t>(c, B_IKEY),
-                                  P<uint64_t>(c, B_IPACKED), pl, true, &f));
+                                  P<uint64_t>(c, B_IPACKED), pl, true, &f, false, xp ? &xp->scan_ticks : nullptr));
       } else {  // timing builds without the bucketed index: the slow list by its own kernel
         slow_kernel<<<2048 / SLOW_WAVES, SLOW_WAVES * 64, 0, c->stream>>>(f);
         KCHK(c, "slow_kernel");
@@ -1390,6 +1445,7 @@ static int optimistic_pass(Ctx* c, const uint8_t* d_span, uint64_t span_off, uin
         const uint32_t fl = (uint32_t)w[0];
         if ((fl & 0x3ffu) == 0x100u) {  // status 0, aliased index, no bucket overflow
           fast = true;
+          scan_tune_feedback(c, var, (uint32_t)w[6]);
           hp = Plan{};
           hp.n_chain = (uint32_t)w[1];
           hp.n_index = (uint32_t)w[2];

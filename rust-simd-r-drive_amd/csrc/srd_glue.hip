@@ -409,7 +409,7 @@ constexpr int IDX_TCAP = 2048;       // max entries per bucket (load <= 1/2)
 // below IDX_TCAP, and an overflowing one sends the build to the global table)
 constexpr int IDX_BUCKET_AVG = 1280;
 constexpr uint64_t IDX_EMPTY = ~0ull;
-constexpr int PUB_WORDS = 6;  // flags, n_chain, n_index, n_bad, K, top_gap
+constexpr int PUB_WORDS = 7;  // flags, n_chain, n_index, n_bad, K, top_gap, the scan's ticks (XPart; 0: none)
 
 struct IdxArgs {
   const uint64_t* kh;    // chain key hashes (o_kh)
@@ -432,6 +432,7 @@ struct IdxArgs {
   uint64_t* pub;
   uint32_t pub_seq;
   uint32_t* ccount;      // [GLUE_BLOCKS] NON-latest entries per chain chunk (idx_dedup -> idx_emit; zero before)
+  const uint64_t* scan_ticks;  // nullable: XPart::scan_ticks of this call's scan (published)
   uint64_t* okey;
   uint64_t* opacked;
   Plan* plan;
@@ -1319,7 +1320,8 @@ __device__ __forceinline__ void publish_outcome(const IdxArgs& a, const Plan* pl
   const uint64_t tag = (uint64_t)a.pub_seq << 32;
   const uint32_t fl = (pl->status & 0xffu) | (a.alias && nl_total == 0 ? 0x100u : 0u) | (pl->idx_overflow ? 0x200u : 0u);
   const uint64_t w[PUB_WORDS] = {tag | fl, tag | (uint32_t)pl->n_chain, tag | (uint32_t)(n - nl_total),
-                                 tag | (uint32_t)pl->n_bad, tag | (uint32_t)pl->K, tag | (uint32_t)pl->top_gap};
+                                 tag | (uint32_t)pl->n_bad, tag | (uint32_t)pl->K, tag | (uint32_t)pl->top_gap,
+                                 tag | (a.scan_ticks ? (uint32_t)min<uint64_t>(*a.scan_ticks, 0xFFFFFFFFull) : 0u)};
 #pragma unroll
   for (int i = 0; i < PUB_WORDS; i++) __hip_atomic_store(a.pub + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

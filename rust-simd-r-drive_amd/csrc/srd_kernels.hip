@@ -121,7 +121,9 @@ struct XPart {
   uint64_t bs[2][XP_MAX_BLOCKS + 1];  // block starts (resident-relative spans) per parity
   uint32_t xcc[XP_MAX_BLOCKS];        // the XCD each block of the last scan ran on
   uint32_t dur[XP_MAX_BLOCKS];        // its duration (s_memrealtime ticks, 10 ns)
+  uint64_t t0[XP_MAX_BLOCKS];         // its start (ticks)
   float w[8];                         // each XCD's relative speed (0: none measured yet)
+  uint64_t scan_ticks;                // the last scan: first block start -> last block end (idx_emit publishes it)
 };
 __host__ __device__ __forceinline__ void part_fill_cw(ScanPart& p) {
   p.cw[0] = 0;
@@ -641,21 +643,26 @@ constexpr uint32_t LINK_WPB = 1;
 // block exceeds (1 + XP_CLAMP) / (1 - XP_CLAMP) of the even share + 1 span
 // (the host's slot-space bound, optimistic_pass).
 __device__ void xpart_update(const ScanArgs& a) {
-  __shared__ unsigned long long s_sp[8], s_du[8];
+  __shared__ unsigned long long s_sp[8], s_du[8], s_t0, s_t1;
   __shared__ float s_w[8];
   __shared__ double s_pre[256 / 64 + 1];
   XPart* xp = a.xp;
   const ScanPart& p = a.part;
   const uint32_t g = p.g, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t < 8) { s_sp[t] = 0; s_du[t] = 0; }
+  if (t == 0) { s_t0 = ~0ull; s_t1 = 0; }
   __syncthreads();
   for (uint32_t b = t; b < g; b += 256) {
     const uint32_t x = xp->xcc[b] & 7u;
+    const uint64_t t0 = xp->t0[b], du = xp->dur[b];
     atomicAdd(&s_sp[x], (unsigned long long)(part_block_start(p, b + 1) - part_block_start(p, b)));
-    atomicAdd(&s_du[x], (unsigned long long)xp->dur[b]);
+    atomicAdd(&s_du[x], (unsigned long long)du);
+    atomicMin(&s_t0, (unsigned long long)t0);
+    atomicMax(&s_t1, (unsigned long long)(t0 + du));
   }
   __syncthreads();
   if (t == 0) {
+    xp->scan_ticks = s_t1 > s_t0 ? s_t1 - s_t0 : 0;  // (the host's load-pattern choice, via idx_emit)
     float sp[8], mean = 0;
     int nx = 0;
     for (int x = 0; x < 8; x++) {
@@ -1349,6 +1356,7 @@ void scan_kernel(ScanArgs a) {
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
       a.xp->xcc[blockIdx.x] = xcc & 7u;
       a.xp->dur[blockIdx.x] = (uint32_t)min<uint64_t>(__builtin_amdgcn_s_memrealtime() - xp_t0, 0xFFFFFFFFull);
+      a.xp->t0[blockIdx.x] = xp_t0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

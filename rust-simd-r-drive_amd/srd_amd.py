@@ -50,7 +50,9 @@ OFFSET_MASK = (1 << 48) - 1
 
 # symbols include/srd_amd.h declares
 EXPORTS = [
-    "srd_ctx_create", "srd_ctx_destroy", "srd_ctx_stream", "srd_last_error", "srd_build_info", "srd_ctx_timings",
+    "srd_ctx_create", "srd_ctx_destroy", "srd_ctx_stream", "srd_ctx_device_bytes", "srd_ctx_scan_loads",
+    "srd_last_error", "srd_build_info",
+    "srd_ctx_timings",
     "srd_ctx_set_timing",
     "srd_validate_index_device", "srd_validate_index", "srd_result_free",
     "srd_recover_valid_chain", "srd_key_indexer_build", "srd_crc32_batch",
@@ -122,6 +124,9 @@ def lib():
         L = C.CDLL(LIB_PATH)
         vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
         L.srd_build_info.restype = C.c_char_p
+        L.srd_ctx_device_bytes.argtypes = [vp]
+        L.srd_ctx_device_bytes.restype = u64
+        L.srd_ctx_scan_loads.argtypes = [vp]
         if not os.environ.get("SRD_LIB_PATH"):  # (timing tools load variant builds by path)
             import importlib.util
             spec = importlib.util.spec_from_file_location("srd_src_hash", os.path.join(HERE, "src_hash.py"))
@@ -178,7 +183,8 @@ def lib():
         L.srd_ctx_multi_shard_ms.argtypes = [vp, C.POINTER(C.c_double), i32]
         L.srd_stream_probe_device.argtypes = [vp, vp, u64, i32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         for f in EXPORTS:
-            if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_last_error", "srd_build_info",
+            if f not in ("srd_ctx_destroy", "srd_result_free", "srd_ctx_stream", "srd_ctx_device_bytes", "srd_last_error",
+                         "srd_build_info",
                          "srd_padded_size", "srd_index_table_bytes"):
                 getattr(L, f).restype = i32
         _lib = L
@@ -229,6 +235,14 @@ class Context:
     def set_timing_every(self, n: int):
         """With TIMING_SCAN: stamp only every n-th scan launch (srd_ctx_set_timing_every)."""
         _check(lib().srd_ctx_set_timing_every(self.h, n))
+
+    def device_bytes(self) -> int:
+        """srd_ctx_device_bytes: the context's device workspace (+ staging copy)."""
+        return int(lib().srd_ctx_device_bytes(self.h))
+
+    def scan_loads(self) -> int:
+        """srd_ctx_scan_loads: 0 coalesced, 1 line per lane, -1 none yet."""
+        return int(lib().srd_ctx_scan_loads(self.h))
 
     def timings(self):
         """(scan_ms, scan_launches) summed over the validate calls since the last

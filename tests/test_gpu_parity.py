@@ -242,22 +242,29 @@ def test_xcd_block_shares_repeated_calls():
     Repeated calls -- small grids (C1: 16 blocks) and the full 256-block grid
     (20,000 x 4 KiB), a Zipf store, and a flipped byte between calls -- must
     give the oracle's outputs every time, and equal a context with the shares
-    off (SRD_XPART=0)."""
+    off (SRD_XPART=0).  The same calls run the per-store choice of the tile-load
+    pattern (scan_variant_tune): both patterns, then the faster one."""
     rnd = random.Random(71)
     lens = _zipf_lens(3000, seed=5)
     stores = [O.synth_store(1000), O.synth_store(20_000), O.synth_store(len(lens), lens=lens)]
     on, off = S.Context(0), _ctx_with_env(SRD_XPART=0)
     try:
         for st in stores:
-            for k in range(5):
+            loads = []
+            for k in range(7):
                 data = st
                 if k == 3:
                     data = st.copy()
                     data[rnd.randrange(data.size)] ^= 0x20
                 r = check_against_oracle(data, on, 0, f"xpart{k}")
+                loads.append(on.scan_loads())
                 r2 = S.validate_index(data, 0, off)
                 assert (r.final_len, r.n_chain, r.n_crc_bad) == (r2.final_len, r2.n_chain, r2.n_crc_bad)
                 assert np.array_equal(r.crc_computed, r2.crc_computed) and r.index() == r2.index()
+            # the tile-load pattern per store: a warm-up call and four measured
+            # calls alternating the two patterns, then the faster one is kept
+            # (a flipped byte keeps the store's span count: still the same store)
+            assert loads[:5] == [0, 0, 1, 0, 1] and loads[5] == loads[6] and loads[5] in (0, 1), loads
     finally:
         on.close()
         off.close()
