@@ -169,6 +169,15 @@ def test_full_c3_properties(ctx):
     st = S.device_to_numpy(r.crc_stored, n, np.uint32)
     assert np.array_equal(ln, lens) and np.array_equal(crc, st)
     assert int(mo[-1]) + 20 == size and np.all(np.diff(mo.astype(np.int64)) > 0)
+    # the whole index (key_indexer.rs:98-124) independently of the device: in
+    # chain order (every key distinct), key i = python-xxhash's XXH3-64 of
+    # b"bench-key-{i}", packed = (hash >> 48) << 48 | its metadata offset
+    ik = S.device_to_numpy(r.index_key_hash, n, np.uint64)
+    iv = S.device_to_numpy(r.index_packed, n, np.uint64)
+    want = np.fromiter((xxhash.xxh3_64_intdigest(b"bench-key-%d" % i) for i in range(n)), np.uint64, n)
+    assert np.array_equal(ik, want)
+    assert np.array_equal(iv, ((want >> np.uint64(48)) << np.uint64(48)) | mo)
+    del ik, iv, want
     for i in np.random.default_rng(5).integers(0, n, 300):
         s0 = int(mo[i] - ln[i])
         assert int(crc[i]) == zlib.crc32(t[s0:int(mo[i])].cpu().numpy().tobytes()), i
@@ -234,6 +243,14 @@ def test_full_c5_write_equals_c2(ctx):
     r = S.validate_index_device(store.data_ptr(), size, 0, ctx)
     assert np.array_equal(S.device_to_numpy(r.index_key_hash, n), kh)
     assert np.array_equal(S.device_to_numpy(r.index_packed, n) & np.uint64((1 << 48) - 1), mo)
+    # independently of the device: every key hash is python-xxhash's XXH3-64 of
+    # the key (compute_hash, digest/compute_hash.rs), every offset the closed
+    # form of the C2 layout (entry i's metadata at 4160 i + 4096), every tag
+    # the hash's top 16 bits (key_indexer.rs:64-93)
+    want = np.array([xxhash.xxh3_64_intdigest(k) for k in keys], np.uint64)
+    assert np.array_equal(kh, want)
+    assert np.array_equal(mo, np.arange(n, dtype=np.uint64) * np.uint64(4160) + np.uint64(4096))
+    assert np.array_equal(S.device_to_numpy(r.index_packed, n) >> np.uint64(48), want >> np.uint64(48))
 
 
 def test_overflow_after_large_call_one_context():
