@@ -146,6 +146,7 @@ struct Ctx {
   CandCap copt{8, 8, 0, 8};
   CandCap cfull{32, 32, 0, 32};
   unsigned scan_blocks = 256;  // persistent scan grid (one 16-wave block per CU)
+  unsigned scan_cus = 256;
   uint32_t scan_wq[16] = {};  // ScanPart::wq (scan_weights())
   uint32_t scan_variant = 0;  // ScanArgs::variant (srd_debug_set_scan_variant)
   // the optimistic pass's slot-space bound (the glue's parent words are 31-bit):
@@ -566,6 +567,11 @@ extern "C" int srd_debug_set_scan_variant(srd_ctx* c, int v) {
   c->scan_variant = (uint32_t)v;
   return 0;
 }
+extern "C" int srd_debug_set_scan_bpc(srd_ctx* c, int bpc) {  // scan blocks per CU (1 or 2; one resident at a time)
+  if (!c || bpc < 1 || bpc > 2) return SRD_ERR_ARG;
+  c->scan_blocks = c->scan_cus * (unsigned)bpc;
+  return 0;
+}
 extern "C" int srd_debug_set_xpart(srd_ctx* c, int on) {  // XCD-aware scan block shares on / off
   if (!c) return SRD_ERR_ARG;
   c->xpart_on = on != 0;
@@ -618,7 +624,7 @@ extern "C" int srd_ctx_create(int device, srd_ctx** out) {
   c->stage_workers = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
-    c->scan_blocks = (unsigned)ncu;
+    c->scan_cus = c->scan_blocks = (unsigned)ncu;
   scan_weights(c->scan_wq);
   if (const char* e = getenv("SRD_SLOT_LIMIT_LOG2")) {
     const long v = strtol(e, nullptr, 10);
