@@ -713,13 +713,58 @@ __device__ void xpart_update(const ScanArgs& a) {
   }
   if (t == 0) nb[g] = p.ns;
 }
+// The optimistic scan's per-wave results reduced (the scan kernel has no
+// last-block epilogue in this pass): k_total[0] = the records, k_total[1] =
+// 1 + the last record's slot, counters[0] = the largest root tail,
+// counters[2] = a region overflowed.  Blocks [0, ceil(n_waves / 256)) of
+// link2_kernel, one scan wave per thread, after their own records, combine
+// their slices with four global atomics (the scan's block 0 zeroed the
+// words); link_record reads wave_total directly, the glue kernels after
+// link2 read these.
+__device__ void scan_reduce(const ScanArgs& a, uint32_t n_waves) {
+  __shared__ unsigned long long s_sum, s_smax, s_rmax, s_ovf;
+  if (threadIdx.x == 0) { s_sum = 0; s_smax = 0; s_rmax = 0; s_ovf = 0; }
+  __syncthreads();
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  uint64_t sum = 0, smax = 0, rmax = 0, o = 0;
+  if (i < n_waves) {
+    const uint64_t v = a.wave_total[i], cnt = v & ~(1ull << 63);
+    sum = cnt;
+    o = v >> 63;
+    rmax = a.wave_root[i];
+    if (cnt) smax = (uint64_t)i * a.wcap + min(cnt, a.wcap);
+  }
+  rmax = wave_max_u64(rmax);
+  smax = wave_max_u64(smax);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    o |= __shfl_xor(o, d);
+    sum += __shfl_xor(sum, d);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&s_sum, (unsigned long long)sum);
+    atomicMax(&s_smax, (unsigned long long)smax);
+    atomicMax(&s_rmax, (unsigned long long)rmax);
+    atomicOr(&s_ovf, (unsigned long long)o);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd((unsigned long long*)&a.k_total[0], s_sum);
+    atomicMax((unsigned long long*)&a.k_total[1], s_smax);
+    atomicMax((unsigned long long*)&a.counters[0], s_rmax);
+    atomicOr((unsigned long long*)&a.counters[2], s_ovf);
+  }
+}
 __global__ __launch_bounds__(256 * LINK_WPB) void link2_kernel(ScanArgs a, uint32_t n_waves) {
   const uint64_t w = (uint64_t)blockIdx.x * LINK_WPB + threadIdx.x / 256;
   if (w < n_waves) {
     const uint64_t nrec = min(a.wave_total[w] & ~(1ull << 63), a.wcap);  // records past wcap: ST_OVERFLOW
     for (uint64_t r = threadIdx.x % 256; r < nrec; r += 256) link_record(a, w, r);
   }
-  if (blockIdx.x == 0 && a.xp) xpart_update(a);
+  if ((uint64_t)blockIdx.x * 256 < n_waves) scan_reduce(a, n_waves);
+  // the next call's block starts in a block of the first dispatch round that
+  // reduces no slice (C2: 4096 waves -> blocks 0-15 reduce, 16 does this)
+  if (a.xp && blockIdx.x == min((n_waves + 255) / 256, gridDim.x - 1)) xpart_update(a);
 }
 
 // ---- coalesced nontemporal tile loads (the product scan's, round 5) ----
@@ -788,7 +833,7 @@ void scan_kernel(ScanArgs a) {
   constexpr int NW = SCAN_WAVES_V2;
   // The product loads each tile coalesced + nontemporal and transposes it in
   // registers (coal_to_lines); SCAN_LINES = round 4's line-per-lane loads
-  // (stores above Ctx::coal_max, srd_api.hip scan_variant_for).  Timing-only
+  // (the pass measures both per store: srd_api.hip scan_variant_tune).  Timing-only
   // ablations of SRD_DEBUG_API builds (results wrong; tools/variant_ab.py):
   // 7 = the ring's coalesced loads alone (each tile XOR-folded), 8 = the whole
   // coalesced tile body on two L2-resident tiles per block (no HBM stream).
@@ -805,6 +850,12 @@ void scan_kernel(ScanArgs a) {
     for (uint32_t i = threadIdx.x; i < a.n_zero_words; i += blockDim.x) a.zero_words[i] = 0;
     for (uint32_t i = threadIdx.x; i < a.n_zero2; i += blockDim.x) a.zero2[i] = 0;
     if (threadIdx.x == 0 && a.sentinel) *a.sentinel = 0;
+    if (!FULL && threadIdx.x == 0) {  // link2's scan_reduce combines into these
+      a.k_total[0] = 0;
+      a.k_total[1] = 0;
+      a.counters[0] = 0;
+      a.counters[2] = 0;
+    }
   }
   uint64_t xp_t0 = 0;  // (thread 0) the block's start, XCD-aware shares
   if (a.xp && threadIdx.x == 0) xp_t0 = __builtin_amdgcn_s_memrealtime();
@@ -1337,9 +1388,7 @@ void scan_kernel(ScanArgs a) {
   if constexpr (MEMONLY) {
     if (memonly_acc == 0x12345678u) a.counters[3] = memonly_acc;  // (keeps the loads)
   }
-  // ---- epilogue: per-wave results; the last block to finish reduces them
-  // (cdna guide: plain stores, vmcnt(0), barrier, lane-0 agent release, add;
-  // the last block acquires before reading) ----
+  // ---- epilogue: per-wave results ----
   if (lane == 0) {
     a.wave_total[w] = wtotal | (ovf ? (1ull << 63) : 0ull);
     a.wave_root[w] = rootmax;  // wave-uniform already
@@ -1347,17 +1396,34 @@ void scan_kernel(ScanArgs a) {
     if (w < 8192) g_wave_stamp[w] = __builtin_amdgcn_s_memrealtime();
 #endif
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  uint32_t& s_last = lds.s_last;
-  if (threadIdx.x == 0) {
-    if (a.xp && blockIdx.x < XP_MAX_BLOCKS) {  // every wave of the block is done: its XCD and duration
+  if (a.xp) {  // (uniform) every wave of the block is done: its XCD and duration
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < XP_MAX_BLOCKS) {
       uint32_t xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
       a.xp->xcc[blockIdx.x] = xcc & 7u;
       a.xp->dur[blockIdx.x] = (uint32_t)min<uint64_t>(__builtin_amdgcn_s_memrealtime() - xp_t0, 0xFFFFFFFFull);
       a.xp->t0[blockIdx.x] = xp_t0;
     }
+  }
+  if constexpr (!FULL) {
+    // The optimistic pass: no last-block reduction here.  Its agent-scope
+    // release (an L2 write-back of every block's XCD, ~4 MB of dirty record
+    // lines) and the reduction sat on the critical path of every call: the
+    // last block ended 7-8 us before the kernel did (tools/wave_stamps.py,
+    // profiles/r06/wave_stamps_r6m.txt).  link2_kernel's block 0 reduces the
+    // wave totals instead (scan_reduce), after the kernel boundary;
+    // find_top's tail (the same value in every wave) goes out from block 0.
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[1] = top;
+    return;
+  }
+  // (the full pass: the last block to finish reduces them -- cdna guide: plain
+  // stores, vmcnt(0), barrier, lane-0 agent release, add; the last block
+  // acquires before reading)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t& s_last = lds.s_last;
+  if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     s_last = atomicAdd(a.done, 1u) == gridDim.x - 1;

@@ -322,8 +322,9 @@ def _ctx_with_loads(mode):
 @pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
 def test_scan_load_patterns_agree(golden_cases, flags):
     """The scan loads a tile either coalesced + nontemporal with an in-register
-    transpose to line-per-lane order (stores up to 32 GiB) or line per lane
-    (above); SRD_SCAN_LOADS pins one pattern for a context.  Both must give
+    transpose to line-per-lane order or line per lane (the optimistic pass
+    measures both per store and keeps the faster); SRD_SCAN_LOADS pins one
+    pattern for a context.  Both must give
     the oracle's outputs on every golden fixture and on mixed-size, tombstone,
     torn and flipped stores, in both passes."""
     rnd = random.Random(23)
