@@ -45,12 +45,12 @@
 
 namespace srd {
 
-// The glue's per-entry outputs (~100 MB per C2 call) are written with
-// nontemporal stores: kept as dirty lines in L2 / the Infinity Cache they were
-// written back while the NEXT call's scan streamed the store (same-process
-// A/B, three contexts each: scan -1 %, call -1 %, profiles/r03/
-// scan_record_regions_ab.txt)
-#define GST(ptr, val) __builtin_nontemporal_store((val), &(ptr))
+// The glue's per-entry outputs (~100 MB per C2 call) are not left as dirty
+// lines in L2: round 3 made them nontemporal (written back while the NEXT
+// call's scan streamed the store: scan -1 %, call -1 %, profiles/r03/
+// scan_record_regions_ab.txt), round 6 writes them through (srd_gst,
+// srd_kernels.hip)
+#define GST(ptr, val) srd_gst(&(ptr), (val))  // (srd_kernels.hip: written through the XCD's L2)
 
 struct Plan {
   uint64_t K;          // dense candidates

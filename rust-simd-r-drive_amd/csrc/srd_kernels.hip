@@ -244,6 +244,25 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* f, uint64_t 
 }
 __device__ __forceinline__ uint64_t prepad64(uint64_t o) { return (64 - (o & 63)) & 63; }
 
+// Stores of results another kernel reads (the glue's outputs, the scan's
+// records and tile values): relaxed system-scope stores (sc0 sc1), written
+// through the XCD's L2 instead of sitting there dirty.  Dirty lines were
+// written back while the scan streamed (and at every kernel's end, before the
+// next one started); in the same process, scan + glue write-through vs the
+// round-5 policies (plain scan stores, nontemporal glue stores): call -2.3 /
+// -4.5 % on two boxes, and the contexts' spread shrank (profiles/r06/
+// lib_ab_store_policy_*.txt).  SRD_GLUE_STORE: 0 nontemporal (round 5), 1
+// system scope (default), 2 agent scope (a timing A/B knob).
+#ifndef SRD_GLUE_STORE
+#define SRD_GLUE_STORE 1
+#endif
+template <class T, class V>
+__device__ __forceinline__ void srd_gst(T* p, V v) {
+  if constexpr (SRD_GLUE_STORE == 1) __hip_atomic_store(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else if constexpr (SRD_GLUE_STORE == 2) __hip_atomic_store(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __builtin_nontemporal_store((T)v, p);
+}
+
 // A claim on a parent: the generation in the high word (stale words of
 // earlier calls lose any atomicMax), ~g in the low word, so the claimer with
 // the SMALLEST slot (file order) holds the parent.  The real child of p is
@@ -618,6 +637,8 @@ __device__ void link_record(const ScanArgs& a, uint64_t w, uint64_t r) {
       par = PAR_ROOT;  // the parent is the root entry (prev 0), data_store.rs:404-416
     }
   }
+  // (plain stores: written through like the scan's records, link2's own
+  // words made the glue 3-5 us slower, profiles/r06/lib_ab_store_policy_r6u.txt)
   if (tomb) a.c_rec[gi] = u32x4{r0[0], r0[1], r0[2] | F_TOMB, r0[3]};
   a.d_par[gi] = (int32_t)par;
   if (par >= 0) atomicMax(&a.childof[par], claim_word(a.gen, gi));
@@ -1283,12 +1304,19 @@ void scan_kernel(ScanArgs a) {
   // six per tile cost 7-8 %, profiles/r04/variant_ab_no_stores.txt), so the
   // ring loop runs one store point per round of 3 tiles, not one per tile (a
   // round completes at most one group of either kind).
+  // the store points' cache policy (buffer-store aux bits): sc0 sc1, written
+  // through the XCD's L2 (srd_gst above; 0 = plain write-back: the round-5
+  // stores, 2 = nt, 16 = sc1 -- timing A/B builds)
+#ifndef SRD_SCAN_STORE_AUX
+#define SRD_SCAN_STORE_AUX 17
+#endif
+  constexpr int SCAN_STORE_AUX = SRD_SCAN_STORE_AUX;
   auto store_point = [&](uint64_t kf, uint32_t nt) {
     if constexpr (MEMONLY) return;
     const bool last = kf + nt == k1;  // uniform
     {
       const uint32_t off = tg_pend && (uint32_t)lane - tg_lo < tg_hi - tg_lo ? 4u * lane : OOB_OFF;
-      __builtin_amdgcn_raw_buffer_store_b32(tg_par ? tacc1 : tacc0, out_rsrc(a.tile + 4 * tg_base, 256), off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(tg_par ? tacc1 : tacc0, out_rsrc(a.tile + 4 * tg_base, 256), off, 0, SCAN_STORE_AUX);
       tg_pend = false;
     }
     {
@@ -1300,12 +1328,12 @@ void scan_kernel(ScanArgs a) {
       const uint64_t rb = w * a.wcap + flushed;  // lane 0's record
       const uint32_t rn = (uint32_t)min<uint64_t>(a.wcap - min(flushed, a.wcap), 64);  // slots left (OOB past)
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{rq[0], rq[1]}, out_rsrc(a.c_m + rb, rn * 8),
-                                            wr ? 8u * lane : OOB_OFF, 0, 0);
+                                            wr ? 8u * lane : OOB_OFF, 0, SCAN_STORE_AUX);
       // the record's halves: {p, flags, crc}, {key_hash, sxm, suf}
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[5], rq[6], rq[4], rq[9]}, out_rsrc(a.c_rec + rb, rn * 16),
-                                             wr ? 16u * lane : OOB_OFF, 0, 0);
+                                             wr ? 16u * lane : OOB_OFF, 0, SCAN_STORE_AUX);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{rq[7], rq[8], rq[2], rq[3]}, out_rsrc(a.c_rec1 + rb, rn * 16),
-                                             wr ? 16u * lane : OOB_OFF, 0, 0);
+                                             wr ? 16u * lane : OOB_OFF, 0, SCAN_STORE_AUX);
       if (fl) {
         flushed = wtotal + count;
         rvalid = 0;
@@ -1313,8 +1341,8 @@ void scan_kernel(ScanArgs a) {
     }
     {
       const uint32_t soff = sg_pend && (uint32_t)lane >= sg_lo && (uint32_t)lane <= sg_hi ? 4u * lane : OOB_OFF;
-      __builtin_amdgcn_raw_buffer_store_b32(scnt, out_rsrc(a.span_count + sg_base, 256), soff, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(sfirst, out_rsrc(a.span_first + sg_base, 256), soff, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(scnt, out_rsrc(a.span_count + sg_base, 256), soff, 0, SCAN_STORE_AUX);
+      __builtin_amdgcn_raw_buffer_store_b32(sfirst, out_rsrc(a.span_first + sg_base, 256), soff, 0, SCAN_STORE_AUX);
       sg_pend = false;
     }
   };
