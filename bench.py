@@ -664,6 +664,8 @@ def main():
         out["workspace_bytes"] = ctx.device_bytes()
         # the tile-load pattern the pass measured fastest for this store (srd_ctx_scan_loads)
         out["roofline"]["scan_loads"] = {0: "coalesced + transpose", 1: "line per lane"}.get(ctx.scan_loads(), "none")
+        _, t_co, t_li = ctx.scan_trial()  # the trial's fastest device-timed scan per pattern (srd_ctx_scan_trial)
+        out["roofline"]["scan_loads_trial_ms"] = {"coalesced": round(t_co, 4), "lines": round(t_li, 4)}
     if world == 1 and not args.no_cpu and args.config == "c2":
         out["cpu_baseline"] = cpu_baseline(store, size, bytes_alg, args.cpu_budget)
     if args.e2e and world == 1:

@@ -103,6 +103,11 @@ uint64_t srd_ctx_device_bytes(srd_ctx *ctx);
  * loads + in-register transpose, 1 line per lane (the pass measures both on
  * each new store and keeps the faster: DESIGN.md section 4.1); -1 before any. */
 int srd_ctx_scan_loads(srd_ctx *ctx);
+/* The load-pattern trial of the current store: ms[0] / ms[1] = the fastest
+ * device-timed optimistic scan with coalesced / line-per-lane loads so far (0
+ * if not measured); returns the choice (0, 1) or -1 while still measuring
+ * (or pinned by SRD_SCAN_LOADS, or with XCD-aware shares off). */
+int srd_ctx_scan_trial(srd_ctx *ctx, double *ms);
 const char *srd_last_error(void);
 /* The sha256 of the sources this library was compiled from (csrc/ +
  * include/srd_amd.h, rust-simd-r-drive_amd/src_hash.py), 64 hex digits;

@@ -162,7 +162,7 @@ struct Ctx {
     uint64_t ns = ~0ull;       // the store (resident spans, grid) the state is for
     uint32_t g = 0;
     uint32_t calls = 0;        // optimistic scans of this store so far
-    double sum[2] = {0, 0};    // measured scan ticks per pattern (0 coalesced, 1 line per lane)
+    uint64_t best[2] = {0, 0};  // the fastest scan of each pattern, ticks (0 coalesced, 1 line per lane)
     uint32_t n[2] = {0, 0};
     int choice = -1;           // -1: still measuring
   } tune;
@@ -682,6 +682,12 @@ extern "C" void srd_ctx_destroy(srd_ctx* c) {
 
 extern "C" void* srd_ctx_stream(srd_ctx* c) { return c ? (void*)c->stream : nullptr; }
 extern "C" int srd_ctx_scan_loads(srd_ctx* c) { return c ? c->last_loads : -1; }
+extern "C" int srd_ctx_scan_trial(srd_ctx* c, double* ms) {
+  if (!c) return -1;
+  if (ms)
+    for (int k = 0; k < 2; k++) ms[k] = c->tune.n[k] ? (double)c->tune.best[k] * 1e-5 : 0.0;  // 10 ns ticks
+  return c->tune.choice;
+}
 extern "C" uint64_t srd_ctx_device_bytes(srd_ctx* c) {
   if (!c) return 0;
   uint64_t n = c->file.n;
@@ -973,13 +979,17 @@ static int next_scan_events(Ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
 // boxes the line-per-lane loads were also faster on C2 in 2 of 3 contexts
 // (profiles/r06/variant_ab_body_stream_c2.txt).  So the optimistic pass
 // measures: for each store (span count, grid) its first scan runs coalesced
-// and is not counted, the next four alternate the patterns, each timed on the
+// and is not counted, the next ones alternate the patterns, each timed on the
 // device (the scan's first block start to its last block end, XPart::
 // scan_ticks, published with the outcome: no host wait, no event), and the
-// faster mean is kept for the store; it is measured again every 4096 calls.
+// pattern with the faster best time is kept for the store: from the fourth
+// measured call on as soon as the bests differ by more than TUNE_MARGIN, at
+// the eighth in any case (a close call costs little either way); measured
+// again every 4096 calls.  srd_ctx_scan_trial reports the two best times.
 // SRD_SCAN_LOADS pins a pattern; the debug build's srd_debug_set_scan_variant
 // overrides both; the full pass takes the current choice (coalesced before one).
-constexpr uint32_t TUNE_WARM = 1, TUNE_TRIAL = 4, TUNE_EVERY = 4096;
+constexpr uint32_t TUNE_WARM = 1, TUNE_TRIAL = 4, TUNE_TRIAL_MAX = 8, TUNE_EVERY = 4096;
+constexpr double TUNE_MARGIN = 0.02;
 static uint32_t scan_variant_for(const Ctx* c, uint64_t) {
   if (c->scan_variant) return c->scan_variant;
   if (c->loads_pin >= 0) return (uint32_t)c->loads_pin;
@@ -989,13 +999,13 @@ static uint32_t scan_variant_tune(Ctx* c, uint64_t ns, uint32_t g) {
   if (c->scan_variant) return c->scan_variant;
   if (c->loads_pin >= 0) return (uint32_t)c->loads_pin;
   Ctx::LoadTune& t = c->tune;
-  if (t.ns != ns || t.g != g || (t.choice >= 0 && t.calls >= TUNE_WARM + TUNE_TRIAL + TUNE_EVERY)) {
+  if (t.ns != ns || t.g != g || (t.choice >= 0 && t.calls >= TUNE_WARM + TUNE_TRIAL_MAX + TUNE_EVERY)) {
     t = Ctx::LoadTune{};
     t.ns = ns;
     t.g = g;
   }
   if (t.choice >= 0) return t.choice ? (uint32_t)SCAN_LINES : 0u;
-  const uint32_t i = t.calls;  // the trial's order: coalesced (warm-up), coalesced, lines, coalesced, lines
+  const uint32_t i = t.calls;  // the trial's order: coalesced (warm-up), then coalesced, lines, coalesced, ...
   return i >= TUNE_WARM && ((i - TUNE_WARM) & 1) ? (uint32_t)SCAN_LINES : 0u;
 }
 // one optimistic scan of the tuned store done: its pattern and device ticks
@@ -1005,9 +1015,12 @@ static void scan_tune_feedback(Ctx* c, uint32_t var, uint64_t ticks) {
   const uint32_t i = t.calls++;
   if (t.choice >= 0 || i < TUNE_WARM || !ticks || c->scan_variant || c->loads_pin >= 0) return;
   const int k = var == SCAN_LINES ? 1 : 0;
-  t.sum[k] += (double)ticks;
+  if (!t.n[k] || ticks < t.best[k]) t.best[k] = ticks;
   t.n[k]++;
-  if (t.n[0] + t.n[1] >= TUNE_TRIAL && t.n[0] && t.n[1]) t.choice = t.sum[1] / t.n[1] < t.sum[0] / t.n[0] ? 1 : 0;
+  const uint32_t m = t.n[0] + t.n[1];
+  if (m < TUNE_TRIAL || !t.n[0] || !t.n[1]) return;
+  const double b0 = (double)t.best[0], b1 = (double)t.best[1];
+  if (m >= TUNE_TRIAL_MAX || fabs(b0 - b1) > TUNE_MARGIN * fmin(b0, b1)) t.choice = b1 < b0 ? 1 : 0;
 }
 
 static int run_scan(Ctx* c, const uint8_t* d_file, uint64_t flen, bool full, uint64_t* K, uint64_t* h) {

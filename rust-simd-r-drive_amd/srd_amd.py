@@ -51,6 +51,7 @@ OFFSET_MASK = (1 << 48) - 1
 # symbols include/srd_amd.h declares
 EXPORTS = [
     "srd_ctx_create", "srd_ctx_destroy", "srd_ctx_stream", "srd_ctx_device_bytes", "srd_ctx_scan_loads",
+    "srd_ctx_scan_trial",
     "srd_last_error", "srd_build_info",
     "srd_ctx_timings",
     "srd_ctx_set_timing",
@@ -127,6 +128,7 @@ def lib():
         L.srd_ctx_device_bytes.argtypes = [vp]
         L.srd_ctx_device_bytes.restype = u64
         L.srd_ctx_scan_loads.argtypes = [vp]
+        L.srd_ctx_scan_trial.argtypes = [vp, C.POINTER(C.c_double)]
         if not os.environ.get("SRD_LIB_PATH"):  # (timing tools load variant builds by path)
             import importlib.util
             spec = importlib.util.spec_from_file_location("srd_src_hash", os.path.join(HERE, "src_hash.py"))
@@ -243,6 +245,12 @@ class Context:
     def scan_loads(self) -> int:
         """srd_ctx_scan_loads: 0 coalesced, 1 line per lane, -1 none yet."""
         return int(lib().srd_ctx_scan_loads(self.h))
+
+    def scan_trial(self):
+        """srd_ctx_scan_trial: (choice, best coalesced ms, best line-per-lane ms); choice -1 = still measuring."""
+        ms = (C.c_double * 2)()
+        ch = int(lib().srd_ctx_scan_trial(self.h, ms))
+        return ch, float(ms[0]), float(ms[1])
 
     def timings(self):
         """(scan_ms, scan_launches) summed over the validate calls since the last
