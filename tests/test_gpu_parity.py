@@ -418,6 +418,78 @@ def test_torn_and_corrupted(ctx):
         check_against_oracle(np.concatenate([store, np.frombuffer(b"CORRUPT", np.uint8)]), ctx, 0, "corrupt")
 
 
+def _fuzz_store(rnd):
+    """A random store built by batch_write_with_key_hashes (data_store.rs:847-939):
+    overwrites from a small key pool, tombstones (a lone NULL byte,
+    data_store.rs:995-1015), zero-heavy payloads, and payloads that embed a
+    forged metadata record (key hash, a prev offset that is an earlier entry's
+    end or junk, a nonzero checksum) at a random alignment -- false candidates
+    for the scan's node filter (data_store.rs:404-470)."""
+    buf = bytearray()
+    t = 0
+    ends = [0]
+    for _ in range(rnd.randrange(1, 120)):
+        batch = []
+        for _ in range(rnd.choice([1, 1, 1, 2, 5])):
+            kh = xxhash.xxh3_64_intdigest(b"fz%d" % rnd.randrange(40))
+            kind = rnd.random()
+            if kind < 0.12:
+                batch.append((kh, b"\x00"))
+                continue
+            n = rnd.choice([1, 2, 7, 19, 20, 21, 63, 64, 65, 100, 500, 2047, 4096, 4100, 9000, rnd.randrange(1, 20000)])
+            if kind < 0.35:
+                pl = bytearray(n)  # zeros with a few set bytes: aligned zero halfwords everywhere
+                for _ in range(max(1, n // 64)):
+                    pl[rnd.randrange(n)] = rnd.randrange(1, 256)
+            else:
+                pl = bytearray(rnd.randbytes(n))
+            if kind > 0.7 and n >= 40:
+                prev = rnd.choice(ends) if rnd.random() < 0.8 else rnd.randrange(1 << 20)
+                forged = struct.pack("<QQI", rnd.getrandbits(64), prev, rnd.randrange(1, 1 << 32))
+                at = rnd.randrange(0, n - 20 + 1)
+                pl[at:at + 20] = forged
+            if bytes(pl) == b"\x00":
+                pl = bytearray(b"\x01")
+            batch.append((kh, bytes(pl)))
+        t = O.write_entries(buf, t, batch, allow_null=True)
+        ends.append(t)
+    store = np.frombuffer(bytes(buf), np.uint8).copy()
+    cut = rnd.random()
+    if cut < 0.15 and store.size > 1:
+        store = store[: rnd.randrange(1, store.size)]
+    elif cut < 0.25 and len(ends) > 2:
+        e = rnd.choice(ends[1:])
+        store = store[: max(1, min(store.size, e + rnd.choice([-21, -20, -19, -1, 1, 7])))]
+    elif cut < 0.35:
+        tail = b"CORRUPT" if rnd.random() < 0.5 else rnd.randbytes(rnd.randrange(1, 300))
+        store = np.concatenate([store, np.frombuffer(tail, np.uint8)])
+    elif cut < 0.5 and store.size:
+        pos = rnd.randrange(max(0, store.size - 20), store.size) if rnd.random() < 0.5 else rnd.randrange(store.size)
+        store[pos] ^= 1 << rnd.randrange(8)
+    elif cut < 0.55 and store.size >= 64:
+        at = rnd.randrange(0, store.size - 63)
+        store[at:at + 64] = 0
+    return store
+
+
+def test_fuzz_adversarial_stores(ctx):
+    """120 random stores (_fuzz_store), each then torn, cut around an entry
+    end, given a junk or b"CORRUPT" tail, bit-flipped (often inside the last
+    metadata record) or given a zeroed line -- both passes against the
+    oracle's recover_valid_chain / chain / KeyIndexer::build."""
+    rnd = random.Random(2026)
+    modes = {S.SRD_MODE_OPTIMISTIC: 0, S.SRD_MODE_FULL: 0}
+    for i in range(120):
+        store = _fuzz_store(rnd)
+        for flags in (0, S.SRD_FLAG_FORCE_FULL):
+            r = check_against_oracle(store, ctx, flags, "fuzz%d/%d" % (i, flags))
+            if flags == 0:
+                modes[r.mode] = modes.get(r.mode, 0) + 1
+    # both passes ran on the default flags: most stores stay optimistic, the
+    # damaged ones take the full pass
+    assert modes[S.SRD_MODE_OPTIMISTIC] > 0 and modes[S.SRD_MODE_FULL] > 0, modes
+
+
 @pytest.mark.parametrize("flags", [0, S.SRD_FLAG_FORCE_FULL])
 def test_torn_tail_start_search(ctx, flags):
     """recover_valid_chain walks the cursor down from file_len and skips every
