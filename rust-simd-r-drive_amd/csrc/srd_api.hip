@@ -3345,6 +3345,12 @@ extern "C" int srd_debug_wave_stamps(uint64_t* out) {
   HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_stamp), sizeof(uint64_t) * (8192 + 1024)));
   return 0;
 }
+// and the shader-clock counter (s_memtime) at the same wave ends / block starts
+extern "C" int srd_debug_wave_clk(uint64_t* out) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_clk), sizeof(uint64_t) * (4096 + 256)));
+  return 0;
+}
 #endif
 
 // host self-test of the CRC algebra (no GPU): checks the tables against a

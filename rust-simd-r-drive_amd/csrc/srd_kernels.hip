@@ -79,6 +79,9 @@ struct DevTables {
 __device__ DevTables g_tabs;
 #ifdef SRD_WAVE_STAMPS
 __device__ uint64_t g_wave_stamp[8192 + 1024];  // [w]: wave w's end; [8192 + b]: block b's start;
+#ifdef SRD_WAVE_STAMPS
+__device__ uint64_t g_wave_clk[4096 + 256];  // s_memtime (shader clock) at wave w's end / block b's start: the scan's clock
+#endif
                                                 // [8192 + 256 + b]: its tables loaded; [8192 + 512 + b]: its
                                                 // XCC_ID; [8192 + 1023]: the epilogue's end
 #endif
@@ -883,6 +886,7 @@ void scan_kernel(ScanArgs a) {
 #ifdef SRD_WAVE_STAMPS
   if (threadIdx.x == 0) {
     g_wave_stamp[8192 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x < 256) g_wave_clk[4096 + blockIdx.x] = __builtin_amdgcn_s_memtime();
     uint32_t xcc, hwid;  // the physical XCD and CU the block runs on (tools/xcc_stamps.py)
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
@@ -1422,6 +1426,7 @@ void scan_kernel(ScanArgs a) {
     a.wave_root[w] = rootmax;  // wave-uniform already
 #ifdef SRD_WAVE_STAMPS  // timing-only build (tools/wave_stamps.py): each wave's end, 100 MHz clock
     if (w < 8192) g_wave_stamp[w] = __builtin_amdgcn_s_memrealtime();
+    if (w < 4096) g_wave_clk[w] = __builtin_amdgcn_s_memtime();
 #endif
   }
   if (a.xp) {  // (uniform) every wave of the block is done: its XCD and duration
