@@ -796,15 +796,18 @@ __global__ __launch_bounds__(256 * LINK_WPB) void link2_kernel(ScanArgs a, uint3
 // ~6.0-6.1 TB/s; loads whose every instruction reads 1 KiB contiguous, with
 // the nontemporal bit, at ~6.75 TB/s (tools/stream_map_probe.hip,
 // profiles/r05/stream_cpol_probe.txt; nt on the line-per-lane pattern: 3.6).
-// The load puts lane l = 16A + 4B + C on 16 B at 1024 j + 256 A + 64 C + 16 B
-// (quarter B of line 16 j + 4 A + C; each 16-lane row reads 256 contiguous
-// bytes), and two register <-> lane field swaps move line L to lane L,
-// quarter q to dwords 4q..4q+3: the register field with lane bits 4-5 by
-// v_permlane16/32_swap, then with lane bits 2-3 by DPP row shifts under bank
-// masks (bank = lane bits 2-3): 16 + 32 VALU per tile, no selects.
+// The load puts lane l = 16 B + 4 A + C on 16 B at 1024 j + 256 A + 64 C + 16 B
+// (quarter B of line 16 j + 4 A + C; every instruction reads its 1 KiB whole,
+// each 16-lane row 16 B of 16 lines), so the quarter index sits in lane bits
+// 4-5 and two register <-> lane field swaps by v_permlane16/32_swap move line L
+// to lane L, quarter q to dwords 4q..4q+3: 16 VALU per tile.  (Rounds 5-6a
+// put the quarter in lane bits 2-3 -- 256 contiguous bytes per row -- and
+// needed 32 DPP bank swaps + 16 copies more for the same loads: the
+// quarter-in-row layout streams alike and the scan runs 1-2 % faster at C2,
+// 4-5 % at C3, profiles/r06/variant_ab_rowq_c{2,3}.txt)
 __device__ __forceinline__ uint32_t coal_lane_off(int lane, int j) {
-  return 1024u * (uint32_t)j + 256u * ((uint32_t)lane >> 4) + 64u * ((uint32_t)lane & 3u) +
-         16u * (((uint32_t)lane >> 2) & 3u);
+  return 1024u * (uint32_t)j + 256u * (((uint32_t)lane >> 2) & 3u) + 64u * ((uint32_t)lane & 3u) +
+         16u * ((uint32_t)lane >> 4);
 }
 template <int RB, bool P32>
 __device__ __forceinline__ void coal_pswap(uint32_t (&d)[16]) {  // register bit RB <-> lane bit 4 (P32: 5)
@@ -821,27 +824,9 @@ __device__ __forceinline__ void coal_pswap(uint32_t (&d)[16]) {  // register bit
     }
   }
 }
-template <int S, int RB>
-__device__ __forceinline__ void coal_bswap(uint32_t (&d)[16]) {  // register bit RB <-> lane bit S (4, 8)
-  constexpr int SHL = 0x100 + S, SHR = 0x110 + S;
-  constexpr int HI = S == 4 ? 0xA : 0xC, LO = S == 4 ? 0x5 : 0x3;  // banks with / without lane bit S
-#pragma unroll
-  for (int r0 = 0; r0 < 4; r0++) {
-    if (r0 & RB) continue;
-    const int r1 = r0 | RB;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int a = (int)d[4 * r0 + i], b = (int)d[4 * r1 + i];
-      d[4 * r0 + i] = (uint32_t)__builtin_amdgcn_update_dpp(a, b, SHR, 0xF, HI, false);  // lanes with bit S <- b[l - S]
-      d[4 * r1 + i] = (uint32_t)__builtin_amdgcn_update_dpp(b, a, SHL, 0xF, LO, false);  // lanes without <- a[l + S]
-    }
-  }
-}
 __device__ __forceinline__ void coal_to_lines(uint32_t (&d)[16]) {
   coal_pswap<1, false>(d);
   coal_pswap<2, true>(d);
-  coal_bswap<4, 1>(d);
-  coal_bswap<8, 2>(d);
 }
 
 // line-per-lane tile loads (round 4's product): the scan of large stores
