@@ -477,9 +477,9 @@ def test_fuzz_adversarial_stores(ctx):
     end, given a junk or b"CORRUPT" tail, bit-flipped (often inside the last
     metadata record) or given a zeroed line -- both passes against the
     oracle's recover_valid_chain / chain / KeyIndexer::build."""
-    rnd = random.Random(2026)
+    rnd = random.Random(int(os.environ.get("SRD_FUZZ_SEED", 2026)))  # (SRD_FUZZ_SEED / SRD_FUZZ_N: longer runs)
     modes = {S.SRD_MODE_OPTIMISTIC: 0, S.SRD_MODE_FULL: 0}
-    for i in range(120):
+    for i in range(int(os.environ.get("SRD_FUZZ_N", 120))):
         store = _fuzz_store(rnd)
         for flags in (0, S.SRD_FLAG_FORCE_FULL):
             r = check_against_oracle(store, ctx, flags, "fuzz%d/%d" % (i, flags))
